@@ -1,0 +1,207 @@
+"""Benchmark: edges/sec of the VQ-GNN per-layer hot path (BASELINE.json metric).
+
+One step = one layer step on a synthetic arxiv-shaped mini-batch:
+  (i)   VQ assign + EMA for all nb branches on the B batch rows — update()
+        semantics (W = 2D: features and gradients), one launch sequence
+        (BN stats -> BN finalize -> MFMA assign + fused EMA statistics ->
+        EMA finalize), c_indices scattered in place;
+  (ii)  codebook-code gather for the B' out-of-batch rows;
+  (iii) fused codebook-gather + CSR SpMM over all nnz edges, all n rows.
+value = edges of all ranks / time.  Inputs are resident in HBM before timing.
+
+Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
+torch.distributed.run (one rank per GPU, RCCL); each rank takes its own batch
+of the same graph (weak scaling) and ranks keep one codebook via an RCCL
+all-reduce of the sufficient statistics and an all-gather of the codes.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--config", default="arxiv_gcn")
+    p.add_argument("--semantics", default="update", choices=["update", "feature_update"])
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
+    return p.parse_args()
+
+
+def main():
+    args = parse()
+    import torch.distributed as dist
+    import vqgnn_pkg
+    vqgnn_pkg.load()
+    from vq_gnn_amd import kernels
+    from vq_gnn_amd.graph import CONFIGS, batch_to_device, make_batch, synthetic_graph
+    from vq_gnn_amd.vq import VQBank
+    import vq_gnn_amd.vq as vqmod
+
+    vqmod.STRICT_BAD_INIT = False   # 'Bad Init!' flag checked after the timed region
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    comm = None
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+        from vq_gnn_amd.dist import CodebookSync
+        comm = CodebookSync(count_group=dist.new_group(backend="gloo"))
+
+    cfg = CONFIGS[args.config]
+    g = synthetic_graph(cfg["N"], cfg["parts"], cfg["edges"], seed=cfg.get("seed", 0))
+    _, _, batch = make_batch(cfg, rank=rank, graph=g)
+    B, n, nnz = batch.B, batch.n, batch.nnz
+    F, M, D = cfg["F"], cfg["M"], 4
+    nb = F // D
+    W = 2 * D if args.semantics == "update" else D
+
+    gen = torch.Generator().manual_seed(1)
+    X = torch.randn(B, F, generator=gen)
+    G = torch.randn(B, F, generator=torch.Generator().manual_seed(2)) * 1e-3
+    codes0 = torch.randint(0, M, (g.N, nb), dtype=torch.int16,
+                           generator=torch.Generator().manual_seed(5))
+    torch.manual_seed(0)
+    bank = VQBank(nb, M, D, warm_up_flag=True)
+    for b in range(nb):
+        bank.init_branch(b)
+    bank = bank.to(dev)
+    Xd, Gd = X.to(dev), G.to(dev)
+    codes = codes0.to(dev)
+    bidx, subset, adj = batch_to_device(batch, dev)
+    if comm is not None:
+        bank.comm = comm
+        tot = comm.global_count(B)
+        comm.cache_count(B, tot)
+        bank.comm_max_B = comm.global_max(B)
+    # codebook state = one feature_update warm pass
+    bank.feature_update(Xd, 0, nb, True, codes=codes, batch_idx=bidx)
+    torch.cuda.synchronize()
+
+    ev = []
+
+    def step(record):
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if record else None
+        if record:
+            e[0].record()
+        if W == 2 * D:
+            bank.update(Xd, Gd, 0, nb, True, codes=codes, batch_idx=bidx)
+        else:
+            bank.feature_update(Xd, 0, nb, True, codes=codes, batch_idx=bidx)
+        if record:
+            e[1].record()
+        lcodes = kernels.gather_codes(subset, B, codes)
+        if record:
+            e[2].record()
+        kernels.spmm(adj.rowptr, adj.col, adj.value, n, nnz, Xd, F, B=B, D=D, lcodes=lcodes,
+                     emb_out=bank.emb_out)
+        if record:
+            e[3].record()
+            ev.append(e)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize()
+    barrier()
+    t1 = time.perf_counter()
+    torch.cuda.synchronize()
+    bank.check_bad_init()
+
+    dt = t1 - t0
+    tvec = torch.tensor([dt, float(nnz)], dtype=torch.float64, device=dev)
+    if world > 1:
+        tmax = tvec[:1].clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        edges = tvec[1:].clone()
+        dist.all_reduce(edges, op=dist.ReduceOp.SUM)
+        dt, total_edges = float(tmax.item()), float(edges.item())
+    else:
+        total_edges = float(nnz)
+    ms_step = dt / args.steps * 1e3
+    value = total_edges * args.steps / dt
+
+    vq_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
+    gather_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in ev]))
+    spmm_ms = float(np.mean([e[2].elapsed_time(e[3]) for e in ev]))
+
+    spmm_bytes = 4 * (n + 1) + 8 * nnz + 4 * B * F + 2 * (n - B) * nb + 4 * nb * M * D + 4 * n * F
+    vq_flops = 2.0 * B * M * W * nb
+    rl_spmm = dict(kernel="spmm_merge_kernel (+fixup)", bound="hbm",
+                   achieved=spmm_bytes / (spmm_ms * 1e-3) / 1e9, peak=8000.0, unit="GB/s",
+                   bytes_per_launch=spmm_bytes, ms_per_launch=spmm_ms)
+    rl_spmm["frac"] = rl_spmm["achieved"] / rl_spmm["peak"]
+    rl_vq = dict(kernel="vq step (bn_stats+finalize+assign+ema)", bound="mfma",
+                 achieved=vq_flops / (vq_ms * 1e-3) / 1e12, peak=157.3, unit="TFLOP/s",
+                 flops_per_launch=vq_flops, ms_per_launch=vq_ms)
+    rl_vq["frac"] = rl_vq["achieved"] / rl_vq["peak"]
+    dominant = rl_spmm if spmm_ms >= vq_ms else rl_vq
+    traffic = None
+    if os.path.exists(args.pmc_json):
+        try:
+            pm = json.load(open(args.pmc_json))
+            if pm.get("config") == args.config:
+                traffic = pm.get("hbm_bytes_per_launch", {}).get(
+                    "spmm" if dominant is rl_spmm else "vq")
+        except Exception:
+            traffic = None
+    roofline = dict(bound=dominant["bound"], achieved=dominant["achieved"], peak=dominant["peak"],
+                    unit=dominant["unit"], frac=dominant["frac"], traffic=traffic,
+                    kernel=dominant["kernel"])
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle.cpu_baseline import layer_step_timer
+        threads = min(16, os.cpu_count() or 1)
+        t_cpu, nsteps = layer_step_timer(X, G, batch, codes0, M, D, threads,
+                                         max_seconds=args.cpu_seconds)
+        cpu = dict(value=nnz / t_cpu, unit="edges/s", cores=threads, kind="port",
+                   sample=f"full {args.config} layer step (update semantics, {nb} branches, "
+                          f"B={B}, nnz={nnz}), median of {nsteps} steps after 1 warm-up; "
+                          f"oracle/cpu_baseline.py, torch {torch.__version__} CPU")
+
+    if rank == 0:
+        out = dict(
+            metric="edges/sec (VQ-assign + aggregate) on arxiv-shaped GCN, 1/2/4/8 MI355X",
+            value=value, unit="edges/s", n_gpus=world, steps=args.steps, warmup=args.warmup,
+            ms_per_step=ms_step, higher_is_better=True, scaling="weak", vs_baseline=None,
+            dtype="f32", data="synthetic (seeded arxiv-shaped graph, random features)",
+            config=dict(workload=f"{args.config}: one layer step (VQ {args.semantics} + EMA for "
+                                 f"{nb} branches, code gather, fused gather-SpMM)",
+                        B=B, B_prime=n - B, nnz=nnz, F=F, M=M, D=D, W=W,
+                        parallelism=f"dp{world}"),
+            roofline=roofline,
+            kernels=dict(vq_ms=vq_ms, gather_ms=gather_ms, spmm_ms=spmm_ms,
+                         spmm=rl_spmm, vq=rl_vq),
+            cpu_baseline=cpu,
+        )
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

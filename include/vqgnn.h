@@ -1,0 +1,172 @@
+/*
+ * vqgnn.h — C-ABI of the MI355X-native VQ-GNN per-layer hot path.
+ *
+ * The reference (devnkong/VQ-GNN, vq_gnn_v2) is pure Python: its hot path is
+ * VectorQuantizerEMA (vq.py), the codebook gather in LowRankGNNLayer.forward
+ * (models.py:157-177) and the sparse aggregation OurGCNConv / OurGATConv
+ * (convs.py), whose arithmetic runs in third-party kernels (ATen, torch_sparse
+ * spmm_sum, torch_scatter segment_csr).  Each entry point below replaces one
+ * of those steps; the comment on each cites the reference line(s) it replaces.
+ * The Python host layer (vq-gnn_amd/vq.py, convs.py, models.py) keeps the
+ * reference's module API and calls these functions through ctypes; the
+ * bindings a maintainer would add on the reference side are in INTEGRATION.md.
+ *
+ * Conventions
+ *  - All pointers are DEVICE pointers (HBM) unless stated otherwise; every call
+ *    is asynchronous on the given stream (a hipStream_t passed as void*; NULL =
+ *    the legacy default stream).  Nothing here synchronises the device.
+ *  - The library never allocates.  Functions that need scratch space take a
+ *    workspace pointer whose size is returned by the matching *_workspace()
+ *    function (host-only arithmetic, no device access).
+ *  - Return value: 0 (VQGNN_OK) or a vqgnn_status code; the message of the
+ *    last failure on the calling thread is returned by vqgnn_last_error().
+ *  - Reentrant, no global mutable state: calls may come from any host thread
+ *    (e.g. the autograd engine's device thread during backward).
+ *  - Index types: CSR rowptr/col are int32 (nnz < 2^31); node ids int64 as in
+ *    the reference (subset / batch_idx are LongTensors); codeword codes int16
+ *    as the reference's c_indices buffer (models.py:27).
+ */
+#ifndef VQGNN_H
+#define VQGNN_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* vqgnn_stream_t;
+
+enum vqgnn_status {
+  VQGNN_OK = 0,
+  VQGNN_ERR_INVALID = 1,     /* bad argument (shape, null pointer, alignment) */
+  VQGNN_ERR_LAUNCH = 2,      /* hipLaunch / hipMemsetAsync failure           */
+  VQGNN_ERR_UNSUPPORTED = 3  /* shape outside what the kernels implement     */
+};
+
+/* Thread-local text of the last error on this thread ("" if none). */
+const char* vqgnn_last_error(void);
+/* ABI version (major*100 + minor). */
+int vqgnn_version(void);
+
+/* ------------------------------------------------------------------------ *
+ * 1. BatchNorm1d sufficient statistics of the VQ inputs.
+ *    Replaces the batch-stat half of BatchNorm1d(train) in
+ *    vq.py:162 (feature_update) and vq.py:208-223 (update).
+ *    Columns: F = nb*D feature columns of X, and (with_grad) F columns of G.
+ *    sums[4][F] (fp64): sum x, sum x^2, sum g, sum g^2 over the B rows.
+ *    These are the quantities a multi-GPU caller all-reduces.
+ * ------------------------------------------------------------------------ */
+size_t vqgnn_bn_stats_workspace(int32_t B, int32_t F);
+int vqgnn_bn_stats(const float* X, int64_t ldx, const float* G, int64_t ldg,
+                   int32_t B, int32_t F, int32_t with_grad,
+                   double* sums, void* workspace, vqgnn_stream_t stream);
+
+/* 2. BatchNorm finalize: batch mean/var -> per-column affine normalisation
+ *    coefficients (alpha = invstd, beta = -mean*invstd, as ATen's CPU
+ *    batch_norm computes them) and the running-stat EMA update.
+ *    Replaces BatchNorm1d.forward's stat update (vq.py:162, :223) and the
+ *    first-call running-stat initialisation of update() (vq.py:216-221).
+ *    mode: 0 = eval (coefficients from running stats, no update)
+ *          1 = train (batch stats, running stats updated with momentum)
+ *          2 = train + init_from_batch (vq.py:216-221, then as 1)
+ *          3 = eval  + init_from_batch (vq.py:216-221, then as 0)
+ *    count = rows over all ranks.  coef[4][F]: alpha_f, beta_f, alpha_g, beta_g.
+ *    batch_out[4][F] (optional, may be NULL): mean_f, std_f, mean_g, std_g with
+ *    std = sqrt(unbiased var + eps_std) (vq.py:208-211 logging stash).         */
+int vqgnn_bn_finalize(const double* sums, int64_t count, int32_t F, int32_t with_grad,
+                      int32_t mode, float momentum_f, float eps_f,
+                      float momentum_g, float eps_g, float eps_std,
+                      float* rm_f, float* rv_f, float* rm_g, float* rv_g,
+                      float* coef, float* batch_out, vqgnn_stream_t stream);
+
+/* ------------------------------------------------------------------------ *
+ * 3. Product-quantised nearest-codeword assignment for nb branches at once,
+ *    plus (ema_stats != NULL) the EMA sufficient statistics.
+ *    Replaces, per branch b, vq.py:166-173 (feature_update, W = D) or
+ *    vq.py:223-238 (update, W = 2D): normalise, d = (|x|^2 + |e|^2) - 2 x.e,
+ *    argmin (first index on ties), and the one-hot reductions of
+ *    vq.py:177-178/191 and :242-243/256 (counts, encodings^T @ x_norm).
+ *    Branch b reads X[:, b*D:(b+1)*D] (and G[:, b*D:(b+1)*D] when W = 2D).
+ *    embedding: [nb][M][ldw] (vq._embedding, ldw = 2D), branch stride
+ *    emb_bstride floats.  coef: output of vqgnn_bn_finalize.
+ *    Outputs (each optional):
+ *      idx_out   [nb][B] int64   — encoding_indices per branch
+ *      codes     [*][ldc] int16  — codes[batch_idx[i]][b] = idx (models.py:63/46)
+ *      ema_stats [nb][M][W+1] fp32 — count, then sum of normalised x per codeword
+ * ------------------------------------------------------------------------ */
+size_t vqgnn_vq_assign_workspace(int32_t B, int32_t nb, int32_t M, int32_t W);
+int vqgnn_vq_assign(const float* X, int64_t ldx, const float* G, int64_t ldg,
+                    int32_t B, int32_t nb, int32_t D, int32_t M, int32_t W,
+                    const float* coef, float grad_scale,
+                    const float* embedding, int32_t ldw, int64_t emb_bstride,
+                    int64_t* idx_out, int16_t* codes, int64_t ldc,
+                    const int64_t* batch_idx, float* ema_stats,
+                    void* workspace, vqgnn_stream_t stream);
+
+/* 4. EMA codebook finalize for nb branches (vq.py:177-200 / :242-277):
+ *    cluster size EMA, Laplace smoothing (laplace != 0, vq.py:182-186),
+ *    'Bad Init!' detection (*bad_init |= 1, vq.py:188), ema_w EMA, embedding =
+ *    ema_w / cs, and the de-normalised _embedding_output.  W = D updates the
+ *    feature half only (feature_update); W = 2D all columns (update).
+ *    Running stats (rm_f, rv_f, rm_g, rv_g) are [nb][D].  Per-branch arrays use strides
+ *    cs_bstride (cluster_size) and emb_bstride (ema_w, embedding, output).   */
+int vqgnn_vq_ema_finalize(const float* ema_stats, int32_t nb, int32_t M,
+                          int32_t D, int32_t W, int32_t ldw,
+                          float decay, int32_t laplace, float grad_scale, float epsilon,
+                          float* cluster_size, int64_t cs_bstride,
+                          float* ema_w, float* embedding, float* embedding_output,
+                          int64_t emb_bstride,
+                          const float* rm_f, const float* rv_f,
+                          const float* rm_g, const float* rv_g,
+                          int32_t* bad_init, vqgnn_stream_t stream);
+
+/* ------------------------------------------------------------------------ *
+ * 5. Out-of-batch code gather (models.py:158, :168): for j in [0, n-B),
+ *    lcodes[j][b] = codes[subset[B+j]][b], b < nb.
+ * ------------------------------------------------------------------------ */
+int vqgnn_gather_codes(const int64_t* subset, int32_t B, int32_t n,
+                       const int16_t* codes, int64_t ldc, int32_t nb,
+                       int16_t* lcodes, vqgnn_stream_t stream);
+
+/* 5b. Code scatter (models.py:63 / :46 across ranks): for i in [0, B),
+ *     codes[batch_idx[i]][b] = local[i][b].  Multi-GPU callers all-gather the
+ *     (batch_idx, local codes) of every rank and scatter them with this so all
+ *     replicas' c_indices stay identical.                                     */
+int vqgnn_scatter_codes(const int64_t* batch_idx, int32_t B, const int16_t* local,
+                        int32_t nb, int16_t* codes, int64_t ldc, vqgnn_stream_t stream);
+
+/* 6. Fused codebook-gather + CSR SpMM (sum):
+ *      out[i][:] = sum_{e in row i} val[e] * xin[col[e]][:]
+ *    with xin[j] = X[j] for j < B, and for j >= B the concatenation over
+ *    branches of embedding_output[b][lcodes[j-B][b]][0:D] (models.py:168-179
+ *    -> convs.py:95 -> torch_sparse spmm_sum).  Rows are summed in CSR order
+ *    (mul then add, as spmm_sum), except rows longer than one edge chunk, whose
+ *    chunk partials are added in chunk order.  lcodes == NULL (or B >= n_cols)
+ *    gives a plain SpMM with a dense right-hand side — the transpose product
+ *    of the backward pass.  F must be a multiple of 4, D a multiple of 4 or
+ *    lcodes NULL.  out: [n_rows][ldo].                                        */
+size_t vqgnn_spmm_workspace(int32_t n_rows, int64_t nnz, int32_t F);
+int vqgnn_spmm(const int32_t* rowptr, const int32_t* col, const float* val,
+               int32_t n_rows, int64_t nnz, int32_t B,
+               const float* X, int64_t ldx, int32_t F, int32_t D,
+               const int16_t* lcodes, int32_t nb,
+               const float* emb_out, int32_t ldw, int64_t emb_bstride,
+               float* out, int64_t ldo, void* workspace, vqgnn_stream_t stream);
+
+/* 7. CSR transpose (structure + values) for the backward product
+ *    dX = A^T dOut (torch_sparse matmul autograd, convs.py:95).  Output CSR of
+ *    A^T with rows sorted by column of A; within a row, entries ordered by
+ *    row of A (canonical, deterministic).                                     */
+size_t vqgnn_csr_transpose_workspace(int32_t n_rows, int32_t n_cols, int64_t nnz);
+int vqgnn_csr_transpose(const int32_t* rowptr, const int32_t* col, const float* val,
+                        int32_t n_rows, int32_t n_cols, int64_t nnz,
+                        int32_t* t_rowptr, int32_t* t_col, float* t_val,
+                        void* workspace, vqgnn_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* VQGNN_H */

@@ -1,0 +1,60 @@
+"""Shared test helpers (golden loading, tie-aware index comparison)."""
+import ast
+import glob
+import os
+
+import numpy as np
+import torch
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+STATE_KEYS = ("embedding", "embedding_output", "ema_cluster_size", "ema_w",
+              "rm_f", "rv_f", "rm_g", "rv_g")
+
+
+def golden_cases():
+    return sorted(os.path.basename(p)[3:-4] for p in glob.glob(os.path.join(GOLDEN, "vq_*.npz")))
+
+
+def load_case(name):
+    z = np.load(os.path.join(GOLDEN, f"vq_{name}.npz"), allow_pickle=False)
+    meta = ast.literal_eval(str(z["meta"]))
+    calls = []
+    for c in range(meta["calls"]):
+        p = f"c{c}_"
+        if p + "X" not in z:
+            break
+        rec = dict(X=torch.from_numpy(z[p + "X"]), G=torch.from_numpy(z[p + "G"]),
+                   idx=torch.from_numpy(z[p + "idx"]), error=str(z[p + "error"]),
+                   bn_inited_pre=bool(z[p + "bn_inited_pre"]),
+                   pre={k: torch.from_numpy(z[p + "pre_" + k]) for k in STATE_KEYS},
+                   post={k: torch.from_numpy(z[p + "post_" + k]) for k in STATE_KEYS})
+        logs = {k[len(p) + 4:]: torch.from_numpy(z[k]) for k in z.files if k.startswith(p + "log_")}
+        rec["logs"] = logs
+        calls.append(rec)
+    return meta, calls
+
+
+def oracle_state_from(meta, pre, bn_inited):
+    st = dict(M=meta["M"], D=meta["D"], decay=0.99, epsilon=1e-24,
+              grad_scale=list(meta["grad_scale"]), warm_up=meta["warm_up"],
+              momentum=meta["momentum"], bn_inited=bn_inited)
+    for k in STATE_KEYS:
+        st[k] = pre[k].clone()
+    return st
+
+
+def tie_aware_mismatch(idx_a, idx_b, dist, rel=1e-5):
+    """Rows where idx_a != idx_b; returns (n_mismatch, n_unexplained) where a
+    mismatch is explained when the two candidates' distances (under the
+    oracle's own distances ``dist`` [B, M]) are within rel of the scale."""
+    idx_a = torch.as_tensor(idx_a).long().view(-1)
+    idx_b = torch.as_tensor(idx_b).long().view(-1)
+    bad = torch.nonzero(idx_a != idx_b).view(-1)
+    if bad.numel() == 0:
+        return 0, 0
+    da = dist[bad, idx_a[bad]].double()
+    db = dist[bad, idx_b[bad]].double()
+    scale = 1.0 + dist[bad].abs().max(dim=1).values.double()
+    unexplained = int(((da - db).abs() > rel * scale).sum())
+    return int(bad.numel()), unexplained

@@ -1,0 +1,49 @@
+"""The C-ABI library builds, loads and exports every symbol of include/vqgnn.h
+(no compute calls: no GPU here)."""
+import os
+import re
+
+import vq_gnn_amd._lib as L
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    text = open(os.path.join(ROOT, "include", "vqgnn.h")).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(vqgnn_\w+)\s*\(", text)))
+
+
+def test_library_exports_header_symbols():
+    h = L.lib()
+    syms = header_symbols()
+    assert len(syms) >= 14
+    for s in syms:
+        assert hasattr(h, s), f"missing export {s}"
+        assert s in L.SIGNATURES, f"no ctypes signature for {s}"
+    assert set(L.SIGNATURES) == set(syms)
+
+
+def test_version_and_error_text():
+    h = L.lib()
+    assert h.vqgnn_version() >= 100
+    assert h.vqgnn_last_error() == b""
+
+
+def test_host_only_workspace_queries():
+    h = L.lib()
+    assert h.vqgnn_bn_stats_workspace(84670, 128) > 0
+    assert h.vqgnn_vq_assign_workspace(84670, 32, 256, 8) >= 32 * 256 * 9 * 4
+    assert h.vqgnn_spmm_workspace(128000, 2_000_000, 128) > 0
+
+
+def test_invalid_arguments_rejected_without_device():
+    # argument validation happens before any launch
+    h = L.lib()
+    rc = h.vqgnn_vq_assign(None, 0, None, 0, 10, 1, 4, 16, 6, None, 1.0, None, 8, 128,
+                           None, None, 0, None, None, None, None)
+    assert rc == 1
+    assert b"null" in h.vqgnn_last_error() or b"W" in h.vqgnn_last_error()
+    rc = h.vqgnn_spmm(None, None, None, 4, 0, 0, None, 4, 6, 4, None, 0, None, 0, 0, None, 4,
+                      None, None)
+    assert rc == 1 and b"null" in h.vqgnn_last_error()

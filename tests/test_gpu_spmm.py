@@ -1,0 +1,151 @@
+"""GPU parity of the fused gather-SpMM, code gather and CSR transpose."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import conv_ref
+from vq_gnn_amd import graph, kernels
+from vq_gnn_amd.sparse import CSR
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+
+def _dev_csr(rowptr, col, val, n_rows, n_cols):
+    return CSR(torch.as_tensor(np.asarray(rowptr)), torch.as_tensor(np.asarray(col)),
+               torch.as_tensor(np.asarray(val, dtype=np.float32)), (n_rows, n_cols)).to(DEV)
+
+
+def _random_csr(n_rows, n_cols, deg_max, rng, hub_rows=(), hub_deg=0, empty_frac=0.1):
+    deg = rng.integers(0, deg_max + 1, size=n_rows)
+    deg[rng.random(n_rows) < empty_frac] = 0
+    for h in hub_rows:
+        deg[h] = hub_deg
+    rowptr = np.zeros(n_rows + 1, np.int64)
+    rowptr[1:] = np.cumsum(deg)
+    col = np.concatenate([np.sort(rng.choice(n_cols, size=d, replace=d > n_cols))
+                          for d in deg]) if rowptr[-1] else np.zeros(0, np.int64)
+    val = rng.standard_normal(col.shape[0]).astype(np.float32)
+    return rowptr, col.astype(np.int64), val
+
+
+@pytest.mark.parametrize("F", [4, 16, 32, 64, 128, 256, 604, 1024])
+def test_spmm_bit_exact_short_rows(F):
+    """Rows inside one edge chunk are summed in CSR order with mul+add ->
+    bit-identical to torch_sparse spmm_sum's CPU loop."""
+    rng = np.random.default_rng(F)
+    rowptr, col, val = _random_csr(700, 500, 12, rng)
+    x = rng.standard_normal((500, F)).astype(np.float32)
+    a = _dev_csr(rowptr, col, val, 700, 500)
+    out = kernels.spmm(a.rowptr, a.col, a.value, 700, a.nnz(), torch.from_numpy(x).to(DEV), F)
+    ref = conv_ref.spmm_seq(rowptr, col, val, x)
+    deg = np.diff(rowptr)
+    S = 128 if F <= 128 else 64
+    inside = (rowptr[:-1] // S == np.maximum(rowptr[1:] - 1, rowptr[:-1]) // S)
+    o = out.cpu().numpy()
+    assert np.array_equal(o[inside], ref[inside])
+    np.testing.assert_allclose(o, ref, rtol=1e-5, atol=1e-5)
+    assert np.all(o[deg == 0] == 0)
+
+
+def test_spmm_hub_rows_span_chunks():
+    rng = np.random.default_rng(1)
+    rowptr, col, val = _random_csr(3000, 4000, 20, rng, hub_rows=(5, 1700, 2999), hub_deg=3900)
+    x = rng.standard_normal((4000, 128)).astype(np.float32)
+    a = _dev_csr(rowptr, col, val, 3000, 4000)
+    out = kernels.spmm(a.rowptr, a.col, a.value, 3000, a.nnz(), torch.from_numpy(x).to(DEV), 128)
+    ref = conv_ref.spmm_fp64(rowptr, col, val, x)
+    scale = conv_ref.spmm_fp64(rowptr, col, np.abs(val), np.abs(x)) + 1e-6
+    assert np.max(np.abs(out.cpu().numpy() - ref) / scale) < 1e-5
+
+
+def test_spmm_empty_and_degenerate():
+    x = torch.randn(10, 8, device=DEV)
+    a = _dev_csr([0, 0, 0, 0], [], [], 3, 10)
+    out = kernels.spmm(a.rowptr, a.col, a.value, 3, 0, x, 8)
+    assert torch.count_nonzero(out) == 0
+    # trailing empty rows + leading empty rows
+    rowptr = [0, 0, 2, 2, 3, 3, 3]
+    a = _dev_csr(rowptr, [1, 4, 9], [1.0, 2.0, 3.0], 6, 10)
+    out = kernels.spmm(a.rowptr, a.col, a.value, 6, 3, x, 8).cpu()
+    xc = x.cpu()
+    exp = torch.zeros(6, 8)
+    exp[1] = 1.0 * xc[1] + 2.0 * xc[4]
+    exp[3] = 3.0 * xc[9]
+    assert torch.equal(out, exp)
+
+
+@pytest.mark.parametrize("F,D", [(128, 4), (32, 4), (256, 4), (64, 8)])
+def test_fused_gather_spmm_vs_oracle(F, D):
+    g = graph.synthetic_graph(4000, 8, 20000, seed=F + D)
+    rp, cl, vl = graph.norm_adj(g, "GCN")
+    b = graph.k_hop_batch(rp, cl, vl, g.N, graph.cluster_batch(g, [0, 2, 5]))
+    nb, M = F // D, 50
+    rng = np.random.default_rng(0)
+    X = rng.standard_normal((b.B, F)).astype(np.float32)
+    emb_out = rng.standard_normal((nb, M, 2 * D)).astype(np.float32)
+    codes = rng.integers(0, M, size=(g.N, nb)).astype(np.int16)
+    bidx, subset, adj = graph.batch_to_device(b, DEV)
+    codes_d = torch.from_numpy(codes).to(DEV)
+    lcodes = kernels.gather_codes(subset, b.B, codes_d)
+    assert torch.equal(lcodes.cpu(), torch.from_numpy(codes[b.subset[b.B:]]))
+    out = kernels.spmm(adj.rowptr, adj.col, adj.value, b.n, b.nnz, torch.from_numpy(X).to(DEV),
+                       F, B=b.B, D=D, lcodes=lcodes, emb_out=torch.from_numpy(emb_out).to(DEV))
+    xin = conv_ref.gather_input(X, b.subset, b.B, codes, emb_out, D).numpy()
+    ref = conv_ref.spmm_seq(b.rowptr, b.col, b.val, xin)
+    np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=1e-5, atol=1e-6)
+    S = 128 if F <= 128 else 64
+    rp_ = b.rowptr
+    inside = (rp_[:-1] // S == np.maximum(rp_[1:] - 1, rp_[:-1]) // S)
+    assert np.array_equal(out.cpu().numpy()[inside], ref[inside])
+
+
+def test_scatter_codes():
+    N, nb, B = 100, 5, 30
+    codes = torch.zeros(N, nb, dtype=torch.int16, device=DEV)
+    bidx = torch.randperm(N)[:B].to(DEV)
+    local = torch.randint(0, 99, (B, nb), dtype=torch.int16, device=DEV)
+    pad = torch.cat([bidx, torch.full((4,), -1, device=DEV)])
+    lpad = torch.cat([local, torch.zeros(4, nb, dtype=torch.int16, device=DEV)])
+    kernels.scatter_codes(pad, lpad, codes)
+    assert torch.equal(codes[bidx], local)
+    mask = torch.ones(N, dtype=torch.bool, device=DEV)
+    mask[bidx] = False
+    assert int(codes[mask].abs().sum()) == 0
+
+
+@pytest.mark.parametrize("n_rows,n_cols", [(500, 700), (1, 9), (300, 300)])
+def test_csr_transpose_and_backward_product(n_rows, n_cols):
+    rng = np.random.default_rng(n_rows)
+    rowptr, col, val = _random_csr(n_rows, n_cols, 15, rng, hub_rows=(0,), hub_deg=min(n_cols, 400))
+    a = _dev_csr(rowptr, col, val, n_rows, n_cols)
+    t = a.transposed()
+    r = np.repeat(np.arange(n_rows), np.diff(rowptr))
+    order = np.lexsort((r, col))
+    exp_ptr = np.zeros(n_cols + 1, np.int64)
+    exp_ptr[1:] = np.cumsum(np.bincount(col, minlength=n_cols))
+    assert np.array_equal(t.rowptr.cpu().numpy(), exp_ptr)
+    assert np.array_equal(t.col.cpu().numpy(), r[order])
+    assert np.array_equal(t.value.cpu().numpy(), val[order])
+    d = rng.standard_normal((n_rows, 16)).astype(np.float32)
+    dx = kernels.spmm(t.rowptr, t.col, t.value, n_cols, t.nnz(), torch.from_numpy(d).to(DEV), 16)
+    exp = np.zeros((n_cols, 16))
+    np.add.at(exp, col, val[:, None].astype(np.float64) * d[r])
+    np.testing.assert_allclose(dx.cpu().numpy(), exp, rtol=1e-4, atol=1e-5)
+
+
+def test_arxiv_shaped_properties():
+    """Full arxiv-shaped batch: SpMM vs fp64 (size-independent bound) and
+    linearity out(a x + y) = a out(x) + out(y) to fp32 rounding."""
+    cfg = graph.CONFIGS["arxiv_gcn"]
+    g, _, b = graph.make_batch(cfg)
+    bidx, subset, adj = graph.batch_to_device(b, DEV)
+    F = 128
+    x = torch.randn(b.n, F, device=DEV)
+    y = torch.randn(b.n, F, device=DEV)
+    ox = kernels.spmm(adj.rowptr, adj.col, adj.value, b.n, b.nnz, x, F)
+    oy = kernels.spmm(adj.rowptr, adj.col, adj.value, b.n, b.nnz, y, F)
+    oxy = kernels.spmm(adj.rowptr, adj.col, adj.value, b.n, b.nnz, 2 * x + y, F)
+    torch.testing.assert_close(oxy, 2 * ox + oy, rtol=1e-4, atol=1e-4)
+    ref = conv_ref.spmm_fp64(b.rowptr, b.col, b.val, x.cpu().numpy())
+    assert np.abs(ox.cpu().numpy() - ref).max() < 1e-4

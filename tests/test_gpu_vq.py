@@ -1,0 +1,186 @@
+"""GPU parity of the VQ kernels (HIP, via the C-ABI) against the oracle and the
+reference's golden vectors."""
+import pytest
+import torch
+
+from helpers import (STATE_KEYS, golden_cases, load_case, oracle_state_from,
+                     tie_aware_mismatch)
+from oracle import vq_ref
+from vq_gnn_amd import kernels
+from vq_gnn_amd.vq import VQBank, VectorQuantizerEMA
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+
+def _coef_tensor(alpha_f, beta_f, alpha_g=None, beta_g=None):
+    F = alpha_f.numel()
+    c = torch.zeros(4, F)
+    c[0], c[1] = alpha_f, beta_f
+    if alpha_g is not None:
+        c[2], c[3] = alpha_g, beta_g
+    return c.to(DEV)
+
+
+@pytest.mark.parametrize("M,D,W,B,tie", [
+    (256, 4, 8, 3000, False), (256, 4, 4, 3000, False), (37, 4, 8, 1000, False),
+    (1030, 4, 8, 2100, False), (4096, 4, 8, 1500, False), (64, 4, 8, 999, True),
+    (128, 2, 4, 777, False), (64, 2, 2, 513, False), (16, 8, 16, 300, False),
+    (5000, 4, 4, 700, False)])
+def test_assign_bit_exact_given_coefficients(M, D, W, B, tie):
+    """Same normalisation coefficients -> the codeword index is bit-exact
+    (ATen fma BN, sequential |x|^2, MKL K<=8 sgemm == MFMA fma chain)."""
+    g = torch.Generator().manual_seed(M * 7 + B)
+    X = torch.randn(B, D, generator=g) * 2 + 0.5
+    G = torch.randn(B, D, generator=g) * 1e-3
+    emb = torch.randn(M, 2 * D, generator=g)
+    if tie:
+        emb[M // 2:] = emb[: M - M // 2]
+    rmf, rvf = torch.zeros(D), torch.ones(D)
+    af, bf = vq_ref.bn_coefficients(X, True, rmf, rvf, 1e-5)
+    ag, bg = vq_ref.bn_coefficients(G, True, torch.zeros(D), torch.ones(D), 1e-24)
+    scale = 0.75
+    idx_ref, _ = vq_ref.assign_with_coef(X, G if W == 2 * D else None, af, bf, ag, bg, scale, emb)
+    coef = _coef_tensor(af, bf, ag, bg)
+    idx = torch.empty(1, B, dtype=torch.long, device=DEV)
+    stats = kernels.vq_assign(X.to(DEV), G.to(DEV) if W == 2 * D else None, coef, scale,
+                              emb.view(1, M, 2 * D).to(DEV), D, W, idx_out=idx, want_stats=True)
+    assert torch.equal(idx.cpu()[0], idx_ref)
+    # EMA statistics: exact counts, fp32 sums of the normalised rows
+    xn = torch.cat([X * af + bf, ((G * ag + bg) * scale)], 1)[:, :W]
+    cnt = torch.bincount(idx_ref, minlength=M).float()
+    dw = torch.zeros(M, W, dtype=torch.float64).index_add_(0, idx_ref, xn.double())
+    st = stats.cpu()[0]
+    assert torch.equal(st[:, 0], cnt)
+    torch.testing.assert_close(st[:, 1:].double(), dw, rtol=1e-4, atol=1e-4)
+
+
+def test_assign_multibranch_strided_views_and_codes():
+    nb, D, M, B, N = 6, 4, 96, 1200, 5000
+    g = torch.Generator().manual_seed(3)
+    X = torch.randn(B, nb * D + 3, generator=g)[:, 1:1 + nb * D]     # strided view
+    emb = torch.randn(nb, M, 2 * D, generator=g)
+    coef = torch.zeros(4, nb * D)
+    coef[0], coef[1] = 1.3, -0.2
+    batch_idx = torch.randperm(N, generator=g)[:B]
+    codes = torch.full((N, nb + 2), -7, dtype=torch.int16)
+    Xd = X.to(DEV)
+    codes_d = codes.to(DEV)
+    idx = torch.empty(nb, B, dtype=torch.long, device=DEV)
+    kernels.vq_assign(Xd, None, coef.to(DEV), 1.0, emb.to(DEV), D, D, idx_out=idx,
+                      codes=codes_d[:, :nb], batch_idx=batch_idx.to(DEV))
+    for b in range(nb):
+        xb = X[:, b * D:(b + 1) * D]
+        r, _ = vq_ref.assign_with_coef(xb, None, coef[0, :D], coef[1, :D], None, None, 1.0,
+                                       emb[b])
+        assert torch.equal(idx.cpu()[b], r)
+        assert torch.equal(codes_d.cpu()[batch_idx, b].long(), r)
+    assert int((codes_d.cpu()[:, nb:] != -7).sum()) == 0
+
+
+def _bank_from_pre(meta, pre, bn_inited):
+    D, M = meta["D"], meta["M"]
+    bank = VQBank(1, M, D, grad_normalize_scale=list(meta["grad_scale"]),
+                  warm_up_flag=meta["warm_up"], momentum=meta["momentum"]).to(DEV)
+    bank.emb[0].copy_(pre["embedding"])
+    bank.emb_out[0].copy_(pre["embedding_output"])
+    bank.cs[0].copy_(pre["ema_cluster_size"])
+    bank.ema_w[0].copy_(pre["ema_w"])
+    bank.rm_f[0].copy_(pre["rm_f"])
+    bank.rv_f[0].copy_(pre["rv_f"])
+    bank.rm_g[0].copy_(pre["rm_g"])
+    bank.rv_g[0].copy_(pre["rv_g"])
+    bank.bn_inited = [bn_inited]
+    return bank
+
+
+def _bank_state(bank):
+    return dict(embedding=bank.emb[0], embedding_output=bank.emb_out[0],
+                ema_cluster_size=bank.cs[0], ema_w=bank.ema_w[0], rm_f=bank.rm_f[0],
+                rv_f=bank.rv_f[0], rm_g=bank.rm_g[0], rv_g=bank.rv_g[0])
+
+
+@pytest.mark.parametrize("name", golden_cases())
+def test_vq_step_vs_reference_golden(name):
+    """Full feature_update / update on the GPU vs the reference's outputs."""
+    meta, calls = load_case(name)
+    D, M = meta["D"], meta["M"]
+    for c, rec in enumerate(calls):
+        bank = _bank_from_pre(meta, rec["pre"], rec["bn_inited_pre"])
+        B = rec["X"].shape[0]
+        idx = torch.empty(1, B, dtype=torch.long, device=DEV)
+        err = ""
+        try:
+            if meta["op"] == "feature_update":
+                bank.feature_update(rec["X"].to(DEV), 0, 1, meta["training"], idx_out=idx)
+            else:
+                bank.update(rec["X"].to(DEV), rec["G"].to(DEV), 0, 1, meta["training"],
+                            idx_out=idx)
+        except ValueError as e:
+            err = str(e)
+        assert err == rec["error"]
+        if err:
+            return
+        # oracle distances on the reference's own normalisation, for tie-awareness
+        st = oracle_state_from(meta, rec["pre"], rec["bn_inited_pre"])
+        if meta["op"] == "feature_update":
+            xn = torch.nn.functional.batch_norm(rec["X"], st["rm_f"].clone(), st["rv_f"].clone(),
+                                                None, None, meta["training"], 0.1, 1e-5)
+            dist = vq_ref.distances(xn, rec["pre"]["embedding"][:, :D])
+        else:
+            _, _, _ = vq_ref.update(st, rec["X"], rec["G"], meta["training"])
+            dist = None
+        got = idx.cpu()[0]
+        if dist is not None:
+            n_mis, n_bad = tie_aware_mismatch(got, rec["idx"], dist)
+            assert n_bad == 0, f"{name}: {n_mis} mismatches, {n_bad} not near-ties"
+        else:
+            n_mis = int((got != rec["idx"]).sum())
+        assert n_mis <= max(1, B // 500), f"{name}: {n_mis} index mismatches"
+        post = _bank_state(bank)
+        moved = set()
+        if n_mis:
+            moved = set(got[got != rec["idx"]].tolist()) | set(
+                rec["idx"][got != rec["idx"]].tolist())
+        keep = torch.tensor([m not in moved for m in range(M)])
+        for k in STATE_KEYS:
+            a, b = post[k].cpu(), rec["post"][k]
+            if k in ("embedding", "embedding_output", "ema_cluster_size", "ema_w") and n_mis:
+                a, b = a[keep], b[keep]
+            torch.testing.assert_close(a, b, rtol=2e-5, atol=2e-5,
+                                       msg=lambda m: f"{name} call {c} {k}: {m}")
+        if meta["op"] == "update":
+            torch.testing.assert_close(bank.last_batch[0].cpu(), rec["logs"]["mean"][0, :D],
+                                       rtol=1e-5, atol=1e-6)
+            torch.testing.assert_close(bank.last_batch[1].cpu(), rec["logs"]["std"][0, :D],
+                                       rtol=1e-5, atol=1e-6)
+
+
+def test_module_api_update_and_state_dict():
+    torch.manual_seed(0)
+    m = VectorQuantizerEMA(64, 4, grad_normalize_scale=[1, 1], warm_up_flag=True).to(DEV)
+    X = torch.randn(500, 4, device=DEV)
+    G = torch.randn(500, 4, device=DEV) * 1e-3
+    m.train()
+    idx = m.feature_update(X)
+    assert idx.shape == (500, 1) and idx.dtype == torch.long
+    idx2, enc = m.update(X, G)
+    assert enc.shape == (500, 64)
+    assert torch.equal(enc.to_dense().argmax(1).cpu(), idx2[:, 0].cpu())
+    assert m.bn_inited and m.mean.shape == (1, 8) and m.std.shape == (1, 8)
+    assert m.running_std.shape == (1, 8)
+    assert 0 <= float(m.feat_zero_rate) <= 1
+    sd = m.state_dict()
+    for k in ("_embedding", "_embedding_output", "_ema_cluster_size", "_ema_w",
+              "batch_norm_feat.running_mean", "batch_norm_feat.running_var",
+              "batch_norm_grad.running_mean", "batch_norm_grad.num_batches_tracked"):
+        assert k in sd, k
+    assert m.get().shape == (64, 8) and m.get_codebook().shape == (64, 4)
+
+
+def test_bad_init_raises_on_gpu():
+    meta, calls = load_case("fu_bad_init")
+    rec = calls[0]
+    bank = _bank_from_pre(meta, rec["pre"], False)
+    with pytest.raises(ValueError, match="Bad Init!"):
+        bank.feature_update(rec["X"].to(DEV), 0, 1, True)

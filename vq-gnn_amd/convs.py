@@ -1,0 +1,148 @@
+"""Drop-in message-passing convolutions (reference: vq_gnn_v2/convs.py).
+
+``OurGCNConv`` (convs.py:26-101) — used for both GCN and SAGE layers
+(models.py:93-94) — is ``out = A @ x`` over the batch adjacency
+(PyG GCNConv.message_and_aggregate -> torch_sparse.matmul(adj_t, x,
+reduce='add')); no weight, bias or normalisation inside (convs.py:69-99 are
+commented out).  Here the product is the HIP merge-SpMM, and the layer's input
+``x_input = [x ; codewords of B']`` (models.py:168-174) may be passed lazily as
+a ``GatheredInput`` so the [B', F] codeword rows are never materialised.
+"""
+from __future__ import annotations
+
+import math
+from typing import NamedTuple
+
+import torch
+from torch import nn
+
+from . import kernels
+from .sparse import CSR, as_csr
+
+
+class GatheredInput(NamedTuple):
+    """x_input = cat([x, concat_b emb_out[b][lcodes[:, b], :D]]) without the cat.
+
+    x: [B, F] batch rows; lcodes: [n - B, nb] int16 codes of the out-of-batch
+    rows; emb_out: [nb, M, 2D] codebooks (vq._embedding_output of each branch);
+    D: sub-vector width."""
+    x: torch.Tensor
+    lcodes: torch.Tensor
+    emb_out: torch.Tensor
+    D: int
+
+    @property
+    def shape(self):
+        return (self.x.shape[0] + self.lcodes.shape[0], self.x.shape[1])
+
+    def materialize(self):
+        nb = self.lcodes.shape[1]
+        idx = self.lcodes.long()
+        parts = [self.emb_out[b][idx[:, b], :self.D] for b in range(nb)]
+        return torch.cat([self.x, torch.cat(parts, dim=1)])
+
+
+class _VQHook:
+    """Backward-time VQ update (the LowRankGNNBlock.hook of models.py:39-56),
+    applied to all branches of a layer in one batched call."""
+
+    def __init__(self, layer, x_detached, batch_idx):
+        self.layer, self.x, self.batch_idx = layer, x_detached, batch_idx
+
+    def __call__(self, grad_out_B):
+        self.layer._backward_vq_update(self.x, grad_out_B, self.batch_idx)
+
+
+class GatherSpMMFunction(torch.autograd.Function):
+    """out = A @ [x ; codewords]; d/dx = (A^T @ dout)[:B] (x_first_order is a
+    buffer, models.py:169-174, so it receives no gradient)."""
+
+    @staticmethod
+    def forward(ctx, x, adj, lcodes, emb_out, D, hook):
+        B, F = x.shape
+        n = adj.size(0)
+        xc = x if (x.stride(1) == 1 and x.stride(0) % 4 == 0) else x.contiguous()
+        out = kernels.spmm(adj.rowptr, adj.col, adj.value, n, adj.nnz(), xc, F, B=B, D=D,
+                           lcodes=lcodes, emb_out=emb_out)
+        ctx.adj, ctx.B, ctx.hook = adj, B, hook
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        B = ctx.B
+        dout = dout.contiguous()
+        if ctx.hook is not None:
+            ctx.hook(dout[:B])
+        dx = None
+        if ctx.needs_input_grad[0]:
+            at = ctx.adj.transposed()
+            F = dout.shape[1]
+            # rows [0, B) of A^T = columns [0, B) of A; the merge kernel bounds
+            # the walk with the full nnz, so no host read of t_rowptr[B] is needed
+            dx = kernels.spmm(at.rowptr, at.col, at.value, B, at.nnz(), dout, F)
+        return dx, None, None, None, None, None
+
+
+class SpMMFunction(torch.autograd.Function):
+    """out = A @ x for a dense x (the plain OurGCNConv call)."""
+
+    @staticmethod
+    def forward(ctx, x, adj):
+        n_cols, F = x.shape
+        pad = (-F) % 4
+        xc = x.contiguous()
+        if pad:
+            xc = torch.nn.functional.pad(xc, (0, pad))
+        out = kernels.spmm(adj.rowptr, adj.col, adj.value, adj.size(0), adj.nnz(), xc, F + pad)
+        ctx.adj, ctx.pad, ctx.F = adj, pad, F
+        return out[:, :F] if pad else out
+
+    @staticmethod
+    def backward(ctx, dout):
+        at = ctx.adj.transposed()
+        d = dout.contiguous()
+        if ctx.pad:
+            d = torch.nn.functional.pad(d, (0, ctx.pad))
+        dx = kernels.spmm(at.rowptr, at.col, at.value, at.size(0), at.nnz(), d, ctx.F + ctx.pad)
+        return (dx[:, :ctx.F] if ctx.pad else dx), None
+
+
+def _glorot_(t):
+    stdv = math.sqrt(6.0 / (t.size(-2) + t.size(-1)))
+    with torch.no_grad():
+        t.uniform_(-stdv, stdv)
+
+
+class OurGCNConv(nn.Module):
+    """Reference: convs.py:26-101 (subclass of PyG GCNConv with forward =
+    propagate only).  Keeps GCNConv's parameters (``weight`` [in, out] glorot,
+    ``bias`` zeros) so the parameter set and the RNG stream at construction
+    match the reference; both are unused in forward, as in the reference."""
+
+    def __init__(self, in_channels, out_channels, improved=False, cached=False,
+                 add_self_loops=True, normalize=True, bias=True, **kwargs):
+        super().__init__()
+        self.in_channels, self.out_channels = in_channels, out_channels
+        self.improved, self.cached = improved, cached
+        self.add_self_loops, self.normalize = add_self_loops, normalize
+        self.weight = nn.Parameter(torch.empty(in_channels, out_channels))
+        self.bias = nn.Parameter(torch.empty(out_channels)) if bias else None
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        _glorot_(self.weight)
+        if self.bias is not None:
+            with torch.no_grad():
+                self.bias.zero_()
+
+    def forward(self, x, edge_index, edge_weight=None, _hook=None):
+        adj = as_csr(edge_index)
+        if isinstance(x, GatheredInput):
+            return GatherSpMMFunction.apply(x.x, adj, x.lcodes, x.emb_out, x.D, _hook)
+        return SpMMFunction.apply(x, adj)
+
+    def __repr__(self):
+        return f"{self.__class__.__name__}({self.in_channels}, {self.out_channels})"
+
+
+__all__ = ["OurGCNConv", "GatheredInput", "CSR"]

@@ -1,0 +1,146 @@
+"""Thin torch-tensor wrappers over the C-ABI (include/vqgnn.h).
+
+Each function validates shapes on the host, allocates outputs / workspace from
+the PyTorch caching allocator and queues exactly the HIP kernels the C-ABI
+entry point launches, on the current stream.  No function here computes
+anything on the CPU or through ATen math: the arithmetic is in
+csrc/*.hip.
+"""
+from __future__ import annotations
+
+import torch
+
+from ._lib import check, lib, ptr, require_gpu, stream_ptr, workspace
+
+# bn_finalize modes (include/vqgnn.h §2)
+BN_EVAL, BN_TRAIN, BN_TRAIN_INIT, BN_EVAL_INIT = 0, 1, 2, 3
+
+
+def _ld(t: torch.Tensor) -> int:
+    if t.dim() != 2 or t.stride(1) != 1:
+        raise ValueError(f"expected a row-major 2-D view, got shape {tuple(t.shape)} "
+                         f"strides {t.stride()}")
+    return t.stride(0)
+
+
+def bn_stats(X: torch.Tensor, G: torch.Tensor | None, F: int) -> torch.Tensor:
+    """fp64 column sums [4, F]: sum x, sum x^2, sum g, sum g^2 (vq.py:162/223)."""
+    require_gpu(X, "bn_stats")
+    B = X.shape[0]
+    L = lib()
+    ws = workspace(L.vqgnn_bn_stats_workspace(B, F), X.device)
+    sums = torch.empty(4, F, dtype=torch.float64, device=X.device)
+    if G is None:
+        sums[2:].zero_()
+    check(L.vqgnn_bn_stats(ptr(X), _ld(X), ptr(G), _ld(G) if G is not None else 0, B, F,
+                           int(G is not None), ptr(sums), ptr(ws), stream_ptr()), "bn_stats")
+    return sums
+
+
+def bn_finalize(sums, count, F, with_grad, mode, mom_f, eps_f, mom_g, eps_g, eps_std,
+                rm_f, rv_f, rm_g=None, rv_g=None, want_batch=False):
+    """-> (coef [4, F], batch_out [4, F] or None); updates running stats in place."""
+    dev = rm_f.device
+    coef = torch.empty(4, F, dtype=torch.float32, device=dev)
+    if not with_grad:
+        coef[2:].zero_()
+    batch = torch.empty(4, F, dtype=torch.float32, device=dev) if want_batch else None
+    check(lib().vqgnn_bn_finalize(ptr(sums), int(count), F, int(with_grad), int(mode),
+                                  float(mom_f), float(eps_f), float(mom_g), float(eps_g),
+                                  float(eps_std), ptr(rm_f), ptr(rv_f), ptr(rm_g), ptr(rv_g),
+                                  ptr(coef), ptr(batch), stream_ptr()), "bn_finalize")
+    return coef, batch
+
+
+def vq_assign(X, G, coef, grad_scale, emb, D, W, idx_out=None, codes=None, batch_idx=None,
+              want_stats=False):
+    """Nearest codeword for every (row, branch); optional EMA statistics.
+
+    emb: [nb, M, ldw] view (row-major per branch, arbitrary branch stride).
+    Returns ema_stats [nb, M, W+1] (float32) if want_stats else None."""
+    require_gpu(X, "vq_assign")
+    B = X.shape[0]
+    nb, M, ldw = emb.shape
+    if emb.stride(2) != 1 or emb.stride(1) != ldw:
+        raise ValueError("codebook must be row-major per branch")
+    L = lib()
+    stats = None
+    ws = None
+    if want_stats:
+        stats = torch.empty(nb, M, W + 1, dtype=torch.float32, device=X.device)
+        ws = workspace(L.vqgnn_vq_assign_workspace(B, nb, M, W), X.device)
+    ldc = 0
+    if codes is not None:
+        if codes.dtype != torch.int16 or codes.stride(1) != 1:
+            raise ValueError("codes must be an int16 [N, ldc] row-major view")
+        ldc = codes.stride(0)
+    check(L.vqgnn_vq_assign(ptr(X), _ld(X), ptr(G), _ld(G) if G is not None else 0, B, nb, D,
+                            M, W, ptr(coef), float(grad_scale), ptr(emb), ldw, emb.stride(0),
+                            ptr(idx_out), ptr(codes), ldc, ptr(batch_idx), ptr(stats), ptr(ws),
+                            stream_ptr()), "vq_assign")
+    return stats
+
+
+def vq_ema_finalize(stats, D, W, decay, laplace, grad_scale, epsilon, cs, ema_w, emb, emb_out,
+                    rm_f, rv_f, rm_g, rv_g, bad_flag):
+    nb, M, _ = stats.shape
+    ldw = emb.shape[2]
+    if not (ema_w.stride() == emb.stride() == emb_out.stride()):
+        raise ValueError("ema_w / embedding / output must share one layout")
+    check(lib().vqgnn_vq_ema_finalize(ptr(stats), nb, M, D, W, ldw, float(decay), int(laplace),
+                                      float(grad_scale), float(epsilon), ptr(cs), cs.stride(0),
+                                      ptr(ema_w), ptr(emb), ptr(emb_out), emb.stride(0),
+                                      ptr(rm_f), ptr(rv_f), ptr(rm_g), ptr(rv_g),
+                                      ptr(bad_flag), stream_ptr()), "vq_ema_finalize")
+
+
+def gather_codes(subset: torch.Tensor, B: int, codes: torch.Tensor) -> torch.Tensor:
+    """lcodes[j] = codes[subset[B + j]]  (models.py:168)."""
+    n = subset.shape[0]
+    nb = codes.shape[1]
+    out = torch.empty(n - B, nb, dtype=torch.int16, device=codes.device)
+    check(lib().vqgnn_gather_codes(ptr(subset), B, n, ptr(codes), codes.stride(0), nb, ptr(out),
+                                   stream_ptr()), "gather_codes")
+    return out
+
+
+def scatter_codes(batch_idx: torch.Tensor, local: torch.Tensor, codes: torch.Tensor) -> None:
+    """codes[batch_idx[i]] = local[i] (batch_idx < 0 entries are padding)."""
+    B, nb = local.shape
+    check(lib().vqgnn_scatter_codes(ptr(batch_idx), B, ptr(local), nb, ptr(codes),
+                                    codes.stride(0), stream_ptr()), "scatter_codes")
+
+
+def spmm(rowptr, col, val, n_rows, nnz, X, F, B=None, D=0, lcodes=None, emb_out=None,
+         out=None):
+    """out[i] = sum_e val[e] * xin[col[e]]; xin = X rows (< B) / codebook rows (>= B)."""
+    require_gpu(X, "spmm")
+    dev = X.device
+    if out is None:
+        out = torch.empty(n_rows, F, dtype=torch.float32, device=dev)
+    L = lib()
+    ws = workspace(L.vqgnn_spmm_workspace(n_rows, nnz, F), dev)
+    if lcodes is not None:
+        nb, _, ldw = emb_out.shape
+        bstride = emb_out.stride(0)
+        Bv = int(B)
+    else:
+        nb, ldw, bstride = 0, 0, 0
+        Bv = 2**31 - 1
+    check(L.vqgnn_spmm(ptr(rowptr), ptr(col), ptr(val), int(n_rows), int(nnz), Bv, ptr(X), _ld(X),
+                       F, D, ptr(lcodes), nb, ptr(emb_out), ldw, bstride, ptr(out), _ld(out),
+                       ptr(ws), stream_ptr()), "spmm")
+    return out
+
+
+def csr_transpose(rowptr, col, val, n_rows, n_cols, nnz):
+    dev = rowptr.device
+    t_rowptr = torch.empty(n_cols + 1, dtype=torch.int32, device=dev)
+    t_col = torch.empty(max(nnz, 1), dtype=torch.int32, device=dev)
+    t_val = torch.empty(max(nnz, 1), dtype=torch.float32, device=dev)
+    L = lib()
+    ws = workspace(L.vqgnn_csr_transpose_workspace(n_rows, n_cols, nnz), dev)
+    check(L.vqgnn_csr_transpose(ptr(rowptr), ptr(col), ptr(val), n_rows, n_cols, nnz,
+                                ptr(t_rowptr), ptr(t_col), ptr(t_val), ptr(ws), stream_ptr()),
+          "csr_transpose")
+    return t_rowptr, t_col[:nnz], t_val[:nnz]

@@ -1,0 +1,402 @@
+"""Drop-in ``VectorQuantizerEMA`` (reference: vq_gnn_v2/vq.py:60-279) on HIP.
+
+State layout.  The reference keeps one ``VectorQuantizerEMA`` per branch
+(feature slice of D columns) with its own small buffers.  Here the state of
+all ``nb`` branches of a layer lives in one ``VQBank`` ([nb, M, 2D] codebooks,
+[nb, M] cluster sizes, [nb, D] BatchNorm running stats) so that one kernel
+launch serves every branch; each per-branch ``VectorQuantizerEMA`` exposes
+views of its slice under the reference's buffer names (``_embedding``,
+``_embedding_output``, ``_ema_cluster_size``, ``_ema_w``,
+``batch_norm_feat.running_mean`` ...), and ``state_dict()`` /
+``load_state_dict()`` use the reference's keys.
+
+Numerics.  BatchNorm statistics are fp64 sums on the GPU; the normalisation,
+distance and argmin follow ATen's CPU arithmetic exactly (see
+csrc/vq_kernels.hip), so codeword indices equal the reference's for equal
+normalisation coefficients; EMA sums are fp32 with a different summation
+order than MKL's one-hot sgemm (tolerance-tested).
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+from torch import nn
+
+from . import kernels
+from .kernels import BN_EVAL, BN_EVAL_INIT, BN_TRAIN, BN_TRAIN_INIT
+
+# 'Bad Init!' (vq.py:188) is a device flag.  The reference checks it with a
+# host sync on every call; VQGNN_DEFER_BAD_INIT=1 defers the check to
+# VQBank.check_bad_init() (used by bench.py so the timed step has no sync).
+STRICT_BAD_INIT = os.environ.get("VQGNN_DEFER_BAD_INIT", "0") != "1"
+
+
+class VQBank(nn.Module):
+    """Packed EMA-VQ state of ``nb`` branches.  Buffers are non-persistent: the
+    per-branch ``VectorQuantizerEMA`` modules own the state_dict entries."""
+
+    def __init__(self, nb, num_embeddings, embedding_dim, decay=0.99, epsilon=1e-24,
+                 grad_normalize_scale=(1, 1), warm_up_flag=False, momentum=0.1):
+        super().__init__()
+        M, D = int(num_embeddings), int(embedding_dim)
+        self.nb, self.M, self.D = int(nb), M, D
+        self.W = 2 * D
+        self.decay, self.epsilon = float(decay), float(epsilon)
+        self.grad_normalize_scale = grad_normalize_scale
+        self.warm_up_flag = bool(warm_up_flag)
+        self.momentum = float(momentum)
+        z = lambda *s: torch.zeros(*s, dtype=torch.float32)  # noqa: E731
+        self.register_buffer("emb", z(nb, M, self.W), persistent=False)
+        self.register_buffer("emb_out", z(nb, M, self.W), persistent=False)
+        self.register_buffer("ema_w", z(nb, M, self.W), persistent=False)
+        self.register_buffer("cs", z(nb, M), persistent=False)
+        self.register_buffer("rm_f", z(nb, D), persistent=False)
+        self.register_buffer("rv_f", torch.ones(nb, D), persistent=False)
+        self.register_buffer("rm_g", z(nb, D), persistent=False)
+        self.register_buffer("rv_g", torch.ones(nb, D), persistent=False)
+        self.register_buffer("nbt_f", torch.zeros(nb, dtype=torch.long), persistent=False)
+        self.register_buffer("nbt_g", torch.zeros(nb, dtype=torch.long), persistent=False)
+        self.register_buffer("bad_flag", torch.zeros(1, dtype=torch.int32), persistent=False)
+        self.bn_inited = [False] * nb
+        # multi-GPU: a dist.CodebookSync (all-reduce of sufficient statistics,
+        # all-gather of codes); None on one GPU
+        self.comm = None
+        self.comm_max_B = None
+        # last batched call's logging stash (vq.py:208-214, :276-277)
+        self.last_batch = None       # [4, nb*D] mean_f, std_f, mean_g, std_g
+        self.last_inputs = None      # (X, G) of the last update()
+
+    def init_branch(self, b):
+        """Per-branch random init in the reference's RNG order (vq.py:73-98)."""
+        M, D = self.M, self.D
+        self.emb[b].copy_(torch.randn(M, self.W))
+        if self.warm_up_flag:
+            self.ema_w[b].normal_()
+        s0 = self.grad_normalize_scale[0]
+        self.emb[b, :, D:2 * D] *= s0
+        self.ema_w[b, :, D:2 * D] *= s0
+
+    # ------------------------------------------------------------------ #
+    def check_bad_init(self):
+        if int(self.bad_flag.item()) != 0:
+            self.bad_flag.zero_()
+            raise ValueError('Bad Init!')
+
+    def _finish(self):
+        if STRICT_BAD_INIT:
+            self.check_bad_init()
+
+    _arange_cache = {}
+
+    def _arange(self, B, device):
+        key = (B, str(device))
+        t = VQBank._arange_cache.get(key)
+        if t is None:
+            t = torch.arange(B, dtype=torch.int64, device=device)
+            VQBank._arange_cache[key] = t
+        return t
+
+    def _sel(self, b0, nbr):
+        return slice(b0, b0 + nbr)
+
+    def feature_update(self, X, b0, nbr, training, idx_out=None, codes=None, batch_idx=None):
+        """vq.py:160-202 for branches [b0, b0+nbr): X is [B, nbr*D] (a row-major view)."""
+        D, F = self.D, nbr * self.D
+        sl = self._sel(b0, nbr)
+        B = X.shape[0]
+        if training and B <= 1:
+            raise ValueError("Expected more than 1 value per channel when training")
+        comm = self.comm if training else None
+        if training:
+            sums = kernels.bn_stats(X, None, F)
+            count = B
+            if comm is not None:
+                comm.allreduce_(sums)
+                count = comm.global_count(B)
+            coef, _ = kernels.bn_finalize(sums, count, F, False, BN_TRAIN, 0.1, 1e-5, 0.0, 0.0,
+                                          0.0, self.rm_f[sl], self.rv_f[sl])
+            self.nbt_f[sl] += 1
+        else:
+            coef, _ = kernels.bn_finalize(None, B, F, False, BN_EVAL, 0.1, 1e-5, 0.0, 0.0, 0.0,
+                                          self.rm_f[sl], self.rv_f[sl])
+        local = None
+        if comm is not None and codes is not None:
+            local = torch.empty(B, nbr, dtype=torch.int16, device=X.device)
+            stats = kernels.vq_assign(X, None, coef, 1.0, self.emb[sl], D, D, idx_out=idx_out,
+                                      codes=local, batch_idx=self._arange(B, X.device),
+                                      want_stats=training)
+        else:
+            stats = kernels.vq_assign(X, None, coef, 1.0, self.emb[sl], D, D, idx_out=idx_out,
+                                      codes=codes, batch_idx=batch_idx, want_stats=training)
+        if comm is not None:
+            comm.allreduce_(stats)
+            if local is not None:
+                comm.allgather_codes_(batch_idx, local, codes, self.comm_max_B)
+        if training:
+            kernels.vq_ema_finalize(stats, D, D, self.decay, self.warm_up_flag, 1.0, self.epsilon,
+                                    self.cs[sl], self.ema_w[sl], self.emb[sl], self.emb_out[sl],
+                                    self.rm_f[sl], self.rv_f[sl], self.rm_g[sl], self.rv_g[sl],
+                                    self.bad_flag)
+            self._finish()
+
+    def update(self, X, G, b0, nbr, training, idx_out=None, codes=None, batch_idx=None):
+        """vq.py:204-279 for branches [b0, b0+nbr): X, G are [B, nbr*D] views."""
+        D, F = self.D, nbr * self.D
+        sl = self._sel(b0, nbr)
+        B = X.shape[0]
+        inited = self.bn_inited[b0:b0 + nbr]
+        if any(inited) != all(inited):
+            raise RuntimeError("batched update() over branches with mixed bn_inited state")
+        init = not inited[0]
+        if training and B <= 1:
+            raise ValueError("Expected more than 1 value per channel when training")
+        comm = self.comm if training else None
+        sums = kernels.bn_stats(X, G, F)
+        count = B
+        if comm is not None:
+            comm.allreduce_(sums)
+            count = comm.global_count(B)
+        mode = (BN_TRAIN_INIT if init else BN_TRAIN) if training else \
+            (BN_EVAL_INIT if init else BN_EVAL)
+        coef, batch = kernels.bn_finalize(sums, count, F, True, mode, 0.1, 1e-5, self.momentum,
+                                          self.epsilon, self.epsilon, self.rm_f[sl],
+                                          self.rv_f[sl], self.rm_g[sl], self.rv_g[sl],
+                                          want_batch=True)
+        for b in range(b0, b0 + nbr):
+            self.bn_inited[b] = True
+        if training:
+            self.nbt_f[sl] += 1
+            self.nbt_g[sl] += 1
+        self.last_batch = batch
+        self.last_inputs = (X, G)
+        scale = float(self.grad_normalize_scale[0])
+        local = None
+        if comm is not None and codes is not None:
+            local = torch.empty(B, nbr, dtype=torch.int16, device=X.device)
+            stats = kernels.vq_assign(X, G, coef, scale, self.emb[sl], D, 2 * D,
+                                      idx_out=idx_out, codes=local,
+                                      batch_idx=self._arange(B, X.device), want_stats=training)
+        else:
+            stats = kernels.vq_assign(X, G, coef, scale, self.emb[sl], D, 2 * D,
+                                      idx_out=idx_out, codes=codes, batch_idx=batch_idx,
+                                      want_stats=training)
+        if comm is not None:
+            comm.allreduce_(stats)
+            if local is not None:
+                comm.allgather_codes_(batch_idx, local, codes, self.comm_max_B)
+        if training:
+            kernels.vq_ema_finalize(stats, D, 2 * D, self.decay, self.warm_up_flag, scale,
+                                    self.epsilon, self.cs[sl], self.ema_w[sl], self.emb[sl],
+                                    self.emb_out[sl], self.rm_f[sl], self.rv_f[sl],
+                                    self.rm_g[sl], self.rv_g[sl], self.bad_flag)
+            self._finish()
+
+
+class _BNView(nn.Module):
+    """BatchNorm1d(affine=False) state view of one branch (vq.py:86-88).  Only
+    the running statistics are state; normalisation runs inside the kernels."""
+
+    def __init__(self, owner, which, num_features, eps, momentum):
+        super().__init__()
+        self.__dict__["_owner"] = owner
+        self.__dict__["_which"] = which
+        self.num_features, self.eps, self.momentum = num_features, eps, momentum
+        self.affine, self.track_running_stats = False, True
+
+    def _bank(self):
+        return self._owner._get_bank()
+
+    @property
+    def running_mean(self):
+        return getattr(self._bank(), "rm_" + self._which)[self._owner._branch]
+
+    @property
+    def running_var(self):
+        return getattr(self._bank(), "rv_" + self._which)[self._owner._branch]
+
+    @property
+    def num_batches_tracked(self):
+        return getattr(self._bank(), "nbt_" + self._which)[self._owner._branch]
+
+    def _save_to_state_dict(self, destination, prefix, keep_vars):
+        destination[prefix + "running_mean"] = self.running_mean.detach().clone()
+        destination[prefix + "running_var"] = self.running_var.detach().clone()
+        destination[prefix + "num_batches_tracked"] = self.num_batches_tracked.detach().clone()
+
+    def _load_from_state_dict(self, state_dict, prefix, local_metadata, strict, missing_keys,
+                              unexpected_keys, error_msgs):
+        for k in ("running_mean", "running_var", "num_batches_tracked"):
+            if prefix + k in state_dict:
+                with torch.no_grad():
+                    getattr(self, k).copy_(state_dict[prefix + k])
+            elif strict:
+                missing_keys.append(prefix + k)
+
+    def forward(self, x):  # pragma: no cover - never on the hot path
+        raise NotImplementedError("normalisation is fused into the VQ kernels")
+
+
+class VectorQuantizerEMA(nn.Module):
+    """Reference: vq_gnn_v2/vq.py:60-279.  Same constructor, methods and buffer
+    names.  ``_bank``/``_branch`` are internal: a LowRankGNNLayer passes its
+    packed bank so that all branches share one launch."""
+
+    def __init__(self, num_embeddings, embedding_dim, commitment_cost=0.5, decay=0.99,
+                 epsilon=1e-24, grad_normalize_scale=(1, 1), warm_up_flag=False, momentum=0.1,
+                 add_flag=False, _bank=None, _branch=0):
+        super().__init__()
+        if add_flag:
+            raise NotImplementedError(
+                "add_flag=True (2D+1 codebook) is unused on the v2 path: models.py:30 hard-codes "
+                "add_flag = False")
+        self.add_flag = add_flag
+        self._embedding_dim = embedding_dim
+        self._num_embeddings = num_embeddings
+        self._commitment_cost = commitment_cost
+        self._warm_up_flag = warm_up_flag
+        self._decay = decay
+        self._epsilon = epsilon
+        self.grad_normalize_scale = grad_normalize_scale
+        if type(self.grad_normalize_scale) is not list:   # vq.py:91-92
+            raise ValueError('grad scale type wrong!')
+        if _bank is None:
+            self._own_bank = VQBank(1, num_embeddings, embedding_dim, decay, epsilon,
+                                    grad_normalize_scale, warm_up_flag, momentum)
+            self.__dict__["_shared_bank"] = None
+            self._branch = 0
+            self._own_bank.init_branch(0)
+        else:
+            self.__dict__["_shared_bank"] = _bank
+            self._branch = int(_branch)
+        self.batch_norm_feat = _BNView(self, "f", embedding_dim, 1e-5, 0.1)
+        self.batch_norm_grad = _BNView(self, "g", embedding_dim, epsilon, momentum)
+        self.mean = self.std = None
+        self.running_mean = self.running_std = None
+
+    # ---- state views -------------------------------------------------- #
+    def _get_bank(self) -> VQBank:
+        sb = self.__dict__.get("_shared_bank")
+        return sb if sb is not None else self._own_bank
+
+    @property
+    def _embedding(self):
+        return self._get_bank().emb[self._branch]
+
+    @property
+    def _embedding_output(self):
+        return self._get_bank().emb_out[self._branch]
+
+    @property
+    def _ema_cluster_size(self):
+        return self._get_bank().cs[self._branch]
+
+    @property
+    def _ema_w(self):
+        return self._get_bank().ema_w[self._branch]
+
+    @property
+    def bn_inited(self):
+        return self._get_bank().bn_inited[self._branch]
+
+    @bn_inited.setter
+    def bn_inited(self, v):
+        self._get_bank().bn_inited[self._branch] = bool(v)
+
+    _STATE = ("_embedding", "_embedding_output", "_ema_cluster_size", "_ema_w")
+
+    def _save_to_state_dict(self, destination, prefix, keep_vars):
+        for k in self._STATE:
+            destination[prefix + k] = getattr(self, k).detach().clone()
+
+    def _load_from_state_dict(self, state_dict, prefix, local_metadata, strict, missing_keys,
+                              unexpected_keys, error_msgs):
+        for k in self._STATE:
+            if prefix + k in state_dict:
+                with torch.no_grad():
+                    getattr(self, k).copy_(state_dict[prefix + k])
+            elif strict:
+                missing_keys.append(prefix + k)
+
+    # ---- reference methods -------------------------------------------- #
+    def feature_kmeans_init(self, kmeans_centroids, kmeans_counts):   # vq.py:102-105
+        D = self._embedding_dim
+        with torch.no_grad():
+            self._embedding[:, :D] = kmeans_centroids
+            self._ema_cluster_size.copy_(kmeans_counts)
+            self._ema_w[:, :D] = kmeans_centroids * kmeans_counts.unsqueeze(1)
+
+    def kmeans_init(self, kmeans_centroids, kmeans_counts):            # vq.py:108-118
+        D = self._embedding_dim
+        s0 = self.grad_normalize_scale[0]
+        with torch.no_grad():
+            self._embedding.copy_(kmeans_centroids)
+            self._ema_cluster_size.copy_(kmeans_counts)
+            self._ema_w.copy_(kmeans_centroids * kmeans_counts.unsqueeze(1))
+            self._embedding[:, D:2 * D] *= s0
+            self._ema_w[:, D:2 * D] *= s0
+
+    def get(self):                                                     # vq.py:120-121
+        return self._embedding_output
+
+    def get_codebook(self):                                            # vq.py:123-124
+        return self._embedding_output[:, :self._embedding_dim]
+
+    def get_grad(self):                                                # vq.py:126-127
+        return self._embedding_output[:, self._embedding_dim:]
+
+    def get_feat_cen_norm(self):                                       # vq.py:129-131
+        return torch.norm(torch.mean(self._embedding[:, :self._embedding_dim], dim=0)).item()
+
+    def get_grad_cen_norm(self):                                       # vq.py:133-135
+        return torch.norm(torch.mean(self._embedding[:, self._embedding_dim:], dim=0)).item()
+
+    def feature_update(self, X_B):                                     # vq.py:160-202
+        bank = self._get_bank()
+        idx = torch.empty(X_B.shape[0], 1, dtype=torch.long, device=X_B.device)
+        bank.feature_update(X_B, self._branch, 1, self.training, idx_out=idx.view(1, -1))
+        return idx
+
+    def update(self, X_B, grad):                                       # vq.py:204-279
+        bank = self._get_bank()
+        B = X_B.shape[0]
+        idx = torch.empty(B, 1, dtype=torch.long, device=X_B.device)
+        bank.update(X_B, grad, self._branch, 1, self.training, idx_out=idx.view(1, -1))
+        self._stash_update_logs(bank, 0, X_B, grad)
+        # The dense [B, M] one-hot of the reference is returned as a sparse COO
+        # tensor (same values; .to_dense() reproduces it) instead of 4*B*M bytes.
+        ones = torch.ones(B, dtype=torch.float32, device=X_B.device)
+        rows = torch.arange(B, device=X_B.device)
+        encodings = torch.sparse_coo_tensor(torch.stack([rows, idx[:, 0]]), ones,
+                                            (B, self._num_embeddings))
+        return idx, encodings
+
+    def _stash_update_logs(self, bank, local_b, X_B, grad):
+        D = self._embedding_dim
+        batch = bank.last_batch          # [4, nbr*D]
+        sl = slice(local_b * D, (local_b + 1) * D)
+        self.mean = torch.cat([batch[0, sl], batch[2, sl]]).unsqueeze(0)
+        self.std = torch.cat([batch[1, sl], batch[3, sl]]).unsqueeze(0)
+        self.__dict__["_zero_rate_src"] = (X_B[:, 0], grad[:, 0], self.std, X_B.shape[0])
+        if self.training:
+            b = self._branch
+            rv = torch.cat([bank.rv_f[b] + 1e-5, bank.rv_g[b] + self._epsilon])
+            self.running_std = torch.sqrt(rv).unsqueeze(0)
+            self.running_mean = torch.cat([bank.rm_f[b], bank.rm_g[b]]).unsqueeze(0)
+
+    # logging-only attributes of vq.py:213-214, computed on access
+    @property
+    def feat_zero_rate(self):
+        src = self.__dict__.get("_zero_rate_src")
+        if src is None:
+            return None
+        x0, _, std, B = src
+        return torch.sum(torch.abs(x0) < std[0][0] * 1e-5) / B
+
+    @property
+    def grad_zero_rate(self):
+        src = self.__dict__.get("_zero_rate_src")
+        if src is None:
+            return None
+        _, g0, std, B = src
+        return torch.sum(g0 < std[0][self._embedding_dim] * 1e-5) / B
