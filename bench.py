@@ -5,8 +5,8 @@ One step = one layer step on a synthetic arxiv-shaped mini-batch (SURVEY.md §8d
         semantics (W = 2D: features and gradients), one launch sequence
         (BN stats -> BN finalize -> MFMA assign + fused EMA statistics ->
         EMA finalize), c_indices scattered in place;
-  (ii)  codebook-code gather for the B' out-of-batch rows;
-  (iii) fused codebook-gather + CSR SpMM over all nnz edges, all n rows.
+  (ii)  codeword gather for the B' out-of-batch rows (x_first_order);
+  (iii) two-source CSR SpMM over all nnz edges, all n rows.
 value = edges of all ranks / time.  Inputs are resident in HBM before timing.
 
 Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
@@ -104,11 +104,10 @@ def main():
             bank.feature_update(Xd, 0, nb, True, codes=codes, batch_idx=bidx)
         if record:
             e[1].record()
-        lcodes = kernels.gather_codes(subset, B, codes)
+        x_first, _ = kernels.gather_codewords(subset, B, codes, bank.emb_out, D)
         if record:
             e[2].record()
-        kernels.spmm(adj.rowptr, adj.col, adj.value, n, nnz, Xd, F, B=B, D=D, lcodes=lcodes,
-                     emb_out=bank.emb_out)
+        kernels.spmm(adj.rowptr, adj.col, adj.value, n, nnz, Xd, F, X2=x_first, B=B)
         if record:
             e[3].record()
             ev.append(e)
@@ -148,9 +147,11 @@ def main():
     gather_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in ev]))
     spmm_ms = float(np.mean([e[2].elapsed_time(e[3]) for e in ev]))
 
-    spmm_bytes = 4 * (n + 1) + 8 * nnz + 4 * B * F + 2 * (n - B) * nb + 4 * nb * M * D + 4 * n * F
+    # SpMM compulsory bytes: rowptr + (col, val) + every input row once (x and
+    # x_first_order) + the output; the codeword gather kernel is counted apart
+    spmm_bytes = 4 * (n + 1) + 8 * nnz + 4 * n * F + 4 * n * F
     vq_flops = 2.0 * B * M * W * nb
-    rl_spmm = dict(kernel="spmm_merge_kernel (+fixup)", bound="hbm",
+    rl_spmm = dict(kernel="spmm_merge_kernel", bound="hbm",
                    achieved=spmm_bytes / (spmm_ms * 1e-3) / 1e9, peak=8000.0, unit="GB/s",
                    bytes_per_launch=spmm_bytes, ms_per_launch=spmm_ms)
     rl_spmm["frac"] = rl_spmm["achieved"] / rl_spmm["peak"]
@@ -190,11 +191,11 @@ def main():
             ms_per_step=ms_step, higher_is_better=True, scaling="weak", vs_baseline=None,
             dtype="f32", data="synthetic (seeded arxiv-shaped graph, random features)",
             config=dict(workload=f"{args.config}: one layer step (VQ {args.semantics} + EMA for "
-                                 f"{nb} branches, code gather, fused gather-SpMM)",
+                                 f"{nb} branches, codeword gather, SpMM)",
                         B=B, B_prime=n - B, nnz=nnz, F=F, M=M, D=D, W=W,
                         parallelism=f"dp{world}"),
             roofline=roofline,
-            kernels=dict(vq_ms=vq_ms, gather_ms=gather_ms, spmm_ms=spmm_ms,
+            kernels=dict(vq_ms=vq_ms, codeword_gather_ms=gather_ms, spmm_ms=spmm_ms,
                          spmm=rl_spmm, vq=rl_vq),
             cpu_baseline=cpu,
         )

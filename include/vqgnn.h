@@ -83,7 +83,7 @@ int vqgnn_bn_finalize(const double* sums, int64_t count, int32_t F, int32_t with
 
 /* ------------------------------------------------------------------------ *
  * 3. Product-quantised nearest-codeword assignment for nb branches at once,
- *    plus (ema_stats != NULL) the EMA sufficient statistics.
+ *    plus (ema_parts != NULL) the EMA sufficient statistics.
  *    Replaces, per branch b, vq.py:166-173 (feature_update, W = D) or
  *    vq.py:223-238 (update, W = 2D): normalise, d = (|x|^2 + |e|^2) - 2 x.e,
  *    argmin (first index on ties), and the one-hot reductions of
@@ -94,25 +94,35 @@ int vqgnn_bn_finalize(const double* sums, int64_t count, int32_t F, int32_t with
  *    Outputs (each optional):
  *      idx_out   [nb][B] int64   — encoding_indices per branch
  *      codes     [*][ldc] int16  — codes[batch_idx[i]][b] = idx (models.py:63/46)
- *      ema_stats [nb][M][W+1] fp32 — count, then sum of normalised x per codeword
+ *      ema_parts [P][nb][M][W+1] fp32 — P = vqgnn_vq_ema_parts(B, nb, M, W)
+ *                partial slabs of (count, sum of normalised x) per codeword;
+ *                their sum (in slab order) is the EMA statistic.
  * ------------------------------------------------------------------------ */
+int32_t vqgnn_vq_ema_parts(int32_t B, int32_t nb, int32_t M, int32_t W);
 size_t vqgnn_vq_assign_workspace(int32_t B, int32_t nb, int32_t M, int32_t W);
 int vqgnn_vq_assign(const float* X, int64_t ldx, const float* G, int64_t ldg,
                     int32_t B, int32_t nb, int32_t D, int32_t M, int32_t W,
                     const float* coef, float grad_scale,
                     const float* embedding, int32_t ldw, int64_t emb_bstride,
                     int64_t* idx_out, int16_t* codes, int64_t ldc,
-                    const int64_t* batch_idx, float* ema_stats,
+                    const int64_t* batch_idx, float* ema_parts,
                     void* workspace, vqgnn_stream_t stream);
+
+/* 3b. Fold P partial slabs into one (slab order): out[i] = sum_p parts[p][i].
+ *     Multi-GPU callers fold, then all-reduce the single slab.               */
+int vqgnn_vq_ema_reduce(const float* parts, int32_t nparts, int64_t part_elems,
+                        float* out, vqgnn_stream_t stream);
 
 /* 4. EMA codebook finalize for nb branches (vq.py:177-200 / :242-277):
  *    cluster size EMA, Laplace smoothing (laplace != 0, vq.py:182-186),
- *    'Bad Init!' detection (*bad_init |= 1, vq.py:188), ema_w EMA, embedding =
- *    ema_w / cs, and the de-normalised _embedding_output.  W = D updates the
- *    feature half only (feature_update); W = 2D all columns (update).
- *    Running stats (rm_f, rv_f, rm_g, rv_g) are [nb][D].  Per-branch arrays use strides
- *    cs_bstride (cluster_size) and emb_bstride (ema_w, embedding, output).   */
-int vqgnn_vq_ema_finalize(const float* ema_stats, int32_t nb, int32_t M,
+ *    'Bad Init!' detection (*bad_init |= 1, vq.py:188, and the branch is left
+ *    with only cluster_size updated, as the reference raises there), ema_w EMA,
+ *    embedding = ema_w / cs, and the de-normalised _embedding_output.  W = D
+ *    updates the feature half only (feature_update); W = 2D all columns.
+ *    ema_parts: nparts slabs of [nb][M][W+1] (summed in order).
+ *    Running stats (rm_f, rv_f, rm_g, rv_g) are [nb][D].  Per-branch arrays use
+ *    strides cs_bstride (cluster_size) and emb_bstride (ema_w, embedding, out). */
+int vqgnn_vq_ema_finalize(const float* ema_parts, int32_t nparts, int32_t nb, int32_t M,
                           int32_t D, int32_t W, int32_t ldw,
                           float decay, int32_t laplace, float grad_scale, float epsilon,
                           float* cluster_size, int64_t cs_bstride,
@@ -123,37 +133,42 @@ int vqgnn_vq_ema_finalize(const float* ema_stats, int32_t nb, int32_t M,
                           int32_t* bad_init, vqgnn_stream_t stream);
 
 /* ------------------------------------------------------------------------ *
- * 5. Out-of-batch code gather (models.py:158, :168): for j in [0, n-B),
- *    lcodes[j][b] = codes[subset[B+j]][b], b < nb.
+ * 5. Out-of-batch codeword gather (models.py:158, :168-173): for j in [0, n-B)
+ *    and b < nb, with code = codes[subset[B+j]][b]:
+ *      xt[j][b*D + k] = emb_out[b][code][col_offset + k],  k < D
+ *      lcodes[j][b]   = code                               (optional)
+ *    col_offset = 0 gives x_first_order (feature halves), col_offset = D the
+ *    grad halves (grad_first_order).  emb_out [nb][M][ldw], branch stride
+ *    emb_bstride; xt [n-B][ldt].  xt may be NULL (codes only).
  * ------------------------------------------------------------------------ */
-int vqgnn_gather_codes(const int64_t* subset, int32_t B, int32_t n,
-                       const int16_t* codes, int64_t ldc, int32_t nb,
-                       int16_t* lcodes, vqgnn_stream_t stream);
+int vqgnn_gather_codewords(const int64_t* subset, int32_t B, int32_t n,
+                           const int16_t* codes, int64_t ldc, int32_t nb, int32_t D,
+                           const float* emb_out, int32_t ldw, int64_t emb_bstride,
+                           int32_t col_offset, float* xt, int64_t ldt,
+                           int16_t* lcodes, vqgnn_stream_t stream);
 
 /* 5b. Code scatter (models.py:63 / :46 across ranks): for i in [0, B),
- *     codes[batch_idx[i]][b] = local[i][b].  Multi-GPU callers all-gather the
- *     (batch_idx, local codes) of every rank and scatter them with this so all
- *     replicas' c_indices stay identical.                                     */
+ *     codes[batch_idx[i]][b] = local[i][b]  (batch_idx[i] < 0: skipped).
+ *     Multi-GPU callers all-gather the (batch_idx, local codes) of every rank
+ *     and scatter them with this so all replicas' c_indices stay identical.  */
 int vqgnn_scatter_codes(const int64_t* batch_idx, int32_t B, const int16_t* local,
                         int32_t nb, int16_t* codes, int64_t ldc, vqgnn_stream_t stream);
 
-/* 6. Fused codebook-gather + CSR SpMM (sum):
+/* 6. Two-source CSR SpMM (sum), the aggregation of OurGCNConv (convs.py:95 ->
+ *    torch_sparse spmm_sum):
  *      out[i][:] = sum_{e in row i} val[e] * xin[col[e]][:]
- *    with xin[j] = X[j] for j < B, and for j >= B the concatenation over
- *    branches of embedding_output[b][lcodes[j-B][b]][0:D] (models.py:168-179
- *    -> convs.py:95 -> torch_sparse spmm_sum).  Rows are summed in CSR order
- *    (mul then add, as spmm_sum), except rows longer than one edge chunk, whose
- *    chunk partials are added in chunk order.  lcodes == NULL (or B >= n_cols)
- *    gives a plain SpMM with a dense right-hand side — the transpose product
- *    of the backward pass.  F must be a multiple of 4, D a multiple of 4 or
- *    lcodes NULL.  out: [n_rows][ldo].                                        */
+ *    with xin[j] = X[j] for j < B and X2[j - B] for j >= B, i.e.
+ *    x_input = cat([x, x_first_order]) (models.py:174) without the copy.
+ *    X2 == NULL: xin = X (plain SpMM; B ignored) — also the transpose product
+ *    of the backward pass.  Rows of at most L edges (L >= 128) are summed in CSR
+ *    order with separate mul and add, bit-identical to spmm_sum's loop; longer
+ *    rows are split into edge chunks whose partials are added in chunk order.
+ *    F must be a multiple of 4; X/X2/out 16-byte aligned; out [n_rows][ldo]. */
 size_t vqgnn_spmm_workspace(int32_t n_rows, int64_t nnz, int32_t F);
 int vqgnn_spmm(const int32_t* rowptr, const int32_t* col, const float* val,
                int32_t n_rows, int64_t nnz, int32_t B,
-               const float* X, int64_t ldx, int32_t F, int32_t D,
-               const int16_t* lcodes, int32_t nb,
-               const float* emb_out, int32_t ldw, int64_t emb_bstride,
-               float* out, int64_t ldo, void* workspace, vqgnn_stream_t stream);
+               const float* X, int64_t ldx, const float* X2, int64_t ldx2,
+               int32_t F, float* out, int64_t ldo, void* workspace, vqgnn_stream_t stream);
 
 /* 7. CSR transpose (structure + values) for the backward product
  *    dX = A^T dOut (torch_sparse matmul autograd, convs.py:95).  Output CSR of

@@ -1,0 +1,42 @@
+"""Run one hot-path kernel a few times on arxiv-shaped data (PMC target)."""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import vqgnn_pkg  # noqa: E402
+
+vqgnn_pkg.load()
+from vq_gnn_amd import kernels  # noqa: E402
+from vq_gnn_amd.graph import CONFIGS, batch_to_device, make_batch  # noqa: E402
+from vq_gnn_amd.vq import VQBank  # noqa: E402
+import vq_gnn_amd.vq as vqmod  # noqa: E402
+
+vqmod.STRICT_BAD_INIT = False
+dev = torch.device("cuda:0")
+what = sys.argv[1] if len(sys.argv) > 1 else "step"
+reps = int(os.environ.get("REPS", "5"))
+cfg = CONFIGS[os.environ.get("CONFIG", "arxiv_gcn")]
+g, _, b = make_batch(cfg)
+bidx, subset, adj = batch_to_device(b, dev)
+F, M, D = cfg["F"], cfg["M"], 4
+nb = F // D
+X = torch.randn(b.B, F, device=dev)
+G = torch.randn(b.B, F, device=dev) * 1e-3
+codes = torch.randint(0, M, (g.N, nb), dtype=torch.int16, device=dev)
+bank = VQBank(nb, M, D, warm_up_flag=True)
+for i in range(nb):
+    bank.init_branch(i)
+bank = bank.to(dev)
+bank.feature_update(X, 0, nb, True, codes=codes, batch_idx=bidx)
+xt, _ = kernels.gather_codewords(subset, b.B, codes, bank.emb_out, D)
+torch.cuda.synchronize()
+for _ in range(reps):
+    if what in ("vq", "step"):
+        bank.update(X, G, 0, nb, True, codes=codes, batch_idx=bidx)
+    if what in ("spmm", "step"):
+        xt, _ = kernels.gather_codewords(subset, b.B, codes, bank.emb_out, D)
+        kernels.spmm(adj.rowptr, adj.col, adj.value, b.n, b.nnz, X, F, X2=xt, B=b.B)
+torch.cuda.synchronize()
+print("done", what, "B", b.B, "n", b.n, "nnz", b.nnz)

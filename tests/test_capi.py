@@ -33,7 +33,9 @@ def test_version_and_error_text():
 def test_host_only_workspace_queries():
     h = L.lib()
     assert h.vqgnn_bn_stats_workspace(84670, 128) > 0
-    assert h.vqgnn_vq_assign_workspace(84670, 32, 256, 8) >= 32 * 256 * 9 * 4
+    assert h.vqgnn_vq_assign_workspace(84670, 32, 256, 8) >= 256       # fused EMA
+    assert h.vqgnn_vq_assign_workspace(30000, 64, 4096, 8) >= 64 * 30000 * 4  # idx scratch
+    assert 1 <= h.vqgnn_vq_ema_parts(84670, 32, 256, 8) <= 64
     assert h.vqgnn_spmm_workspace(128000, 2_000_000, 128) > 0
 
 
@@ -44,6 +46,8 @@ def test_invalid_arguments_rejected_without_device():
                            None, None, 0, None, None, None, None)
     assert rc == 1
     assert b"null" in h.vqgnn_last_error() or b"W" in h.vqgnn_last_error()
-    rc = h.vqgnn_spmm(None, None, None, 4, 0, 0, None, 4, 6, 4, None, 0, None, 0, 0, None, 4,
-                      None, None)
+    # dummy non-null addresses: validation rejects F before any pointer is used
+    rc = h.vqgnn_spmm(16, None, None, 4, 0, 0, None, 4, None, 0, 6, 16, 4, None, None)
+    assert rc == 1 and b"multiple of 4" in h.vqgnn_last_error()
+    rc = h.vqgnn_spmm(None, None, None, 4, 0, 0, None, 4, None, 0, 8, None, 8, None, None)
     assert rc == 1 and b"null" in h.vqgnn_last_error()

@@ -40,8 +40,7 @@ def test_spmm_bit_exact_short_rows(F):
     out = kernels.spmm(a.rowptr, a.col, a.value, 700, a.nnz(), torch.from_numpy(x).to(DEV), F)
     ref = conv_ref.spmm_seq(rowptr, col, val, x)
     deg = np.diff(rowptr)
-    S = 128 if F <= 128 else 64
-    inside = (rowptr[:-1] // S == np.maximum(rowptr[1:] - 1, rowptr[:-1]) // S)
+    inside = deg <= 128   # rows of <= L edges are summed whole by their owner
     o = out.cpu().numpy()
     assert np.array_equal(o[inside], ref[inside])
     np.testing.assert_allclose(o, ref, rtol=1e-5, atol=1e-5)
@@ -75,8 +74,8 @@ def test_spmm_empty_and_degenerate():
     assert torch.equal(out, exp)
 
 
-@pytest.mark.parametrize("F,D", [(128, 4), (32, 4), (256, 4), (64, 8)])
-def test_fused_gather_spmm_vs_oracle(F, D):
+@pytest.mark.parametrize("F,D", [(128, 4), (32, 4), (256, 4), (64, 8), (48, 2), (60, 3)])
+def test_codeword_gather_and_two_source_spmm_vs_oracle(F, D):
     g = graph.synthetic_graph(4000, 8, 20000, seed=F + D)
     rp, cl, vl = graph.norm_adj(g, "GCN")
     b = graph.k_hop_batch(rp, cl, vl, g.N, graph.cluster_batch(g, [0, 2, 5]))
@@ -87,16 +86,18 @@ def test_fused_gather_spmm_vs_oracle(F, D):
     codes = rng.integers(0, M, size=(g.N, nb)).astype(np.int16)
     bidx, subset, adj = graph.batch_to_device(b, DEV)
     codes_d = torch.from_numpy(codes).to(DEV)
-    lcodes = kernels.gather_codes(subset, b.B, codes_d)
+    emb_d = torch.from_numpy(emb_out).to(DEV)
+    xt, lcodes = kernels.gather_codewords(subset, b.B, codes_d, emb_d, D, want_codes=True)
     assert torch.equal(lcodes.cpu(), torch.from_numpy(codes[b.subset[b.B:]]))
+    gfo, _ = kernels.gather_codewords(subset, b.B, codes_d, emb_d, D, col_offset=D)
+    torch.testing.assert_close(gfo.cpu(), conv_ref.grad_first_order(b.subset, b.B, codes,
+                                                                    emb_out, D), rtol=0, atol=0)
     out = kernels.spmm(adj.rowptr, adj.col, adj.value, b.n, b.nnz, torch.from_numpy(X).to(DEV),
-                       F, B=b.B, D=D, lcodes=lcodes, emb_out=torch.from_numpy(emb_out).to(DEV))
+                       F, X2=xt, B=b.B)
     xin = conv_ref.gather_input(X, b.subset, b.B, codes, emb_out, D).numpy()
     ref = conv_ref.spmm_seq(b.rowptr, b.col, b.val, xin)
     np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=1e-5, atol=1e-6)
-    S = 128 if F <= 128 else 64
-    rp_ = b.rowptr
-    inside = (rp_[:-1] // S == np.maximum(rp_[1:] - 1, rp_[:-1]) // S)
+    inside = np.diff(b.rowptr) <= 128
     assert np.array_equal(out.cpu().numpy()[inside], ref[inside])
 
 

@@ -50,7 +50,7 @@ def test_assign_bit_exact_given_coefficients(M, D, W, B, tie):
     xn = torch.cat([X * af + bf, ((G * ag + bg) * scale)], 1)[:, :W]
     cnt = torch.bincount(idx_ref, minlength=M).float()
     dw = torch.zeros(M, W, dtype=torch.float64).index_add_(0, idx_ref, xn.double())
-    st = stats.cpu()[0]
+    st = stats.sum(0).cpu()[0]
     assert torch.equal(st[:, 0], cnt)
     torch.testing.assert_close(st[:, 1:].double(), dw, rtol=1e-4, atol=1e-4)
 

@@ -33,23 +33,26 @@ SIGNATURES = {
     "vqgnn_bn_finalize": (ctypes.c_int, [_c_void_p, _i64, _i32, _i32, _i32, _f32, _f32, _f32,
                                          _f32, _f32, _c_void_p, _c_void_p, _c_void_p,
                                          _c_void_p, _c_void_p, _c_void_p, _c_void_p]),
+    "vqgnn_vq_ema_parts": (_i32, [_i32, _i32, _i32, _i32]),
     "vqgnn_vq_assign_workspace": (_size, [_i32, _i32, _i32, _i32]),
+    "vqgnn_vq_ema_reduce": (ctypes.c_int, [_c_void_p, _i32, _i64, _c_void_p, _c_void_p]),
     "vqgnn_vq_assign": (ctypes.c_int, [_c_void_p, _i64, _c_void_p, _i64, _i32, _i32, _i32,
                                        _i32, _i32, _c_void_p, _f32, _c_void_p, _i32, _i64,
                                        _c_void_p, _c_void_p, _i64, _c_void_p, _c_void_p,
                                        _c_void_p, _c_void_p]),
-    "vqgnn_vq_ema_finalize": (ctypes.c_int, [_c_void_p, _i32, _i32, _i32, _i32, _i32, _f32,
+    "vqgnn_vq_ema_finalize": (ctypes.c_int, [_c_void_p, _i32, _i32, _i32, _i32, _i32, _i32, _f32,
                                              _i32, _f32, _f32, _c_void_p, _i64, _c_void_p,
                                              _c_void_p, _c_void_p, _i64, _c_void_p, _c_void_p,
                                              _c_void_p, _c_void_p, _c_void_p, _c_void_p]),
-    "vqgnn_gather_codes": (ctypes.c_int, [_c_void_p, _i32, _i32, _c_void_p, _i64, _i32,
-                                          _c_void_p, _c_void_p]),
+    "vqgnn_gather_codewords": (ctypes.c_int, [_c_void_p, _i32, _i32, _c_void_p, _i64, _i32,
+                                              _i32, _c_void_p, _i32, _i64, _i32, _c_void_p,
+                                              _i64, _c_void_p, _c_void_p]),
     "vqgnn_scatter_codes": (ctypes.c_int, [_c_void_p, _i32, _c_void_p, _i32, _c_void_p, _i64,
                                            _c_void_p]),
     "vqgnn_spmm_workspace": (_size, [_i32, _i64, _i32]),
     "vqgnn_spmm": (ctypes.c_int, [_c_void_p, _c_void_p, _c_void_p, _i32, _i64, _i32,
-                                  _c_void_p, _i64, _i32, _i32, _c_void_p, _i32, _c_void_p,
-                                  _i32, _i64, _c_void_p, _i64, _c_void_p, _c_void_p]),
+                                  _c_void_p, _i64, _c_void_p, _i64, _i32, _c_void_p, _i64,
+                                  _c_void_p, _c_void_p]),
     "vqgnn_csr_transpose_workspace": (_size, [_i32, _i32, _i64]),
     "vqgnn_csr_transpose": (ctypes.c_int, [_c_void_p, _c_void_p, _c_void_p, _i32, _i32, _i64,
                                            _c_void_p, _c_void_p, _c_void_p, _c_void_p,

@@ -4,9 +4,10 @@
 (models.py:93-94) — is ``out = A @ x`` over the batch adjacency
 (PyG GCNConv.message_and_aggregate -> torch_sparse.matmul(adj_t, x,
 reduce='add')); no weight, bias or normalisation inside (convs.py:69-99 are
-commented out).  Here the product is the HIP merge-SpMM, and the layer's input
-``x_input = [x ; codewords of B']`` (models.py:168-174) may be passed lazily as
-a ``GatheredInput`` so the [B', F] codeword rows are never materialised.
+commented out).  Here the product is the HIP edge-balanced SpMM, and the
+layer's input ``x_input = [x ; x_first_order]`` (models.py:168-174) may be
+passed as a ``GatheredInput`` pair so the concatenation is never copied: the
+kernel reads rows < B from x and rows >= B from x_first_order.
 """
 from __future__ import annotations
 
@@ -21,25 +22,19 @@ from .sparse import CSR, as_csr
 
 
 class GatheredInput(NamedTuple):
-    """x_input = cat([x, concat_b emb_out[b][lcodes[:, b], :D]]) without the cat.
+    """x_input = cat([x, x_first_order]) (models.py:174) without the cat.
 
-    x: [B, F] batch rows; lcodes: [n - B, nb] int16 codes of the out-of-batch
-    rows; emb_out: [nb, M, 2D] codebooks (vq._embedding_output of each branch);
-    D: sub-vector width."""
+    x: [B, F] batch rows (requires grad); x_first: [n - B, F] codeword rows of
+    the out-of-batch nodes (a buffer: no gradient, models.py:169-173)."""
     x: torch.Tensor
-    lcodes: torch.Tensor
-    emb_out: torch.Tensor
-    D: int
+    x_first: torch.Tensor
 
     @property
     def shape(self):
-        return (self.x.shape[0] + self.lcodes.shape[0], self.x.shape[1])
+        return (self.x.shape[0] + self.x_first.shape[0], self.x.shape[1])
 
     def materialize(self):
-        nb = self.lcodes.shape[1]
-        idx = self.lcodes.long()
-        parts = [self.emb_out[b][idx[:, b], :self.D] for b in range(nb)]
-        return torch.cat([self.x, torch.cat(parts, dim=1)])
+        return torch.cat([self.x, self.x_first])
 
 
 class _VQHook:
@@ -54,16 +49,16 @@ class _VQHook:
 
 
 class GatherSpMMFunction(torch.autograd.Function):
-    """out = A @ [x ; codewords]; d/dx = (A^T @ dout)[:B] (x_first_order is a
+    """out = A @ [x ; x_first]; d/dx = (A^T @ dout)[:B] (x_first_order is a
     buffer, models.py:169-174, so it receives no gradient)."""
 
     @staticmethod
-    def forward(ctx, x, adj, lcodes, emb_out, D, hook):
+    def forward(ctx, x, adj, x_first, hook, anchor):
         B, F = x.shape
         n = adj.size(0)
-        xc = x if (x.stride(1) == 1 and x.stride(0) % 4 == 0) else x.contiguous()
-        out = kernels.spmm(adj.rowptr, adj.col, adj.value, n, adj.nnz(), xc, F, B=B, D=D,
-                           lcodes=lcodes, emb_out=emb_out)
+        xc = x if (x.stride(1) == 1 and x.stride(0) % 4 == 0 and
+                   x.data_ptr() % 16 == 0) else x.contiguous()
+        out = kernels.spmm(adj.rowptr, adj.col, adj.value, n, adj.nnz(), xc, F, X2=x_first, B=B)
         ctx.adj, ctx.B, ctx.hook = adj, B, hook
         return out
 
@@ -80,7 +75,7 @@ class GatherSpMMFunction(torch.autograd.Function):
             # rows [0, B) of A^T = columns [0, B) of A; the merge kernel bounds
             # the walk with the full nnz, so no host read of t_rowptr[B] is needed
             dx = kernels.spmm(at.rowptr, at.col, at.value, B, at.nnz(), dout, F)
-        return dx, None, None, None, None, None
+        return dx, None, None, None, None
 
 
 class SpMMFunction(torch.autograd.Function):
@@ -138,7 +133,12 @@ class OurGCNConv(nn.Module):
     def forward(self, x, edge_index, edge_weight=None, _hook=None):
         adj = as_csr(edge_index)
         if isinstance(x, GatheredInput):
-            return GatherSpMMFunction.apply(x.x, adj, x.lcodes, x.emb_out, x.D, _hook)
+            anchor = None
+            if _hook is not None and not x.x.requires_grad:
+                # the v1 hook must run even for a first layer whose input needs
+                # no grad (models.py:184 requires_grad_() on the output slice)
+                anchor = torch.zeros((), device=x.x.device, requires_grad=True)
+            return GatherSpMMFunction.apply(x.x, adj, x.x_first, _hook, anchor)
         return SpMMFunction.apply(x, adj)
 
     def __repr__(self):

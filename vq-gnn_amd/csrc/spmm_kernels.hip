@@ -1,24 +1,28 @@
-// Fused codebook-gather + CSR SpMM for gfx950 (MI355X), the out-of-batch code
-// gather, and the CSR transpose for the backward product.
+// Codeword gather, two-source CSR SpMM, code scatter and CSR transpose for
+// gfx950 (MI355X).
 //
 // Reference path: LowRankGNNLayer.forward (vq_gnn_v2/models.py:157-179) builds
 // x_input = [x ; concat_b codebook_b[c_b[subset[B:]], :D]] and calls
 // OurGCNConv.forward (convs.py:65-101) -> PyG GCNConv.message_and_aggregate ->
-// torch_sparse.matmul(adj_t, x_input, reduce='add') (spmm_sum).  Here the
-// [B', F] codeword rows are never materialised: an edge to j >= B reads the
-// node's int16 code per branch and the codeword's feature half straight from
-// the (L2-resident) _embedding_output.
+// torch_sparse.matmul(adj_t, x_input, reduce='add') (spmm_sum).
 //
-// Work decomposition: merge-based / edge-balanced.  The nnz range is cut into
-// chunks of S edges; one lane group (G lanes, each owning float4 column
-// chunks) walks one chunk, summing each row's edges in CSR order with
-// separate mul and add (spmm_sum's `out = out + val * x`, init 0) and storing
-// rows that end inside the chunk.  A row that crosses a chunk boundary leaves
-// one partial per chunk ("carry"); a fix-up kernel adds them in chunk order.
-// Zipf hub rows therefore spread over many groups instead of serialising one.
+// Here: (1) gather_codewords writes x_first_order [B', F] once per
+// out-of-batch node (one coalesced 4*F-byte row per node; the codebooks are
+// L2-resident) — measured 2.3x faster than gathering codewords per edge,
+// where each edge touches nb different codebook lines; (2) the SpMM reads
+// rows j < B from x and rows j >= B from x_first_order (no torch.cat copy).
+//
+// SpMM work decomposition: edge-balanced.  The nnz range is cut into chunks
+// of S edges; a lane group (G lanes, float4 column chunks each) owns the rows
+// that START in its chunk and sums each of them in CSR order with separate
+// mul and add (spmm_sum's `out = out + val * x`, init 0) — bit-identical to
+// the reference loop.  Rows longer than L edges are cut at chunk boundaries
+// instead; their per-chunk partials ("carries") are added in chunk order by
+// a fix-up kernel, so Zipf hub rows spread over many groups.
 
 #include "common.h"
 
+#include <cstdlib>
 #include <cstring>
 #include <rocprim/device/device_radix_sort.hpp>
 
@@ -43,72 +47,79 @@ struct SpmmArgs {
   int n_rows;
   int nnz;
   int S;          // edges per chunk
+  int L;          // rows longer than L edges are split at chunk boundaries
   int nchunks;
-  int B;          // columns < B read X; >= B read the codebook (GATHER)
+  int B;          // columns < B read X; >= B read X2 (row j - B)
   const float* X;
   int64_t ldx4;   // in float4
+  const float* X2;
+  int64_t ldx24;
   int F4;         // F / 4
-  int D;
-  const int16_t* lcodes;
-  int nb;
-  const float* emb;
-  int64_t ldw;
-  int64_t emb_bstride;
   float* out;
   int64_t ldo4;
   float* carry;   // [nchunks][2][F]
   int* carry_row; // [nchunks]
 };
 
-// Accumulate edges [eb, ee) into acc (float4 x NCH), in order.
-template <int G, int NCH, bool GATHER>
+template <int NCH>
+__host__ __device__ constexpr int spmm_unroll() {
+  return NCH <= 2 ? 8 : (NCH <= 4 ? 4 : 2);
+}
+
+// Accumulate edges [eb, ee) into acc (float4 x NCH), in CSR order.  The
+// group's lanes first load up to G consecutive (col, val) pairs with one
+// coalesced access each, then walk them U at a time: every lane fetches U
+// independent float4 rows (X for j < B; for j >= B the int16 code first,
+// then the codeword's feature half) before adding them in order.
+template <int G, int NCH, bool TWO>
 __device__ __forceinline__ void spmm_segment(const SpmmArgs& a, int eb, int ee, int lg,
                                              float4 (&acc)[NCH]) {
 #pragma unroll
   for (int c = 0; c < NCH; ++c) acc[c] = make_float4(0.f, 0.f, 0.f, 0.f);
   const float4* X4 = reinterpret_cast<const float4*>(a.X);
-  constexpr int U = 4;
-  for (int e = eb; e < ee; e += U) {
-    int jj[U];
-    float ww[U];
+  const float4* Y4 = reinterpret_cast<const float4*>(a.X2);
+  constexpr int U = spmm_unroll<NCH>();
+  for (int base = eb; base < ee; base += G) {
+    const int e = base + lg;
+    const bool ok = e < ee;
+    const int myj = ok ? a.col[e] : -1;
+    const float myw = ok ? a.val[e] : 0.f;
+    const int cnt = min(G, ee - base);
+    for (int k = 0; k < cnt; k += U) {
+      int jj[U];
+      float ww[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const bool ok = e + u < ee;
-      jj[u] = ok ? a.col[e + u] : -1;
-      ww[u] = ok ? a.val[e + u] : 0.f;
-    }
-    float4 v[U][NCH];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int j = jj[u];
-#pragma unroll
-      for (int c = 0; c < NCH; ++c) {
-        const int cc = lg + c * G;
-        float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (j >= 0 && cc < a.F4) {
-          if (!GATHER || j < a.B) {
-            x = X4[(int64_t)j * a.ldx4 + cc];
-          } else {
-            const int col0 = cc * 4;
-            const int br = col0 / a.D, off = col0 - br * a.D;
-            const int code = a.lcodes[(int64_t)(j - a.B) * a.nb + br];
-            x = *reinterpret_cast<const float4*>(a.emb + br * a.emb_bstride +
-                                                 (int64_t)code * a.ldw + off);
-          }
-        }
-        v[u][c] = x;
+      for (int u = 0; u < U; ++u) {
+        const int src = min(k + u, G - 1);
+        const int j = __shfl(myj, src, G);
+        const float w = __shfl(myw, src, G);
+        const bool v = k + u < cnt;
+        jj[u] = v ? j : -1;
+        ww[u] = v ? w : 0.f;
       }
-    }
+      float4 v[U][NCH];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (jj[u] >= 0) {
-        const float w = ww[u];
+      for (int u = 0; u < U; ++u) {
+        const int j = jj[u];
+        const float4* row = (!TWO || j < a.B) ? X4 + (int64_t)j * a.ldx4
+                                              : Y4 + (int64_t)(j - a.B) * a.ldx24;
 #pragma unroll
         for (int c = 0; c < NCH; ++c) {
-          acc[c].x = __fadd_rn(acc[c].x, __fmul_rn(w, v[u][c].x));
-          acc[c].y = __fadd_rn(acc[c].y, __fmul_rn(w, v[u][c].y));
-          acc[c].z = __fadd_rn(acc[c].z, __fmul_rn(w, v[u][c].z));
-          acc[c].w = __fadd_rn(acc[c].w, __fmul_rn(w, v[u][c].w));
+          const int cc = lg + c * G;
+          v[u][c] = (j >= 0 && cc < a.F4) ? row[cc] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (jj[u] >= 0) {
+          const float w = ww[u];
+#pragma unroll
+          for (int c = 0; c < NCH; ++c) {
+            acc[c].x = __fadd_rn(acc[c].x, __fmul_rn(w, v[u][c].x));
+            acc[c].y = __fadd_rn(acc[c].y, __fmul_rn(w, v[u][c].y));
+            acc[c].z = __fadd_rn(acc[c].z, __fmul_rn(w, v[u][c].z));
+            acc[c].w = __fadd_rn(acc[c].w, __fmul_rn(w, v[u][c].w));
+          }
         }
       }
     }
@@ -124,14 +135,38 @@ __device__ __forceinline__ void store_row(float4* dst, int lg, int F4, const flo
   }
 }
 
-template <int G, int NCH, bool GATHER>
+// Row ownership: chunk g owns every row whose first edge lies in
+// [g*S, (g+1)*S) (plus, for the last chunk, trailing empty rows).  A row of at
+// most L edges is summed entirely by its owner, even past the chunk end, so
+// it is bit-identical to spmm_sum's sequential loop; only rows longer than L
+// are cut at chunk boundaries and leave per-chunk partials ("carries").
+// Chunk -> XCD placement (speed only): each XCD receives a contiguous 1/8 of
+// the chunks before the split edge (rows < B: batch rows, whose neighbours are
+// mostly intra-cluster and therefore L2-local) and a contiguous 1/8 of the
+// chunks after it (the out-of-batch rows, whose gathers are mostly random), so
+// neither the L2 locality nor the XCD balance is lost.  Blocks b and b+8
+// share an XCD under the observed round-robin dispatch.
+__device__ __forceinline__ int spmm_chunk_of(int blk, int group, int gpw, int nchunks,
+                                             int split) {
+  const int xcd = blk % kNumXcd, local = blk / kNumXcd;
+  const int c1 = split, c2 = nchunks - split;
+  const int a1 = xcd * c1 / kNumXcd, n1 = (xcd + 1) * c1 / kNumXcd - a1;
+  const int a2 = split + xcd * c2 / kNumXcd, n2 = split + (xcd + 1) * c2 / kNumXcd - a2;
+  const int lc = local * gpw + group;
+  if (lc < n1) return a1 + lc;
+  if (lc < n1 + n2) return a2 + (lc - n1);
+  return -1;
+}
+
+template <int G, int NCH, bool TWO>
 __global__ void __launch_bounds__(kSpmmThreads)
 spmm_merge_kernel(SpmmArgs a) {
   constexpr int GPW = kSpmmThreads / G;  // groups per workgroup
-  const int wg = xcd_remap(blockIdx.x, gridDim.x);
-  const int chunk = wg * GPW + threadIdx.x / G;
   const int lg = threadIdx.x % G;
-  if (chunk >= a.nchunks) return;
+  int split = a.nchunks;
+  if (TWO && a.B < a.n_rows) split = min(a.nchunks, a.rowptr[a.B] / a.S);
+  const int chunk = spmm_chunk_of(blockIdx.x, threadIdx.x / G, GPW, a.nchunks, split);
+  if (chunk < 0) return;
   const int e0 = chunk * a.S;
   const int e1 = min(e0 + a.S, a.nnz);
   const bool last = e1 == a.nnz;
@@ -143,56 +178,200 @@ spmm_merge_kernel(SpmmArgs a) {
   int crow = -1;
   float4 acc[NCH];
   if (i > 0 && a.rowptr[i] > e0) {  // row i-1 started before this chunk
-    const int re = min(a.rowptr[i], e1);
-    spmm_segment<G, NCH, GATHER>(a, e0, re, lg, acc);
-    store_row<G, NCH>(carry4 + (int64_t)chunk * 2 * F4, lg, F4, acc);
-    crow = i - 1;
+    const int rs = a.rowptr[i - 1];
+    if (a.rowptr[i] - rs > a.L) {     // long row: this chunk's piece is a carry
+      const int re = min(a.rowptr[i], e1);
+      spmm_segment<G, NCH, TWO>(a, e0, re, lg, acc);
+      store_row<G, NCH>(carry4 + (int64_t)chunk * 2 * F4, lg, F4, acc);
+      crow = i - 1;
+    }
   }
+  int rb = (i < a.n_rows) ? a.rowptr[i] : 0;
   for (; i < a.n_rows; ++i) {
-    const int rb = a.rowptr[i];
     if (!(rb < e1 || last)) break;
     const int re_full = a.rowptr[i + 1];
-    const int re = min(re_full, e1);
-    spmm_segment<G, NCH, GATHER>(a, rb, re, lg, acc);
-    if (re_full <= e1) {
+    if (re_full - rb <= a.L) {
+      spmm_segment<G, NCH, TWO>(a, rb, re_full, lg, acc);
       store_row<G, NCH>(out4 + (int64_t)i * a.ldo4, lg, F4, acc);
     } else {
-      store_row<G, NCH>(carry4 + ((int64_t)chunk * 2 + 1) * F4, lg, F4, acc);
-      break;
+      const int re = min(re_full, e1);
+      spmm_segment<G, NCH, TWO>(a, rb, re, lg, acc);
+      if (re_full <= e1) {
+        store_row<G, NCH>(out4 + (int64_t)i * a.ldo4, lg, F4, acc);
+      } else {
+        store_row<G, NCH>(carry4 + ((int64_t)chunk * 2 + 1) * F4, lg, F4, acc);
+        break;
+      }
     }
+    rb = re_full;
   }
   if (lg == 0) a.carry_row[chunk] = crow;
 }
 
+// ---------------------------------------------------------------------------
+// Wave-uniform variant for F = 64*V (V = 1, 2, 4): one wave owns a chunk, the
+// edge stream (col, val, row base address) is wave-uniform and lives in
+// scalar registers, and each lane owns V consecutive columns of every row:
+// per edge one vector load of 4*F bytes per wave and 2V VALU (mul, add).
+// ---------------------------------------------------------------------------
+template <int V>
+struct VecT;
+template <>
+struct VecT<1> { using T = float; };
+template <>
+struct VecT<2> { using T = float2; };
+template <>
+struct VecT<4> { using T = float4; };
+
+template <int V>
+__device__ __forceinline__ void vload(const float* p, float (&v)[V]) {
+  if constexpr (V == 1) {
+    v[0] = *p;
+  } else if constexpr (V == 2) {
+    const float2 t = *reinterpret_cast<const float2*>(p);
+    v[0] = t.x; v[1] = t.y;
+  } else {
+    const float4 t = *reinterpret_cast<const float4*>(p);
+    v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+  }
+}
+
+template <int V>
+__device__ __forceinline__ void vstore(float* p, const float (&v)[V]) {
+  if constexpr (V == 1) {
+    *p = v[0];
+  } else if constexpr (V == 2) {
+    *reinterpret_cast<float2*>(p) = make_float2(v[0], v[1]);
+  } else {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  }
+}
+
+__device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
+
+template <int V, bool TWO>
+__device__ __forceinline__ void wave_segment(const SpmmArgs& a, int eb, int ee, int lane,
+                                             float (&acc)[V]) {
+#pragma unroll
+  for (int k = 0; k < V; ++k) acc[k] = 0.f;
+  constexpr int U = V == 4 ? 8 : 16;
+  const int64_t ldx = a.ldx4 * 4, ldx2 = a.ldx24 * 4;
+  for (int e = eb; e < ee; e += U) {
+    int jj[U];
+    float ww[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const bool ok = e + u < ee;   // wave-uniform
+      jj[u] = ok ? uni(a.col[e + u]) : -1;
+      ww[u] = ok ? __builtin_bit_cast(float, uni(__builtin_bit_cast(int, a.val[e + u]))) : 0.f;
+    }
+    float v[U][V];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int j = jj[u];
+      if (j >= 0) {
+        const float* row = (!TWO || j < a.B) ? a.X + (int64_t)j * ldx
+                                             : a.X2 + (int64_t)(j - a.B) * ldx2;
+        vload<V>(row + lane * V, v[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (jj[u] >= 0) {
+#pragma unroll
+        for (int k = 0; k < V; ++k) acc[k] = __fadd_rn(acc[k], __fmul_rn(ww[u], v[u][k]));
+      }
+    }
+  }
+}
+
+template <int V, bool TWO>
+__global__ void __launch_bounds__(kSpmmThreads)
+spmm_wave_kernel(SpmmArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int wave = uni(threadIdx.x >> 6);
+  int split = a.nchunks;
+  if (TWO && a.B < a.n_rows) split = min(a.nchunks, uni(a.rowptr[a.B]) / a.S);
+  const int chunk = spmm_chunk_of(blockIdx.x, wave, kSpmmThreads / 64, a.nchunks, split);
+  if (chunk < 0) return;
+  const int e0 = chunk * a.S;
+  const int e1 = min(e0 + a.S, a.nnz);
+  const bool last = e1 == a.nnz;
+  const int ldo = (int)(a.ldo4 * 4);
+  int i = uni(lower_bound_i32(a.rowptr, a.n_rows, e0));
+  int crow = -1;
+  float acc[V];
+  if (i > 0) {
+    const int ri = uni(a.rowptr[i]);
+    if (ri > e0) {  // row i-1 started before this chunk
+      const int rs = uni(a.rowptr[i - 1]);
+      if (ri - rs > a.L) {
+        const int re = min(ri, e1);
+        wave_segment<V, TWO>(a, e0, re, lane, acc);
+        vstore<V>(a.carry + (int64_t)chunk * 2 * (a.F4 * 4) + lane * V, acc);
+        crow = i - 1;
+      }
+    }
+  }
+  int rb = (i < a.n_rows) ? uni(a.rowptr[i]) : 0;
+  for (; i < a.n_rows; ++i) {
+    if (!(rb < e1 || last)) break;
+    const int re_full = uni(a.rowptr[i + 1]);
+    if (re_full - rb <= a.L) {
+      wave_segment<V, TWO>(a, rb, re_full, lane, acc);
+      vstore<V>(a.out + (int64_t)i * ldo + lane * V, acc);
+    } else {
+      const int re = min(re_full, e1);
+      wave_segment<V, TWO>(a, rb, re, lane, acc);
+      if (re_full <= e1) {
+        vstore<V>(a.out + (int64_t)i * ldo + lane * V, acc);
+      } else {
+        vstore<V>(a.carry + ((int64_t)chunk * 2 + 1) * (a.F4 * 4) + lane * V, acc);
+        break;
+      }
+    }
+    rb = re_full;
+  }
+  if (lane == 0) a.carry_row[chunk] = crow;
+}
+
 // For every row that spans chunks, the chunk where it ends adds the partials:
 // carry_last[start chunk] + carry_first[start+1 .. end] (chunk order).
-template <int G, int NCH>
-__global__ void __launch_bounds__(kSpmmThreads)
+// One wave scans 64 chunks and serves the few that end a spanning row.
+__global__ void __launch_bounds__(256)
 spmm_fixup_kernel(SpmmArgs a) {
-  constexpr int GPW = kSpmmThreads / G;
-  const int chunk = blockIdx.x * GPW + threadIdx.x / G;
-  const int lg = threadIdx.x % G;
-  if (chunk >= a.nchunks) return;
-  const int r = a.carry_row[chunk];
-  if (r < 0) return;
-  const int e1 = min(chunk * a.S + a.S, a.nnz);
-  if (a.rowptr[r + 1] > e1) return;  // not the end chunk of row r
-  const int gs = a.rowptr[r] / a.S;
+  const int lane = threadIdx.x & 63;
+  const int chunk = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 64 + lane;
+  bool need = false;
+  int r = -1;
+  if (chunk < a.nchunks) {
+    r = a.carry_row[chunk];
+    if (r >= 0) {
+      const int e1 = min(chunk * a.S + a.S, a.nnz);
+      need = a.rowptr[r + 1] <= e1;
+    }
+  }
+  unsigned long long mask = __ballot(need);
   const int F4 = a.F4;
   const float4* carry4 = reinterpret_cast<const float4*>(a.carry);
-#pragma unroll
-  for (int c = 0; c < NCH; ++c) {
-    const int cc = lg + c * G;
-    if (cc >= F4) continue;
-    float4 s = carry4[((int64_t)gs * 2 + 1) * F4 + cc];
-    for (int g = gs + 1; g <= chunk; ++g) {
-      const float4 t = carry4[(int64_t)g * 2 * F4 + cc];
-      s.x = __fadd_rn(s.x, t.x);
-      s.y = __fadd_rn(s.y, t.y);
-      s.z = __fadd_rn(s.z, t.z);
-      s.w = __fadd_rn(s.w, t.w);
+  float4* out4 = reinterpret_cast<float4*>(a.out);
+  while (mask) {
+    const int src = __ffsll((long long)mask) - 1;
+    mask &= mask - 1;
+    const int ch = __shfl(chunk, src);
+    const int row = __shfl(r, src);
+    const int gs = a.rowptr[row] / a.S;
+    for (int cc = lane; cc < F4; cc += 64) {
+      float4 s = carry4[((int64_t)gs * 2 + 1) * F4 + cc];
+      for (int g = gs + 1; g <= ch; ++g) {
+        const float4 t = carry4[(int64_t)g * 2 * F4 + cc];
+        s.x = __fadd_rn(s.x, t.x);
+        s.y = __fadd_rn(s.y, t.y);
+        s.z = __fadd_rn(s.z, t.z);
+        s.w = __fadd_rn(s.w, t.w);
+      }
+      out4[(int64_t)row * a.ldo4 + cc] = s;
     }
-    reinterpret_cast<float4*>(a.out)[(int64_t)r * a.ldo4 + cc] = s;
   }
 }
 
@@ -202,15 +381,28 @@ __global__ void zero_rows_kernel(float* out, int64_t ldo, int n_rows, int F) {
   out[(i / F) * ldo + (i % F)] = 0.f;
 }
 
-// lcodes[j][b] = codes[subset[B + j]][b]                         models.py:168
-__global__ void gather_codes_kernel(const int64_t* __restrict__ subset, int B, int nprime,
-                                    const int16_t* __restrict__ codes, int64_t ldc, int nb,
-                                    int16_t* __restrict__ lcodes) {
+// x_first_order[j][b*D + k] = emb_out[b][codes[subset[B + j]][b]][off + k]
+// (models.py:168-173; off = 0 feature half, off = D grad half), and optionally
+// lcodes[j][b] = the code.  Thread per (node, branch); D == 4 stores float4.
+__global__ void gather_codewords_kernel(const int64_t* __restrict__ subset, int B, int nprime,
+                                        const int16_t* __restrict__ codes, int64_t ldc, int nb,
+                                        int D, const float* __restrict__ emb, int ldw,
+                                        int64_t bstride, int off, float* __restrict__ xt,
+                                        int64_t ldt, int16_t* __restrict__ lcodes) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= (int64_t)nprime * nb) return;
   const int64_t j = t / nb;
   const int b = (int)(t % nb);
-  lcodes[t] = codes[subset[B + j] * ldc + b];
+  const int code = codes[subset[B + j] * ldc + b];
+  if (lcodes) lcodes[t] = (int16_t)code;
+  if (!xt) return;
+  const float* src = emb + b * bstride + (int64_t)code * ldw + off;
+  float* dst = xt + j * ldt + (int64_t)b * D;
+  if (D == 4 && ((((uintptr_t)src) | ((uintptr_t)dst)) & 15) == 0) {
+    *reinterpret_cast<float4*>(dst) = *reinterpret_cast<const float4*>(src);
+  } else {
+    for (int k = 0; k < D; ++k) dst[k] = src[k];
+  }
 }
 
 // codes[batch_idx[i]][b] = local[i][b]
@@ -263,7 +455,19 @@ __global__ void transpose_finish_kernel(const int32_t* __restrict__ sorted_cols,
   }
 }
 
-static int spmm_chunk_edges(int F4) { return F4 > 32 ? 64 : 128; }
+static int env_int(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v && *v ? atoi(v) : dflt;
+}
+static int spmm_chunk_edges(int F4) {
+  static const int s_env = env_int("VQGNN_SPMM_S", 0);
+  if (s_env > 0) return s_env;
+  return F4 > 32 ? 32 : 64;
+}
+static int spmm_long_row(int S) {
+  static const int l_env = env_int("VQGNN_SPMM_L", 0);
+  return l_env > 0 ? l_env : 4 * S;
+}
 
 }  // namespace vqgnn
 
@@ -278,24 +482,53 @@ extern "C" size_t vqgnn_spmm_workspace(int32_t n_rows, int64_t nnz, int32_t F) {
          align_up((size_t)nchunks * sizeof(int), 256);
 }
 
-template <int G, int NCH, bool GATHER>
+template <int G, int NCH, bool TWO>
 static void launch_spmm(const SpmmArgs& a, hipStream_t s) {
   constexpr int GPW = kSpmmThreads / G;
-  const int grid = (a.nchunks + GPW - 1) / GPW;
-  hipLaunchKernelGGL((spmm_merge_kernel<G, NCH, GATHER>), dim3(grid), dim3(kSpmmThreads), 0, s, a);
-  hipLaunchKernelGGL((spmm_fixup_kernel<G, NCH>), dim3(grid), dim3(kSpmmThreads), 0, s, a);
+  // per XCD at most ceil(c1/8) + ceil(c2/8) <= ceil(nchunks/8) + 1 chunks
+  const int per_xcd = (a.nchunks + kNumXcd - 1) / kNumXcd + 1;
+  const int grid = kNumXcd * ((per_xcd + GPW - 1) / GPW);
+  hipLaunchKernelGGL((spmm_merge_kernel<G, NCH, TWO>), dim3(grid), dim3(kSpmmThreads), 0, s, a);
+  hipLaunchKernelGGL(spmm_fixup_kernel, dim3((a.nchunks + 255) / 256), dim3(256), 0, s, a);
 }
 
-template <bool GATHER>
+template <int V, bool TWO>
+static void launch_spmm_wave(const SpmmArgs& a, hipStream_t s) {
+  constexpr int WPB = kSpmmThreads / 64;
+  const int per_xcd = (a.nchunks + kNumXcd - 1) / kNumXcd + 1;
+  const int grid = kNumXcd * ((per_xcd + WPB - 1) / WPB);
+  hipLaunchKernelGGL((spmm_wave_kernel<V, TWO>), dim3(grid), dim3(kSpmmThreads), 0, s, a);
+  hipLaunchKernelGGL(spmm_fixup_kernel, dim3((a.nchunks + 255) / 256), dim3(256), 0, s, a);
+}
+
+static int spmm_mode() {
+  static const int m = env_int("VQGNN_SPMM_MODE", 0);  // 0 = merge kernel, 1 = wave-uniform
+  return m;
+}
+
+template <bool TWO>
 static int dispatch_spmm(const SpmmArgs& a, hipStream_t s) {
   const int F4 = a.F4;
-  if (F4 <= 16) launch_spmm<16, 1, GATHER>(a, s);
-  else if (F4 <= 32) launch_spmm<32, 1, GATHER>(a, s);
-  else if (F4 <= 64) launch_spmm<64, 1, GATHER>(a, s);
-  else if (F4 <= 128) launch_spmm<64, 2, GATHER>(a, s);
-  else if (F4 <= 192) launch_spmm<64, 3, GATHER>(a, s);
-  else if (F4 <= 256) launch_spmm<64, 4, GATHER>(a, s);
-  else if (F4 <= 512) launch_spmm<64, 8, GATHER>(a, s);
+  const bool al2 = (((uintptr_t)a.X | (uintptr_t)a.out | (uintptr_t)a.carry) & 7) == 0;
+  if (spmm_mode() == 1 && F4 * 4 == 64 * 2 && al2) {
+    launch_spmm_wave<2, TWO>(a, s);
+    return check_launch("spmm");
+  }
+  if (spmm_mode() == 1 && F4 * 4 == 64 * 4) {
+    launch_spmm_wave<4, TWO>(a, s);
+    return check_launch("spmm");
+  }
+  if (spmm_mode() == 1 && F4 * 4 == 64) {
+    launch_spmm_wave<1, TWO>(a, s);
+    return check_launch("spmm");
+  }
+  if (F4 <= 16) launch_spmm<16, 1, TWO>(a, s);
+  else if (F4 <= 32) launch_spmm<32, 1, TWO>(a, s);
+  else if (F4 <= 64) launch_spmm<64, 1, TWO>(a, s);
+  else if (F4 <= 128) launch_spmm<64, 2, TWO>(a, s);
+  else if (F4 <= 192) launch_spmm<64, 3, TWO>(a, s);
+  else if (F4 <= 256) launch_spmm<64, 4, TWO>(a, s);
+  else if (F4 <= 512) launch_spmm<64, 8, TWO>(a, s);
   else {
     set_error("spmm: F=%d > 2048 not implemented", F4 * 4);
     return VQGNN_ERR_UNSUPPORTED;
@@ -305,14 +538,15 @@ static int dispatch_spmm(const SpmmArgs& a, hipStream_t s) {
 
 extern "C" int vqgnn_spmm(const int32_t* rowptr, const int32_t* col, const float* val,
                           int32_t n_rows, int64_t nnz, int32_t B, const float* X, int64_t ldx,
-                          int32_t F, int32_t D, const int16_t* lcodes, int32_t nb,
-                          const float* emb_out, int32_t ldw, int64_t emb_bstride, float* out,
-                          int64_t ldo, void* workspace, vqgnn_stream_t stream) {
+                          const float* X2, int64_t ldx2, int32_t F, float* out, int64_t ldo,
+                          void* workspace, vqgnn_stream_t stream) {
   clear_error();
   VQGNN_REQUIRE(rowptr && out && n_rows >= 0, "spmm: null pointer");
   VQGNN_REQUIRE(F > 0 && F % 4 == 0, "spmm: F=%d must be a positive multiple of 4", F);
   VQGNN_REQUIRE(ldx % 4 == 0 && ldo % 4 == 0 && ldx >= F && ldo >= F,
                 "spmm: ldx/ldo must be multiples of 4 and >= F");
+  VQGNN_REQUIRE(!X2 || (ldx2 % 4 == 0 && ldx2 >= F && ((uintptr_t)X2 & 15) == 0),
+                "spmm: X2 must be 16-byte aligned with ldx2 a multiple of 4, >= F");
   VQGNN_REQUIRE(((uintptr_t)X & 15) == 0 && ((uintptr_t)out & 15) == 0,
                 "spmm: X/out must be 16-byte aligned");
   VQGNN_REQUIRE(nnz < (int64_t)INT32_MAX, "spmm: nnz >= 2^31");
@@ -325,15 +559,6 @@ extern "C" int vqgnn_spmm(const int32_t* rowptr, const int32_t* col, const float
     return check_launch("spmm(zero)");
   }
   VQGNN_REQUIRE(col && val && X && workspace, "spmm: null pointer");
-  const bool gather = lcodes != nullptr;
-  if (gather) {
-    VQGNN_REQUIRE(D > 0 && D % 4 == 0 && F % D == 0 && nb == F / D,
-                  "spmm: codebook gather needs D %% 4 == 0 and nb == F/D (D=%d F=%d nb=%d)", D, F,
-                  nb);
-    VQGNN_REQUIRE(emb_out && ldw % 4 == 0 && emb_bstride % 4 == 0 &&
-                      ((uintptr_t)emb_out & 15) == 0,
-                  "spmm: codebook must be 16-byte aligned with ldw, stride multiples of 4");
-  }
   SpmmArgs a;
   a.rowptr = rowptr;
   a.col = col;
@@ -342,35 +567,38 @@ extern "C" int vqgnn_spmm(const int32_t* rowptr, const int32_t* col, const float
   a.nnz = (int)nnz;
   a.F4 = F / 4;
   a.S = spmm_chunk_edges(a.F4);
+  a.L = spmm_long_row(a.S);
   a.nchunks = (int)((nnz + a.S - 1) / a.S);
-  a.B = B;
+  a.B = X2 ? B : INT32_MAX;
   a.X = X;
   a.ldx4 = ldx / 4;
-  a.D = D;
-  a.lcodes = lcodes;
-  a.nb = nb;
-  a.emb = emb_out;
-  a.ldw = ldw;
-  a.emb_bstride = emb_bstride;
+  a.X2 = X2;
+  a.ldx24 = X2 ? ldx2 / 4 : 0;
   a.out = out;
   a.ldo4 = ldo / 4;
   a.carry = reinterpret_cast<float*>(workspace);
   a.carry_row = reinterpret_cast<int*>(reinterpret_cast<char*>(workspace) +
                                        align_up((size_t)a.nchunks * 2 * F * sizeof(float), 256));
-  return gather ? dispatch_spmm<true>(a, s) : dispatch_spmm<false>(a, s);
+  return X2 ? dispatch_spmm<true>(a, s) : dispatch_spmm<false>(a, s);
 }
 
-extern "C" int vqgnn_gather_codes(const int64_t* subset, int32_t B, int32_t n,
-                                  const int16_t* codes, int64_t ldc, int32_t nb,
-                                  int16_t* lcodes, vqgnn_stream_t stream) {
+extern "C" int vqgnn_gather_codewords(const int64_t* subset, int32_t B, int32_t n,
+                                      const int16_t* codes, int64_t ldc, int32_t nb, int32_t D,
+                                      const float* emb_out, int32_t ldw, int64_t emb_bstride,
+                                      int32_t col_offset, float* xt, int64_t ldt,
+                                      int16_t* lcodes, vqgnn_stream_t stream) {
   clear_error();
-  VQGNN_REQUIRE(n >= B && B >= 0 && nb > 0 && ldc >= nb, "gather_codes: bad shape");
+  VQGNN_REQUIRE(n >= B && B >= 0 && nb > 0 && ldc >= nb && D > 0, "gather_codewords: bad shape");
   const int64_t tot = (int64_t)(n - B) * nb;
   if (tot == 0) return VQGNN_OK;
-  VQGNN_REQUIRE(subset && codes && lcodes, "gather_codes: null pointer");
-  hipLaunchKernelGGL(gather_codes_kernel, dim3((tot + 255) / 256), dim3(256), 0,
-                     as_stream(stream), subset, B, n - B, codes, ldc, nb, lcodes);
-  return check_launch("gather_codes");
+  VQGNN_REQUIRE(subset && codes && (xt || lcodes), "gather_codewords: null pointer");
+  VQGNN_REQUIRE(!xt || (emb_out && ldt >= (int64_t)nb * D && col_offset >= 0 &&
+                        col_offset + D <= ldw),
+                "gather_codewords: bad codebook / output layout");
+  hipLaunchKernelGGL(gather_codewords_kernel, dim3((tot + 255) / 256), dim3(256), 0,
+                     as_stream(stream), subset, B, n - B, codes, ldc, nb, D, emb_out, ldw,
+                     emb_bstride, col_offset, xt, ldt, lcodes);
+  return check_launch("gather_codewords");
 }
 
 extern "C" int vqgnn_scatter_codes(const int64_t* batch_idx, int32_t B, const int16_t* local,

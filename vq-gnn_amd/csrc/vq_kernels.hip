@@ -15,6 +15,7 @@
 #include "common.h"
 
 #include <cfloat>
+#include <cstdlib>
 #include <cmath>
 
 namespace vqgnn {
@@ -23,84 +24,159 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 // ---------------------------------------------------------------------------
 // 1. BatchNorm column statistics (fp64 sums)          vq.py:162, vq.py:223
+//    Work item = (row, float4 column chunk); X chunks then G chunks.  Each
+//    thread accumulates 8 doubles (sum, sum of squares of 4 columns) over its
+//    rows; the row phases of a workgroup are folded in LDS (fixed order), then
+//    a second kernel folds the chunk partials (fixed order): deterministic.
 // ---------------------------------------------------------------------------
 constexpr int kStatsThreads = 256;
-constexpr int kStatsMaxChunks = 1024;
+constexpr int kStatsMaxChunks = 512;
 
-static int stats_chunks(int B) {
-  int c = (B + 255) / 256;
+static int stats_chunks(int B, int C4) {
+  const int rows_per_iter = C4 >= kStatsThreads ? 1 : kStatsThreads / C4;
+  int c = (B + rows_per_iter * 8 - 1) / (rows_per_iter * 8);
   return c < 1 ? 1 : (c > kStatsMaxChunks ? kStatsMaxChunks : c);
 }
 
-// Grid: chunks of rows.  Thread t handles column (t % C) for rows of phase t / C
-// (C <= 256) or columns t, t+256, ... (C > 256).  Partials [chunk][2][C].
 __global__ void __launch_bounds__(kStatsThreads)
 bn_stats_partial_kernel(const float* __restrict__ X, int64_t ldx,
                         const float* __restrict__ G, int64_t ldg,
-                        int B, int F, int C, int rows_per_chunk,
+                        int B, int F4, int C4, int rows_per_chunk,
                         double* __restrict__ part) {
+  __shared__ double red[kStatsThreads][9];  // 8 sums (+1 pad vs bank conflicts)
+  const int t = threadIdx.x;
+  const int r0 = blockIdx.x * rows_per_chunk;
+  const int r1 = min(B, r0 + rows_per_chunk);
+  const int C = C4 * 4;
+  double* out = part + (int64_t)blockIdx.x * 2 * C;
+  const float4* X4 = reinterpret_cast<const float4*>(X);
+  const float4* G4 = reinterpret_cast<const float4*>(G);
+  const int64_t ldx4 = ldx / 4, ldg4 = ldg / 4;
+  const int phases = C4 >= kStatsThreads ? 1 : kStatsThreads / C4;
+  for (int cbase = 0; cbase < C4; cbase += kStatsThreads) {
+    const int c4 = cbase + (C4 >= kStatsThreads ? t : t % C4);
+    const int ph = C4 >= kStatsThreads ? 0 : t / C4;
+    double s[4] = {0, 0, 0, 0}, q[4] = {0, 0, 0, 0};
+    if (ph < phases && c4 < C4) {
+      const float4* base = c4 < F4 ? X4 + c4 : G4 + (c4 - F4);
+      const int64_t ld = c4 < F4 ? ldx4 : ldg4;
+      int r = r0 + ph;
+      for (; r + phases < r1; r += 2 * phases) {
+        const float4 a = base[(int64_t)r * ld];
+        const float4 b = base[(int64_t)(r + phases) * ld];
+        const double av[4] = {a.x, a.y, a.z, a.w}, bv[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          s[k] += av[k];
+          q[k] = fma(av[k], av[k], q[k]);
+          s[k] += bv[k];
+          q[k] = fma(bv[k], bv[k], q[k]);
+        }
+      }
+      if (r < r1) {
+        const float4 a = base[(int64_t)r * ld];
+        const double av[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          s[k] += av[k];
+          q[k] = fma(av[k], av[k], q[k]);
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      red[t][k] = s[k];
+      red[t][4 + k] = q[k];
+    }
+    __syncthreads();
+    if (ph == 0 && c4 < C4) {
+      double a[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) a[k] = red[t][k];
+      for (int p = 1; p < phases; ++p) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) a[k] += red[p * C4 + t][k];
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        out[c4 * 4 + k] = a[k];
+        out[C + c4 * 4 + k] = a[4 + k];
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// Scalar variant for column sets that are not float4-aligned (e.g. D = 2 on
+// one branch): thread t -> column t % C, row phase t / C.
+__global__ void __launch_bounds__(kStatsThreads)
+bn_stats_partial_scalar_kernel(const float* __restrict__ X, int64_t ldx,
+                               const float* __restrict__ G, int64_t ldg, int B, int F, int C,
+                               int rows_per_chunk, double* __restrict__ part) {
   __shared__ double red[2][kStatsThreads];
   const int t = threadIdx.x;
   const int r0 = blockIdx.x * rows_per_chunk;
   const int r1 = min(B, r0 + rows_per_chunk);
   double* out = part + (int64_t)blockIdx.x * 2 * C;
-  if (C <= kStatsThreads) {
-    const int phases = kStatsThreads / C;
-    const int c = t % C, ph = t / C;
-    double s = 0.0, s2 = 0.0;
+  for (int cbase = 0; cbase < C; cbase += kStatsThreads) {
+    const int cols = min(C - cbase, kStatsThreads);
+    const int phases = kStatsThreads / cols;
+    const int c = cbase + t % cols, ph = t / cols;
+    double sm = 0.0, sq = 0.0;
     if (ph < phases) {
       const float* base = (c < F) ? (X + c) : (G + (c - F));
       const int64_t ld = (c < F) ? ldx : ldg;
       for (int r = r0 + ph; r < r1; r += phases) {
         const double v = (double)base[(int64_t)r * ld];
-        s += v;
-        s2 = fma(v, v, s2);
+        sm += v;
+        sq = fma(v, v, sq);
       }
     }
-    red[0][t] = s;
-    red[1][t] = s2;
+    red[0][t] = sm;
+    red[1][t] = sq;
     __syncthreads();
-    if (t < C) {
+    if (t < cols) {
       double a = 0.0, b = 0.0;
       for (int p = 0; p < phases; ++p) {
-        a += red[0][p * C + t];
-        b += red[1][p * C + t];
+        a += red[0][p * cols + t];
+        b += red[1][p * cols + t];
       }
-      out[t] = a;
-      out[C + t] = b;
+      out[cbase + t] = a;
+      out[C + cbase + t] = b;
     }
-  } else {
-    for (int c = t; c < C; c += kStatsThreads) {
-      const float* base = (c < F) ? (X + c) : (G + (c - F));
-      const int64_t ld = (c < F) ? ldx : ldg;
-      double s = 0.0, s2 = 0.0;
-      for (int r = r0; r < r1; ++r) {
-        const double v = (double)base[(int64_t)r * ld];
-        s += v;
-        s2 = fma(v, v, s2);
-      }
-      out[c] = s;
-      out[C + c] = s2;
-    }
+    __syncthreads();
   }
 }
 
-// Sum partials in chunk order (deterministic) -> sums[4][F] (sx, sxx, sg, sgg).
-__global__ void bn_stats_reduce_kernel(const double* __restrict__ part, int chunks,
-                                       int F, int C, double* __restrict__ sums) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+// Fold chunk partials (16 phases per column, fixed tree) -> sums[4][F].
+__global__ void __launch_bounds__(256)
+bn_stats_reduce_kernel(const double* __restrict__ part, int chunks, int F, int C,
+                       double* __restrict__ sums) {
+  __shared__ double red[2][16][17];
+  const int cl = threadIdx.x & 15, ph = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cl;
   double a = 0.0, b = 0.0;
-  for (int p = 0; p < chunks; ++p) {
-    a += part[(int64_t)p * 2 * C + c];
-    b += part[(int64_t)p * 2 * C + C + c];
+  if (c < C) {
+    for (int p = ph; p < chunks; p += 16) {
+      a += part[(int64_t)p * 2 * C + c];
+      b += part[(int64_t)p * 2 * C + C + c];
+    }
   }
-  if (c < F) {
-    sums[c] = a;
-    sums[F + c] = b;
-  } else {
-    sums[2 * F + (c - F)] = a;
-    sums[3 * F + (c - F)] = b;
+  red[0][ph][cl] = a;
+  red[1][ph][cl] = b;
+  __syncthreads();
+  if (ph == 0 && c < C) {
+    for (int p = 1; p < 16; ++p) {
+      a += red[0][p][cl];
+      b += red[1][p][cl];
+    }
+    if (c < F) {
+      sums[c] = a;
+      sums[F + c] = b;
+    } else {
+      sums[2 * F + (c - F)] = a;
+      sums[3 * F + (c - F)] = b;
+    }
   }
 }
 
@@ -169,51 +245,35 @@ __global__ void bn_finalize_kernel(const double* __restrict__ sums, int64_t n, i
 // ---------------------------------------------------------------------------
 // 3. PQ assignment on MFMA f32 (v_mfma_f32_16x16x4_f32)
 //
-// Workgroup = (branch b, row range); 4 waves, each wave owns 64 rows per
-// iteration as 4 groups of 16.  MFMA tile: A = 16 codewords x 4 k (from LDS),
-// B = 4 k x 16 rows (registers), D[16 codewords][16 rows]:
+// Workgroup = (branch b, row part); 16 waves.  The branch's codebook is staged
+// in LDS once and reused for every row of the part; each wave owns 64 rows
+// per iteration (4 groups of 16) and prefetches the next iteration's raw rows
+// into registers while the MFMA sweep runs.  MFMA tile: A = 16 codewords x 4 k
+// (LDS), B = 4 k x 16 rows (registers), D[16 codewords][16 rows]:
 //   lane l: q = l>>4, j = l&15; A operand E[m0+j][kc*4+q], B operand
 //   Xn[row j][kc*4+q]; D reg r = codeword m0 + 4q + r for row j.
 // Per lane a running (best, index) over its codewords in increasing order with
 // strict '<' keeps the first index; the 4 q-lanes of a row merge with
 // (d, index) lexicographic order -> torch.argmin semantics (first index).
 //
-// LDS: codebook chunk as [q][m][KC] floats (q stride padded so the 16-lane
-// halves of a ds_read hit disjoint banks), |e|^2 per codeword, and (fused EMA)
-// the per-codeword count + sum of normalised x accumulated with ds_add.
+// LDS: codebook as [q][m][KC] floats (q stride padded so the 16-lane halves of
+// a ds_read hit disjoint banks), |e|^2 per codeword, and (fused EMA) the
+// per-codeword count + sum of normalised x accumulated with ds_add_f32; the
+// accumulators leave as one partial slab per (part, branch) — a handful of
+// parts, summed in order by the finalize kernel (deterministic).
 // ---------------------------------------------------------------------------
-constexpr int kAssignThreads = 256;
-constexpr int kRowsPerIter = 256;      // 4 waves x 64 rows
-constexpr int kTargetWgs = 2048;       // ~8 per CU
-constexpr int kMaxChunk = 1024;        // codewords per LDS chunk
-constexpr int kFuseEmaMaxM = 1024;     // fused EMA accumulators when M <= this
+constexpr int kAssignThreads = 1024;       // non-fused EMA kernel block
+constexpr size_t kLdsBudget = 160 * 1024;
 
 struct AssignGeom {
-  int iters_per_wg;   // row iterations (256 rows each) per workgroup
-  int ranges;         // row ranges per branch (= partial slabs)
-  int wgs;            // total workgroups = ranges * nb
+  int parts;          // row parts per branch (= EMA partial slabs)
+  int rows_per_part;
+  int iters;          // 1024-row iterations per part
   int mpad;           // M rounded up to 16
   int chunk;          // codewords per LDS chunk (multiple of 16)
   int kc;             // k-chunks of 4 (W padded to 4*kc)
   bool fused;         // EMA statistics accumulated in the assign kernel
 };
-
-static AssignGeom assign_geom(int B, int nb, int M, int W) {
-  AssignGeom g;
-  const int row_blocks = (B + kRowsPerIter - 1) / kRowsPerIter;
-  int target_ranges = (kTargetWgs + nb - 1) / nb;
-  if (target_ranges < 1) target_ranges = 1;
-  if (target_ranges > row_blocks) target_ranges = row_blocks;
-  g.iters_per_wg = (row_blocks + target_ranges - 1) / target_ranges;
-  g.ranges = (row_blocks + g.iters_per_wg - 1) / g.iters_per_wg;
-  if (g.ranges < 1) g.ranges = 1;
-  g.wgs = g.ranges * nb;
-  g.mpad = (M + 15) / 16 * 16;
-  g.chunk = g.mpad < kMaxChunk ? g.mpad : kMaxChunk;
-  g.kc = W <= 4 ? 1 : (W <= 8 ? 2 : 4);
-  g.fused = M <= kFuseEmaMaxM;
-  return g;
-}
 
 template <int KC>
 __host__ __device__ constexpr int q_pad_bytes() {
@@ -225,12 +285,48 @@ __host__ __device__ inline int q_stride_floats(int chunk) {
   return chunk * KC + q_pad_bytes<KC>() / 4;
 }
 
-template <int KC>
-static size_t assign_lds_bytes(const AssignGeom& g, int M, int W) {
-  size_t b = (size_t)4 * q_stride_floats<KC>(g.chunk) * 4;  // codebook chunk
-  b += (size_t)g.chunk * 4;                                   // |e|^2
-  if (g.fused) b += (size_t)M * (W + 1) * 4;                  // EMA accumulators
-  return b;
+static size_t cb_lds_bytes(int kc, int chunk) {
+  const int pad = kc == 1 ? 64 : (kc == 2 ? 128 : 0);
+  return (size_t)4 * (chunk * kc * 4 + pad) + (size_t)chunk * 4;
+}
+
+static int env_int_vq(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v && *v ? atoi(v) : dflt;
+}
+static int asg_waves() {
+  static const int w = env_int_vq("VQGNN_ASG_WV", 8) == 16 ? 16 : 8;
+  return w;
+}
+static int asg_ng() {
+  static const int g = env_int_vq("VQGNN_ASG_NG", 2) == 4 ? 4 : 2;
+  return g;
+}
+
+static AssignGeom assign_geom(int B, int nb, int M, int W) {
+  AssignGeom g;
+  g.kc = W <= 4 ? 1 : (W <= 8 ? 2 : 4);
+  g.mpad = (M + 15) / 16 * 16;
+  const size_t acc = (size_t)M * (W + 1) * 4;
+  // fused EMA when codebook + accumulators share the LDS
+  g.fused = cb_lds_bytes(g.kc, g.mpad) + acc <= kLdsBudget;
+  if (g.fused) {
+    g.chunk = g.mpad;
+  } else {
+    int c = g.mpad;
+    while (c > 16 && cb_lds_bytes(g.kc, c) > kLdsBudget) c = (c / 2 + 15) / 16 * 16;
+    g.chunk = c;
+  }
+  const int rows_per_iter = asg_waves() * 16 * asg_ng();
+  const int row_blocks = (B + rows_per_iter - 1) / rows_per_iter;
+  const int target = env_int_vq("VQGNN_ASG_TARGET", asg_waves() == 8 ? 768 : 256);
+  int parts = (target + nb - 1) / nb;
+  if (parts < 1) parts = 1;
+  if (parts > row_blocks) parts = row_blocks;
+  g.parts = parts;
+  g.rows_per_part = (B + parts - 1) / parts;
+  g.iters = (g.rows_per_part + rows_per_iter - 1) / rows_per_iter;
+  return g;
 }
 
 template <int KC>
@@ -257,15 +353,45 @@ __device__ __forceinline__ Frag<KC> lds_frag(const float* p) {
   return f;
 }
 
-__device__ __forceinline__ float pick4(const float (&a)[4], int i) {
-  return i == 0 ? a[0] : (i == 1 ? a[1] : (i == 2 ? a[2] : a[3]));
-}
-__device__ __forceinline__ int pick4(const int (&a)[4], int i) {
-  return i == 0 ? a[0] : (i == 1 ? a[1] : (i == 2 ? a[2] : a[3]));
+template <int NG>
+__device__ __forceinline__ int pickn(const int (&a)[NG], int i) {
+  int v = a[0];
+#pragma unroll
+  for (int g = 1; g < NG; ++g) v = (i == g) ? a[g] : v;
+  return v;
 }
 
-template <int KC, bool FUSED>
-__global__ void __launch_bounds__(kAssignThreads)
+// stage codebook rows [mc0, mc0+chunk) of E into LDS (cb [4][qs], se [chunk])
+template <int KC, int NT>
+__device__ __forceinline__ void stage_chunk(const float* __restrict__ E, int ldw, int W,
+                                            int mc0, int mcount, int chunk, int qs,
+                                            float* cb, float* se, int tid) {
+  for (int m = tid; m < chunk; m += NT) {
+    float e[4 * KC];
+    const bool mv = m < mcount;
+#pragma unroll
+    for (int k = 0; k < 4 * KC; ++k) e[k] = (mv && k < W) ? E[(int64_t)(mc0 + m) * ldw + k] : 0.f;
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4 * KC; ++k)
+      if (k < W) s = (k == 0) ? __fmul_rn(e[k], e[k]) : __fadd_rn(s, __fmul_rn(e[k], e[k]));
+    se[m] = mv ? s : INFINITY;
+#pragma unroll
+    for (int qq = 0; qq < 4; ++qq) {
+      if constexpr (KC == 1) {
+        cb[qq * qs + m] = e[qq];
+      } else if constexpr (KC == 2) {
+        *reinterpret_cast<float2*>(cb + qq * qs + m * 2) = make_float2(e[qq], e[4 + qq]);
+      } else {
+        *reinterpret_cast<float4*>(cb + qq * qs + m * 4) =
+            make_float4(e[qq], e[4 + qq], e[8 + qq], e[12 + qq]);
+      }
+    }
+  }
+}
+
+template <int KC, bool FUSED, int NG, int WV>
+__global__ void __launch_bounds__(WV * 64)
 vq_assign_kernel(const float* __restrict__ X, int64_t ldx,
                  const float* __restrict__ Gr, int64_t ldg,
                  int B, int nb, int D, int M, int W,
@@ -274,12 +400,13 @@ vq_assign_kernel(const float* __restrict__ X, int64_t ldx,
                  int64_t* __restrict__ idx_out, int16_t* __restrict__ codes, int64_t ldc,
                  const int64_t* __restrict__ batch_idx,
                  int* __restrict__ idx32, float* __restrict__ partial,
-                 int iters_per_wg, int ranges, int chunk) {
+                 int rows_per_part, int chunk) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  constexpr int NT = WV * 64;
   const int F = nb * D;
   const int wg = xcd_remap(blockIdx.x, gridDim.x);
   const int b = wg % nb;
-  const int range = wg / nb;
+  const int part = wg / nb;
   const int qs = q_stride_floats<KC>(chunk);
   float* cb = smem;                       // [4][qs]
   float* se = smem + 4 * qs;              // [chunk]
@@ -288,49 +415,87 @@ vq_assign_kernel(const float* __restrict__ X, int64_t ldx,
   const int lane = tid & 63, wave = tid >> 6;
   const int q = lane >> 4, j = lane & 15;
   const float* E = emb + (int64_t)b * emb_bstride;
+  const int nchunks = (M + chunk - 1) / chunk;
 
   if constexpr (FUSED) {
-    for (int i = tid; i < M * (W + 1); i += kAssignThreads) acc[i] = 0.f;
+    for (int i = tid; i < M * (W + 1); i += NT) acc[i] = 0.f;
   }
+  if (nchunks == 1) stage_chunk<KC, NT>(E, ldw, W, 0, M, chunk, qs, cb, se, tid);
 
   // per-column normalisation coefficients for this lane's k values
   float al[KC], be[KC];
   bool isg[KC], kval[KC];
+  int colx[KC];
 #pragma unroll
   for (int kc = 0; kc < KC; ++kc) {
     const int k = kc * 4 + q;
     kval[kc] = k < W;
     isg[kc] = k >= D;
     const int c = isg[kc] ? (b * D + (k - D)) : (b * D + k);
+    colx[kc] = c;
     al[kc] = kval[kc] ? coef[(isg[kc] ? 2 * F : 0) + c] : 0.f;
     be[kc] = kval[kc] ? coef[(isg[kc] ? 3 * F : F) + c] : 0.f;
   }
 
-  const int nchunks = (M + chunk - 1) / chunk;
-  const int row_begin = range * iters_per_wg * kRowsPerIter;
+  const int part_begin = part * rows_per_part;
+  const int part_end = min(B, part_begin + rows_per_part);
 
-  for (int it = 0; it < iters_per_wg; ++it) {
-    const int row0 = row_begin + it * kRowsPerIter + wave * 64;
-    // ---- load + normalise this wave's 64 rows (4 groups of 16) ----
-    float xk[4][KC];
-    float sx[4];
-    bool rv[4];
+  // raw row values for one iteration: lane (q, j) of group g holds row
+  // row0 + 16g + j, k = kc*4 + q
+  constexpr int RPW = 16 * NG;                 // rows per wave per iteration
+  constexpr int RPI = WV * RPW;                // rows per workgroup iteration
+  auto load_rows = [&](int it, float (&raw)[NG][KC]) {
+    const int row0 = part_begin + it * RPI + wave * RPW;
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
+    for (int g = 0; g < NG; ++g) {
       const int row = row0 + g * 16 + j;
-      rv[g] = row < B;
+      const bool ok = row < part_end;
+#pragma unroll
+      for (int kc = 0; kc < KC; ++kc) {
+        float v = 0.f;
+        if (ok && kval[kc])
+          v = isg[kc] ? Gr[(int64_t)row * ldg + colx[kc]] : X[(int64_t)row * ldx + colx[kc]];
+        raw[g][kc] = v;
+      }
+    }
+  };
+
+  float nxt[NG][KC];
+  int64_t nbi = -1;                       // batch_idx of this lane's output row
+  auto load_bidx = [&](int it) {
+    const int row = part_begin + it * RPI + wave * RPW + q * 16 + j;
+    return (codes && q < NG && row < part_end) ? batch_idx[row] : (int64_t)-1;
+  };
+  load_rows(0, nxt);
+  nbi = load_bidx(0);
+  if (nchunks == 1) __syncthreads();
+
+  const int n_iters = (part_end - part_begin + RPI - 1) / RPI;
+  for (int it = 0; it < n_iters; ++it) {
+    const int row0 = part_begin + it * RPI + wave * RPW;
+    float xk[NG][KC];
+    float sx[NG];
+    bool rv[NG];
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      rv[g] = row0 + g * 16 + j < part_end;
 #pragma unroll
       for (int kc = 0; kc < KC; ++kc) {
         float v = 0.f;
         if (rv[g] && kval[kc]) {
-          const int k = kc * 4 + q;
-          const float raw = isg[kc] ? Gr[(int64_t)row * ldg + b * D + (k - D)]
-                                    : X[(int64_t)row * ldx + b * D + k];
-          v = fmaf(raw, al[kc], be[kc]);        // BatchNorm1d (ATen: x*alpha+beta fused)
-          if (isg[kc]) v = __fmul_rn(v, grad_scale);  // vq.py:224
+          v = fmaf(nxt[g][kc], al[kc], be[kc]);             // BatchNorm1d (ATen: fma)
+          if (isg[kc]) v = __fmul_rn(v, grad_scale);        // vq.py:224
         }
         xk[g][kc] = v;
       }
+    }
+    const int64_t cur_bi = nbi;
+    if (it + 1 < n_iters) {                                // prefetch under the MFMA sweep
+      load_rows(it + 1, nxt);
+      nbi = load_bidx(it + 1);
+    }
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
       // |x|^2 summed sequentially over k = 0..W-1 (torch.sum(x**2, dim=1))
       float s = 0.f;
 #pragma unroll
@@ -341,10 +506,10 @@ vq_assign_kernel(const float* __restrict__ X, int64_t ldx,
       sx[g] = s;
     }
 
-    float best[4];
-    int bidx[4];
+    float best[NG];
+    int bidx[NG];
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
+    for (int g = 0; g < NG; ++g) {
       best[g] = INFINITY;
       bidx[g] = 0;
     }
@@ -352,35 +517,24 @@ vq_assign_kernel(const float* __restrict__ X, int64_t ldx,
     for (int ch = 0; ch < nchunks; ++ch) {
       const int mc0 = ch * chunk;
       const int mcount = min(chunk, M - mc0);
-      __syncthreads();
-      // stage chunk: cb[q][m][kc] = E[mc0+m][kc*4+q] (0 beyond W / M), se[m]
-      for (int m = tid; m < chunk; m += kAssignThreads) {
-        float e[4 * KC];
-        float s = 0.f;
-        const bool mv = m < mcount;
-#pragma unroll
-        for (int k = 0; k < 4 * KC; ++k) {
-          e[k] = (mv && k < W) ? E[(int64_t)(mc0 + m) * ldw + k] : 0.f;
-        }
-#pragma unroll
-        for (int k = 0; k < 4 * KC; ++k)
-          if (k < W) s = (k == 0) ? __fmul_rn(e[k], e[k]) : __fadd_rn(s, __fmul_rn(e[k], e[k]));
-        se[m] = mv ? s : INFINITY;
-#pragma unroll
-        for (int qq = 0; qq < 4; ++qq) {
-#pragma unroll
-          for (int kc = 0; kc < KC; ++kc) cb[qq * qs + m * KC + kc] = e[kc * 4 + qq];
-        }
+      if (nchunks > 1) {
+        __syncthreads();
+        stage_chunk<KC, NT>(E, ldw, W, mc0, mcount, chunk, qs, cb, se, tid);
+        __syncthreads();
       }
-      __syncthreads();
-
       const float* cbq = cb + q * qs;
+      // operands of the next tile are read while this tile computes
+      Frag<KC> a_nx = lds_frag<KC>(cbq + j * KC);
+      float4 s_nx = *reinterpret_cast<const float4*>(se + 4 * q);
       for (int m0 = 0; m0 < mcount; m0 += 16) {
-        const Frag<KC> a = lds_frag<KC>(cbq + (m0 + j) * KC);
-        const float4 s4 = *reinterpret_cast<const float4*>(se + m0 + 4 * q);
-        floatx4 d[4];
+        const Frag<KC> a = a_nx;
+        const float4 s4 = s_nx;
+        const int mn = min(m0 + 16, chunk - 16);   // in-bounds (staged up to chunk)
+        a_nx = lds_frag<KC>(cbq + (mn + j) * KC);
+        s_nx = *reinterpret_cast<const float4*>(se + mn + 4 * q);
+        floatx4 d[NG];
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
+        for (int g = 0; g < NG; ++g) {
           d[g] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
           for (int kc = 0; kc < KC; ++kc)
@@ -389,7 +543,7 @@ vq_assign_kernel(const float* __restrict__ X, int64_t ldx,
         const int mb = mc0 + m0 + 4 * q;
         const float sev[4] = {s4.x, s4.y, s4.z, s4.w};
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
+        for (int g = 0; g < NG; ++g) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const float dist = fmaf(-2.f, d[g][r], __fadd_rn(sx[g], sev[r]));
@@ -403,7 +557,7 @@ vq_assign_kernel(const float* __restrict__ X, int64_t ldx,
 
     // ---- merge the 4 q-lanes of each row: (d, idx) lexicographic ----
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
+    for (int g = 0; g < NG; ++g) {
 #pragma unroll
       for (int off = 16; off <= 32; off <<= 1) {
         const float od = __shfl_xor(best[g], off);
@@ -415,19 +569,19 @@ vq_assign_kernel(const float* __restrict__ X, int64_t ldx,
     }
 
     // ---- outputs: lane (q, j) writes group q's row j ----
-    {
+    if (q < NG) {
       const int row = row0 + q * 16 + j;
-      if (row < B) {
-        const int m = pick4(bidx, q);
+      if (row < part_end) {
+        const int m = pickn<NG>(bidx, q);
         if (idx_out) idx_out[(int64_t)b * B + row] = (int64_t)m;
         if (idx32) idx32[(int64_t)b * B + row] = m;
-        if (codes) codes[batch_idx[row] * ldc + b] = (int16_t)m;
+        if (codes) codes[cur_bi * ldc + b] = (int16_t)m;
       }
     }
 
     if constexpr (FUSED) {
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
+      for (int g = 0; g < NG; ++g) {
         if (rv[g]) {
           float* a = acc + bidx[g] * (W + 1);
           if (q == 0) atomicAdd(a, 1.0f);
@@ -441,67 +595,70 @@ vq_assign_kernel(const float* __restrict__ X, int64_t ldx,
 
   if constexpr (FUSED) {
     __syncthreads();
-    float* out = partial + ((int64_t)range * nb + b) * M * (W + 1);
-    for (int i = tid; i < M * (W + 1); i += kAssignThreads) out[i] = acc[i];
+    float* out = partial + ((int64_t)part * nb + b) * M * (W + 1);
+    for (int i = tid; i < M * (W + 1); i += NT) out[i] = acc[i];
   }
 }
 
-// Separate EMA statistics (M above the fused limit): LDS accumulators for the
-// whole codebook of one branch; rows re-read and re-normalised.
-template <int KC>
+// Separate EMA statistics (codebook too large to share the LDS with the
+// accumulators): LDS accumulators for the whole codebook of one branch; rows
+// re-read and re-normalised.  use_lds == 0: global atomics into partial
+// (caller zeroes it; single slab).
 __global__ void __launch_bounds__(kAssignThreads)
 vq_ema_partial_kernel(const float* __restrict__ X, int64_t ldx,
                       const float* __restrict__ Gr, int64_t ldg,
                       int B, int nb, int D, int M, int W,
                       const float* __restrict__ coef, float grad_scale,
                       const int* __restrict__ idx32, float* __restrict__ partial,
-                      int iters_per_wg, int use_lds) {
+                      int rows_per_part, int use_lds) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int F = nb * D;
   const int wg = xcd_remap(blockIdx.x, gridDim.x);
   const int b = wg % nb;
-  const int range = wg / nb;
+  const int part = wg / nb;
   const int tid = threadIdx.x;
   float* acc = use_lds ? smem : (partial + (int64_t)b * M * (W + 1));
   if (use_lds) {
     for (int i = tid; i < M * (W + 1); i += kAssignThreads) acc[i] = 0.f;
     __syncthreads();
   }
-  const int row_begin = range * iters_per_wg * kRowsPerIter;
-  const int row_end = min(B, row_begin + iters_per_wg * kRowsPerIter);
-  // thread -> (row phase, k); W + 1 work slots per row (count + W values)
-  for (int r = row_begin + tid / (W + 1); r < row_end; r += kAssignThreads / (W + 1)) {
-    if (tid / (W + 1) >= kAssignThreads / (W + 1)) break;
-    const int k1 = tid % (W + 1);
-    const int m = idx32[(int64_t)b * B + r];
-    float* a = acc + m * (W + 1);
-    if (k1 == 0) {
-      atomicAdd(a, 1.0f);
-    } else {
-      const int k = k1 - 1;
-      const bool g = k >= D;
-      const int c = g ? b * D + (k - D) : b * D + k;
-      const float raw = g ? Gr[(int64_t)r * ldg + c] : X[(int64_t)r * ldx + c];
-      float v = fmaf(raw, coef[(g ? 2 * F : 0) + c], coef[(g ? 3 * F : F) + c]);
-      if (g) v = __fmul_rn(v, grad_scale);
-      atomicAdd(a + k1, v);
+  const int row_begin = part * rows_per_part;
+  const int row_end = min(B, row_begin + rows_per_part);
+  const int slots = W + 1;
+  const int rows_per_pass = kAssignThreads / slots;
+  const int rph = tid / slots, k1 = tid % slots;
+  if (rph < rows_per_pass) {
+    for (int r = row_begin + rph; r < row_end; r += rows_per_pass) {
+      const int m = idx32[(int64_t)b * B + r];
+      float* a = acc + m * (W + 1);
+      if (k1 == 0) {
+        atomicAdd(a, 1.0f);
+      } else {
+        const int k = k1 - 1;
+        const bool g = k >= D;
+        const int c = g ? b * D + (k - D) : b * D + k;
+        const float raw = g ? Gr[(int64_t)r * ldg + c] : X[(int64_t)r * ldx + c];
+        float v = fmaf(raw, coef[(g ? 2 * F : 0) + c], coef[(g ? 3 * F : F) + c]);
+        if (g) v = __fmul_rn(v, grad_scale);
+        atomicAdd(a + k1, v);
+      }
     }
   }
   if (use_lds) {
     __syncthreads();
-    float* out = partial + ((int64_t)range * nb + b) * M * (W + 1);
+    float* out = partial + ((int64_t)part * nb + b) * M * (W + 1);
     for (int i = tid; i < M * (W + 1); i += kAssignThreads) out[i] = acc[i];
   }
 }
 
-// stats[b][m][c] = sum over ranges (in order) of partial[range][b][m][c]
-__global__ void vq_ema_reduce_kernel(const float* __restrict__ partial, int ranges,
-                                     int64_t per_range, float* __restrict__ stats) {
+// out[i] = sum over parts (in order) of parts[p][i]
+__global__ void vq_ema_reduce_kernel(const float* __restrict__ parts, int nparts,
+                                     int64_t per_part, float* __restrict__ out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= per_range) return;
-  float s = 0.f;
-  for (int p = 0; p < ranges; ++p) s = __fadd_rn(s, partial[(int64_t)p * per_range + i]);
-  stats[i] = s;
+  if (i >= per_part) return;
+  float s = parts[i];
+  for (int p = 1; p < nparts; ++p) s = __fadd_rn(s, parts[(int64_t)p * per_part + i]);
+  out[i] = s;
 }
 
 // ---------------------------------------------------------------------------
@@ -510,7 +667,8 @@ __global__ void vq_ema_reduce_kernel(const float* __restrict__ partial, int rang
 constexpr int kFinThreads = 256;
 
 __global__ void __launch_bounds__(kFinThreads)
-vq_ema_finalize_kernel(const float* __restrict__ stats, int M, int D, int W, int ldw,
+vq_ema_finalize_kernel(const float* __restrict__ stats, int nparts, int64_t part_stride,
+                       int M, int D, int W, int ldw,
                        float decay, int laplace, float grad_scale, float epsilon,
                        float* __restrict__ cluster_size, int64_t cs_bstride,
                        float* __restrict__ ema_w, float* __restrict__ emb,
@@ -523,6 +681,12 @@ vq_ema_finalize_kernel(const float* __restrict__ stats, int M, int D, int W, int
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
   const float* st = stats + (int64_t)b * M * (W + 1);
+  // statistics = sum of the per-part slabs, in part order (deterministic)
+  auto stat = [&](int64_t i) {
+    float v = st[i];
+    for (int p = 1; p < nparts; ++p) v = __fadd_rn(v, st[(int64_t)p * part_stride + i]);
+    return v;
+  };
   float* cs = cluster_size + (int64_t)b * cs_bstride;
   float* ew = ema_w + (int64_t)b * emb_bstride;
   float* e = emb + (int64_t)b * emb_bstride;
@@ -532,7 +696,7 @@ vq_ema_finalize_kernel(const float* __restrict__ stats, int M, int D, int W, int
 
   // cs = cs*decay + (1-decay)*counts  (vq.py:177-178; fp32 tensor ops)
   for (int m = tid; m < M; m += kFinThreads)
-    cs[m] = __fadd_rn(__fmul_rn(cs[m], decay), __fmul_rn(one_m_decay, st[(int64_t)m * (W + 1)]));
+    cs[m] = __fadd_rn(__fmul_rn(cs[m], decay), __fmul_rn(one_m_decay, stat((int64_t)m * (W + 1))));
   __syncthreads();
 
   if (laplace) {  // vq.py:182-186
@@ -566,7 +730,7 @@ vq_ema_finalize_kernel(const float* __restrict__ stats, int M, int D, int W, int
   for (int i = tid; i < nw; i += kFinThreads) {
     const int m = i / W, k = i % W;
     const int64_t o = (int64_t)m * ldw + k;
-    const float dw = st[(int64_t)m * (W + 1) + 1 + k];
+    const float dw = stat((int64_t)m * (W + 1) + 1 + k);
     const float w = __fadd_rn(__fmul_rn(ew[o], decay), __fmul_rn(one_m_decay, dw));
     ew[o] = w;
     const float ev = __fdiv_rn(w, cs[m]);
@@ -594,8 +758,8 @@ vq_ema_finalize_kernel(const float* __restrict__ stats, int M, int D, int W, int
 using namespace vqgnn;
 
 extern "C" size_t vqgnn_bn_stats_workspace(int32_t B, int32_t F) {
-  const int C = 2 * F;  // worst case with grads
-  return align_up((size_t)stats_chunks(B) * 2 * C * sizeof(double), 256);
+  const int C4 = (2 * F + 3) / 4;  // worst case with grads
+  return align_up((size_t)stats_chunks(B, C4) * 2 * C4 * 4 * sizeof(double), 256);
 }
 
 extern "C" int vqgnn_bn_stats(const float* X, int64_t ldx, const float* G, int64_t ldg,
@@ -606,14 +770,22 @@ extern "C" int vqgnn_bn_stats(const float* X, int64_t ldx, const float* G, int64
   VQGNN_REQUIRE(B > 0 && F > 0 && ldx >= F, "bn_stats: bad shape B=%d F=%d ldx=%lld", B, F,
                 (long long)ldx);
   VQGNN_REQUIRE(!with_grad || (G && ldg >= F), "bn_stats: grads required");
+  const bool vec = F % 4 == 0 && ldx % 4 == 0 && ((uintptr_t)X & 15) == 0 &&
+                   (!with_grad || (ldg % 4 == 0 && ((uintptr_t)G & 15) == 0));
   const int C = with_grad ? 2 * F : F;
-  const int chunks = stats_chunks(B);
+  const int C4 = (C + 3) / 4;
+  const int chunks = stats_chunks(B, C4);
   const int rpc = (B + chunks - 1) / chunks;
   double* part = reinterpret_cast<double*>(workspace);
   hipStream_t s = as_stream(stream);
-  hipLaunchKernelGGL(bn_stats_partial_kernel, dim3(chunks), dim3(kStatsThreads), 0, s, X, ldx,
-                     G, ldg, B, F, C, rpc, part);
-  hipLaunchKernelGGL(bn_stats_reduce_kernel, dim3((C + 255) / 256), dim3(256), 0, s, part,
+  if (vec) {
+    hipLaunchKernelGGL(bn_stats_partial_kernel, dim3(chunks), dim3(kStatsThreads), 0, s, X, ldx,
+                       G, ldg, B, F / 4, C4, rpc, part);
+  } else {
+    hipLaunchKernelGGL(bn_stats_partial_scalar_kernel, dim3(chunks), dim3(kStatsThreads), 0, s,
+                       X, ldx, G, ldg, B, F, C, rpc, part);
+  }
+  hipLaunchKernelGGL(bn_stats_reduce_kernel, dim3((C + 15) / 16), dim3(256), 0, s, part,
                      chunks, F, C, sums);
   return check_launch("bn_stats");
 }
@@ -634,79 +806,74 @@ extern "C" int vqgnn_bn_finalize(const double* sums, int64_t count, int32_t F, i
   return check_launch("bn_finalize");
 }
 
+extern "C" int32_t vqgnn_vq_ema_parts(int32_t B, int32_t nb, int32_t M, int32_t W) {
+  if (B <= 0 || nb <= 0 || M <= 0 || W <= 0) return 0;
+  const AssignGeom g = assign_geom(B, nb, M, W);
+  if (!g.fused && (size_t)M * (W + 1) * 4 > kLdsBudget) return 1;  // global-atomic slab
+  return g.parts;
+}
+
 extern "C" size_t vqgnn_vq_assign_workspace(int32_t B, int32_t nb, int32_t M, int32_t W) {
   if (B <= 0 || nb <= 0 || M <= 0 || W <= 0) return 0;
   const AssignGeom g = assign_geom(B, nb, M, W);
-  size_t bytes = align_up((size_t)g.ranges * nb * M * (W + 1) * sizeof(float), 256);
-  if (!g.fused) bytes += align_up((size_t)nb * B * sizeof(int), 256);
-  return bytes;
+  return g.fused ? 256 : align_up((size_t)nb * B * sizeof(int), 256);
 }
 
 template <int KC>
 static int launch_assign(const float* X, int64_t ldx, const float* G, int64_t ldg, int B,
                          int nb, int D, int M, int W, const float* coef, float grad_scale,
                          const float* emb, int ldw, int64_t emb_bstride, int64_t* idx_out,
-                         int16_t* codes, int64_t ldc, const int64_t* batch_idx, float* stats,
+                         int16_t* codes, int64_t ldc, const int64_t* batch_idx, float* parts,
                          void* workspace, hipStream_t s) {
   const AssignGeom g = assign_geom(B, nb, M, W);
-  const bool want_ema = stats != nullptr;
-  float* partial = reinterpret_cast<float*>(workspace);
-  int* idx32 = nullptr;
-  if (want_ema && !g.fused) {
-    idx32 = reinterpret_cast<int*>(reinterpret_cast<char*>(workspace) +
-                                   align_up((size_t)g.ranges * nb * M * (W + 1) * sizeof(float), 256));
-  }
+  const bool want_ema = parts != nullptr;
   const bool fused = want_ema && g.fused;
-  AssignGeom lg = g;
-  lg.fused = fused;
-  const size_t lds = assign_lds_bytes<KC>(lg, M, W);
-  if (lds > 160 * 1024) {
+  int* idx32 = (want_ema && !g.fused) ? reinterpret_cast<int*>(workspace) : nullptr;
+  size_t lds = cb_lds_bytes(KC, g.chunk);
+  if (fused) lds += (size_t)M * (W + 1) * 4;
+  if (lds > kLdsBudget) {
     set_error("vq_assign: LDS %zu B exceeds 160 KiB (M=%d W=%d)", lds, M, W);
     return VQGNN_ERR_UNSUPPORTED;
   }
-  if (lds > 64 * 1024) {
-    (void)hipFuncSetAttribute(fused ? (const void*)vq_assign_kernel<KC, true>
-                                    : (const void*)vq_assign_kernel<KC, false>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  }
-  if (fused) {
-    hipLaunchKernelGGL((vq_assign_kernel<KC, true>), dim3(g.wgs), dim3(kAssignThreads), lds, s,
-                       X, ldx, G, ldg, B, nb, D, M, W, coef, grad_scale, emb, ldw, emb_bstride,
-                       idx_out, codes, ldc, batch_idx, idx32, partial, g.iters_per_wg, g.ranges,
-                       g.chunk);
-  } else {
-    hipLaunchKernelGGL((vq_assign_kernel<KC, false>), dim3(g.wgs), dim3(kAssignThreads), lds, s,
-                       X, ldx, G, ldg, B, nb, D, M, W, coef, grad_scale, emb, ldw, emb_bstride,
-                       idx_out, codes, ldc, batch_idx, idx32, partial, g.iters_per_wg, g.ranges,
-                       g.chunk);
-  }
+  const int ng_env = asg_ng(), wv = asg_waves();
+  const int wgs = g.parts * nb;
+#define VQ_LAUNCH(FU, NGV, WVV)                                                               \
+  do {                                                                                        \
+    const void* fn = (const void*)vq_assign_kernel<KC, FU, NGV, WVV>;                         \
+    if (lds > 64 * 1024)                                                                      \
+      (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);    \
+    hipLaunchKernelGGL((vq_assign_kernel<KC, FU, NGV, WVV>), dim3(wgs), dim3(WVV * 64), lds,   \
+                       s, X, ldx, G, ldg, B, nb, D, M, W, coef, grad_scale, emb, ldw,          \
+                       emb_bstride, idx_out, codes, ldc, batch_idx, idx32, parts,             \
+                       g.rows_per_part, g.chunk);                                             \
+  } while (0)
+#define VQ_LAUNCH_W(FU)                                                                       \
+  do {                                                                                        \
+    if (wv == 8) {                                                                            \
+      if (ng_env == 4) VQ_LAUNCH(FU, 4, 8); else VQ_LAUNCH(FU, 2, 8);                         \
+    } else {                                                                                  \
+      if (ng_env == 4) VQ_LAUNCH(FU, 4, 16); else VQ_LAUNCH(FU, 2, 16);                       \
+    }                                                                                         \
+  } while (0)
+  if (fused) VQ_LAUNCH_W(true); else VQ_LAUNCH_W(false);
+#undef VQ_LAUNCH_W
+#undef VQ_LAUNCH
   int rc = check_launch("vq_assign");
-  if (rc || !want_ema) return rc;
-  const int64_t per_range = (int64_t)nb * M * (W + 1);
-  if (!fused) {
-    const size_t acc_bytes = (size_t)M * (W + 1) * sizeof(float);
-    const int use_lds = acc_bytes <= 160 * 1024;
-    if (use_lds) {
-      if (acc_bytes > 64 * 1024)
-        (void)hipFuncSetAttribute((const void*)vq_ema_partial_kernel<KC>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)acc_bytes);
-      hipLaunchKernelGGL((vq_ema_partial_kernel<KC>), dim3(g.wgs), dim3(kAssignThreads),
-                         acc_bytes, s, X, ldx, G, ldg, B, nb, D, M, W, coef, grad_scale, idx32,
-                         partial, g.iters_per_wg, 1);
-    } else {
-      // global-atomic fallback straight into the stats buffer
-      (void)hipMemsetAsync(stats, 0, per_range * sizeof(float), s);
-      hipLaunchKernelGGL((vq_ema_partial_kernel<KC>), dim3(g.wgs), dim3(kAssignThreads), 0, s,
-                         X, ldx, G, ldg, B, nb, D, M, W, coef, grad_scale, idx32, stats,
-                         g.iters_per_wg, 0);
-      return check_launch("vq_ema_partial(global)");
-    }
-    rc = check_launch("vq_ema_partial");
-    if (rc) return rc;
+  if (rc || !want_ema || fused) return rc;
+  const size_t acc_bytes = (size_t)M * (W + 1) * sizeof(float);
+  if (acc_bytes <= kLdsBudget) {
+    if (acc_bytes > 64 * 1024)
+      (void)hipFuncSetAttribute((const void*)vq_ema_partial_kernel,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)acc_bytes);
+    hipLaunchKernelGGL(vq_ema_partial_kernel, dim3(wgs), dim3(kAssignThreads), acc_bytes, s, X,
+                       ldx, G, ldg, B, nb, D, M, W, coef, grad_scale, idx32, parts,
+                       g.rows_per_part, 1);
+  } else {  // one slab, global atomics
+    (void)hipMemsetAsync(parts, 0, (size_t)nb * M * (W + 1) * sizeof(float), s);
+    hipLaunchKernelGGL(vq_ema_partial_kernel, dim3(wgs), dim3(kAssignThreads), 0, s, X, ldx, G,
+                       ldg, B, nb, D, M, W, coef, grad_scale, idx32, parts, g.rows_per_part, 0);
   }
-  hipLaunchKernelGGL(vq_ema_reduce_kernel, dim3((per_range + 255) / 256), dim3(256), 0, s,
-                     partial, g.ranges, per_range, stats);
-  return check_launch("vq_ema_reduce");
+  return check_launch("vq_ema_partial");
 }
 
 extern "C" int vqgnn_vq_assign(const float* X, int64_t ldx, const float* G, int64_t ldg,
@@ -714,7 +881,7 @@ extern "C" int vqgnn_vq_assign(const float* X, int64_t ldx, const float* G, int6
                                const float* coef, float grad_scale, const float* embedding,
                                int32_t ldw, int64_t emb_bstride, int64_t* idx_out,
                                int16_t* codes, int64_t ldc, const int64_t* batch_idx,
-                               float* ema_stats, void* workspace, vqgnn_stream_t stream) {
+                               float* ema_parts, void* workspace, vqgnn_stream_t stream) {
   clear_error();
   VQGNN_REQUIRE(X && coef && embedding, "vq_assign: null pointer");
   VQGNN_REQUIRE(B > 0 && nb > 0 && D > 0 && M > 0, "vq_assign: bad shape");
@@ -724,37 +891,46 @@ extern "C" int vqgnn_vq_assign(const float* X, int64_t ldx, const float* G, int6
   VQGNN_REQUIRE(W == D || (G && ldg >= (int64_t)nb * D), "vq_assign: grads required for W=2D");
   VQGNN_REQUIRE(ldw >= W && emb_bstride >= (int64_t)M * ldw, "vq_assign: bad codebook layout");
   VQGNN_REQUIRE(!codes || (batch_idx && ldc >= nb), "vq_assign: codes needs batch_idx, ldc>=nb");
-  VQGNN_REQUIRE(!ema_stats || workspace, "vq_assign: workspace required for EMA statistics");
+  VQGNN_REQUIRE(!ema_parts || workspace, "vq_assign: workspace required for EMA statistics");
   VQGNN_REQUIRE(M <= 32767 || !codes, "vq_assign: int16 codes need M <= 32767");
   hipStream_t s = as_stream(stream);
   const int kc = W <= 4 ? 1 : (W <= 8 ? 2 : 4);
   if (kc == 1)
     return launch_assign<1>(X, ldx, G, ldg, B, nb, D, M, W, coef, grad_scale, embedding, ldw,
-                            emb_bstride, idx_out, codes, ldc, batch_idx, ema_stats, workspace, s);
+                            emb_bstride, idx_out, codes, ldc, batch_idx, ema_parts, workspace, s);
   if (kc == 2)
     return launch_assign<2>(X, ldx, G, ldg, B, nb, D, M, W, coef, grad_scale, embedding, ldw,
-                            emb_bstride, idx_out, codes, ldc, batch_idx, ema_stats, workspace, s);
+                            emb_bstride, idx_out, codes, ldc, batch_idx, ema_parts, workspace, s);
   return launch_assign<4>(X, ldx, G, ldg, B, nb, D, M, W, coef, grad_scale, embedding, ldw,
-                          emb_bstride, idx_out, codes, ldc, batch_idx, ema_stats, workspace, s);
+                          emb_bstride, idx_out, codes, ldc, batch_idx, ema_parts, workspace, s);
 }
 
-extern "C" int vqgnn_vq_ema_finalize(const float* ema_stats, int32_t nb, int32_t M, int32_t D,
-                                     int32_t W, int32_t ldw, float decay, int32_t laplace,
-                                     float grad_scale, float epsilon, float* cluster_size,
-                                     int64_t cs_bstride, float* ema_w, float* embedding,
-                                     float* embedding_output, int64_t emb_bstride,
-                                     const float* rm_f, const float* rv_f, const float* rm_g,
-                                     const float* rv_g, int32_t* bad_init,
+extern "C" int vqgnn_vq_ema_reduce(const float* parts, int32_t nparts, int64_t part_elems,
+                                   float* out, vqgnn_stream_t stream) {
+  clear_error();
+  VQGNN_REQUIRE(parts && out && nparts > 0 && part_elems > 0, "ema_reduce: bad arguments");
+  hipLaunchKernelGGL(vq_ema_reduce_kernel, dim3((part_elems + 255) / 256), dim3(256), 0,
+                     as_stream(stream), parts, nparts, part_elems, out);
+  return check_launch("ema_reduce");
+}
+
+extern "C" int vqgnn_vq_ema_finalize(const float* ema_parts, int32_t nparts, int32_t nb,
+                                     int32_t M, int32_t D, int32_t W, int32_t ldw, float decay,
+                                     int32_t laplace, float grad_scale, float epsilon,
+                                     float* cluster_size, int64_t cs_bstride, float* ema_w,
+                                     float* embedding, float* embedding_output,
+                                     int64_t emb_bstride, const float* rm_f, const float* rv_f,
+                                     const float* rm_g, const float* rv_g, int32_t* bad_init,
                                      vqgnn_stream_t stream) {
   clear_error();
-  VQGNN_REQUIRE(ema_stats && cluster_size && ema_w && embedding && embedding_output && bad_init,
+  VQGNN_REQUIRE(ema_parts && cluster_size && ema_w && embedding && embedding_output && bad_init,
                 "ema_finalize: null pointer");
   VQGNN_REQUIRE(rm_f && rv_f, "ema_finalize: feature running stats required");
   VQGNN_REQUIRE(W == D || (W == 2 * D && rm_g && rv_g), "ema_finalize: W must be D or 2D");
-  VQGNN_REQUIRE(nb > 0 && M > 0 && ldw >= W, "ema_finalize: bad shape");
+  VQGNN_REQUIRE(nb > 0 && M > 0 && ldw >= W && nparts > 0, "ema_finalize: bad shape");
   hipLaunchKernelGGL(vq_ema_finalize_kernel, dim3(nb), dim3(kFinThreads), 0, as_stream(stream),
-                     ema_stats, M, D, W, ldw, decay, laplace, grad_scale, epsilon, cluster_size,
-                     cs_bstride, ema_w, embedding, embedding_output, emb_bstride, rm_f, rv_f,
-                     rm_g, rv_g, bad_init);
+                     ema_parts, nparts, (int64_t)nb * M * (W + 1), M, D, W, ldw, decay, laplace,
+                     grad_scale, epsilon, cluster_size, cs_bstride, ema_w, embedding,
+                     embedding_output, emb_bstride, rm_f, rv_f, rm_g, rv_g, bad_init);
   return check_launch("ema_finalize");
 }

@@ -57,17 +57,19 @@ def vq_assign(X, G, coef, grad_scale, emb, D, W, idx_out=None, codes=None, batch
     """Nearest codeword for every (row, branch); optional EMA statistics.
 
     emb: [nb, M, ldw] view (row-major per branch, arbitrary branch stride).
-    Returns ema_stats [nb, M, W+1] (float32) if want_stats else None."""
+    Returns the EMA partial slabs [P, nb, M, W+1] (float32) if want_stats,
+    else None; their sum over P is the statistic (vq_ema_reduce)."""
     require_gpu(X, "vq_assign")
     B = X.shape[0]
     nb, M, ldw = emb.shape
     if emb.stride(2) != 1 or emb.stride(1) != ldw:
         raise ValueError("codebook must be row-major per branch")
     L = lib()
-    stats = None
+    parts = None
     ws = None
     if want_stats:
-        stats = torch.empty(nb, M, W + 1, dtype=torch.float32, device=X.device)
+        P = L.vqgnn_vq_ema_parts(B, nb, M, W)
+        parts = torch.empty(P, nb, M, W + 1, dtype=torch.float32, device=X.device)
         ws = workspace(L.vqgnn_vq_assign_workspace(B, nb, M, W), X.device)
     ldc = 0
     if codes is not None:
@@ -76,32 +78,51 @@ def vq_assign(X, G, coef, grad_scale, emb, D, W, idx_out=None, codes=None, batch
         ldc = codes.stride(0)
     check(L.vqgnn_vq_assign(ptr(X), _ld(X), ptr(G), _ld(G) if G is not None else 0, B, nb, D,
                             M, W, ptr(coef), float(grad_scale), ptr(emb), ldw, emb.stride(0),
-                            ptr(idx_out), ptr(codes), ldc, ptr(batch_idx), ptr(stats), ptr(ws),
+                            ptr(idx_out), ptr(codes), ldc, ptr(batch_idx), ptr(parts), ptr(ws),
                             stream_ptr()), "vq_assign")
-    return stats
+    return parts
 
 
-def vq_ema_finalize(stats, D, W, decay, laplace, grad_scale, epsilon, cs, ema_w, emb, emb_out,
+def vq_ema_reduce(parts):
+    """[P, nb, M, W+1] -> [1, nb, M, W+1] (slab order)."""
+    P = parts.shape[0]
+    if P == 1:
+        return parts
+    out = torch.empty((1,) + tuple(parts.shape[1:]), dtype=torch.float32, device=parts.device)
+    check(lib().vqgnn_vq_ema_reduce(ptr(parts), P, parts[0].numel(), ptr(out), stream_ptr()),
+          "vq_ema_reduce")
+    return out
+
+
+def vq_ema_finalize(parts, D, W, decay, laplace, grad_scale, epsilon, cs, ema_w, emb, emb_out,
                     rm_f, rv_f, rm_g, rv_g, bad_flag):
-    nb, M, _ = stats.shape
+    P, nb, M, _ = parts.shape
     ldw = emb.shape[2]
     if not (ema_w.stride() == emb.stride() == emb_out.stride()):
         raise ValueError("ema_w / embedding / output must share one layout")
-    check(lib().vqgnn_vq_ema_finalize(ptr(stats), nb, M, D, W, ldw, float(decay), int(laplace),
-                                      float(grad_scale), float(epsilon), ptr(cs), cs.stride(0),
-                                      ptr(ema_w), ptr(emb), ptr(emb_out), emb.stride(0),
-                                      ptr(rm_f), ptr(rv_f), ptr(rm_g), ptr(rv_g),
+    check(lib().vqgnn_vq_ema_finalize(ptr(parts), P, nb, M, D, W, ldw, float(decay),
+                                      int(laplace), float(grad_scale), float(epsilon), ptr(cs),
+                                      cs.stride(0), ptr(ema_w), ptr(emb), ptr(emb_out),
+                                      emb.stride(0), ptr(rm_f), ptr(rv_f), ptr(rm_g), ptr(rv_g),
                                       ptr(bad_flag), stream_ptr()), "vq_ema_finalize")
 
 
-def gather_codes(subset: torch.Tensor, B: int, codes: torch.Tensor) -> torch.Tensor:
-    """lcodes[j] = codes[subset[B + j]]  (models.py:168)."""
+def gather_codewords(subset, B, codes, emb_out, D, col_offset=0, want_x=True,
+                     want_codes=False):
+    """models.py:168-173 for all branches: returns (xt [n-B, nb*D] or None,
+    lcodes [n-B, nb] int16 or None).  col_offset 0 = feature halves
+    (x_first_order), D = grad halves (grad_first_order)."""
     n = subset.shape[0]
     nb = codes.shape[1]
-    out = torch.empty(n - B, nb, dtype=torch.int16, device=codes.device)
-    check(lib().vqgnn_gather_codes(ptr(subset), B, n, ptr(codes), codes.stride(0), nb, ptr(out),
-                                   stream_ptr()), "gather_codes")
-    return out
+    dev = codes.device
+    xt = torch.empty(n - B, nb * D, dtype=torch.float32, device=dev) if want_x else None
+    lc = torch.empty(n - B, nb, dtype=torch.int16, device=dev) if want_codes else None
+    ldw = emb_out.shape[2] if emb_out is not None else 0
+    bstride = emb_out.stride(0) if emb_out is not None else 0
+    check(lib().vqgnn_gather_codewords(ptr(subset), B, n, ptr(codes), codes.stride(0), nb, D,
+                                       ptr(emb_out), ldw, bstride, int(col_offset), ptr(xt),
+                                       nb * D, ptr(lc), stream_ptr()), "gather_codewords")
+    return xt, lc
 
 
 def scatter_codes(batch_idx: torch.Tensor, local: torch.Tensor, codes: torch.Tensor) -> None:
@@ -111,25 +132,18 @@ def scatter_codes(batch_idx: torch.Tensor, local: torch.Tensor, codes: torch.Ten
                                     codes.stride(0), stream_ptr()), "scatter_codes")
 
 
-def spmm(rowptr, col, val, n_rows, nnz, X, F, B=None, D=0, lcodes=None, emb_out=None,
-         out=None):
-    """out[i] = sum_e val[e] * xin[col[e]]; xin = X rows (< B) / codebook rows (>= B)."""
+def spmm(rowptr, col, val, n_rows, nnz, X, F, X2=None, B=None, out=None):
+    """out[i] = sum_e val[e] * xin[col[e]]; xin = X rows (< B), X2 rows (>= B)."""
     require_gpu(X, "spmm")
     dev = X.device
     if out is None:
         out = torch.empty(n_rows, F, dtype=torch.float32, device=dev)
     L = lib()
     ws = workspace(L.vqgnn_spmm_workspace(n_rows, nnz, F), dev)
-    if lcodes is not None:
-        nb, _, ldw = emb_out.shape
-        bstride = emb_out.stride(0)
-        Bv = int(B)
-    else:
-        nb, ldw, bstride = 0, 0, 0
-        Bv = 2**31 - 1
+    Bv = int(B) if X2 is not None else 0
     check(L.vqgnn_spmm(ptr(rowptr), ptr(col), ptr(val), int(n_rows), int(nnz), Bv, ptr(X), _ld(X),
-                       F, D, ptr(lcodes), nb, ptr(emb_out), ldw, bstride, ptr(out), _ld(out),
-                       ptr(ws), stream_ptr()), "spmm")
+                       ptr(X2), _ld(X2) if X2 is not None else 0, F, ptr(out), _ld(out), ptr(ws),
+                       stream_ptr()), "spmm")
     return out
 
 

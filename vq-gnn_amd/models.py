@@ -8,8 +8,9 @@ different is where the work happens:
   launch sequence over a packed ``VQBank`` (vq.py here);
 * ``c_indices`` of all blocks of a layer live in one node-major int16 array
   [N, nb]; each block's ``c_indices`` is the column view ``codes[:, i]``;
-* the codebook gather + ``torch.cat`` + ``self.conv(x_input, adj)``
-  (models.py:168-179) is one fused gather-SpMM launch (convs.py here).
+* the per-branch codebook gathers (models.py:168-173) are one codeword-gather
+  launch over all branches, and ``torch.cat`` + ``self.conv(x_input, adj)``
+  (models.py:174-179) one two-source SpMM launch (convs.py here).
 
 Reference behaviour that is kept on purpose: the backward
 hooks registered at models.py:181-185 never fire in v2 (they sit on an
@@ -46,7 +47,7 @@ class LowRankGNNBlock(torch.nn.Module):
         self._branch = int(_branch)
         c = torch.randint(0, self.num_M, (self.num_N,), dtype=torch.short)  # models.py:27
         if _codes is None:
-            self._own_codes = torch.nn.Parameter(c.view(-1, 1), requires_grad=False)
+            self.register_buffer("_own_codes", c.view(-1, 1), persistent=False)
             self.__dict__["_codes_owner"] = None
         else:
             self.__dict__["_codes_owner"] = _codes
@@ -209,7 +210,8 @@ class LowRankGNNLayer(torch.nn.Module):
             for i in need:
                 self.gnn_block[i].init(x_det[:, D * i:D * (i + 1)], batch_idx)
 
-        lcodes = kernels.gather_codes(subset, B, self._codes)
+        # x_first_order (models.py:168-173): codeword feature halves of B'
+        x_first, _ = kernels.gather_codewords(subset, B, self._codes, self._bank.emb_out, D)
 
         hook = None
         if self.vq_update_in_backward and self.training and not unlabeled and \
@@ -217,10 +219,9 @@ class LowRankGNNLayer(torch.nn.Module):
             hook = _VQHook(self, x_det, batch_idx)
 
         if self.conv_type == 'GAT':
-            x_output = self.conv.fused_forward(x, adj, lcodes, self._bank.emb_out, D, B, hook)
+            x_output = self.conv.fused_forward(x, adj, x_first, B, hook)
         else:
-            gin = GatheredInput(x, lcodes, self._bank.emb_out, D)
-            x_output = self.conv(gin, adj, _hook=hook)
+            x_output = self.conv(GatheredInput(x, x_first), adj, _hook=hook)
 
         for _ in branch_idx:
             errors.append(0)
@@ -228,7 +229,8 @@ class LowRankGNNLayer(torch.nn.Module):
             quantized_norms.append(0)
 
         # info_backward (models.py:198): sum(out[B:] * grad half of the codewords)
-        grad_first_order = self._grad_first_order(lcodes)
+        grad_first_order, _ = kernels.gather_codewords(subset, B, self._codes,
+                                                       self._bank.emb_out, D, col_offset=D)
         info_backward = torch.sum(x_output[B:] * grad_first_order * warm_up_rate)
         if self.training:
             info_backwards += info_backward
@@ -239,14 +241,6 @@ class LowRankGNNLayer(torch.nn.Module):
         if self.skip:
             x_output = x_output + self.linear_skip(x)
         return x_output, errors, X_B_norms, quantized_norms, losses, info_backwards, hookeds
-
-    def _grad_first_order(self, lcodes):
-        """grad_first_order of models.py:171-173: the codewords' grad halves."""
-        D = self.num_D
-        eo = self._bank.emb_out
-        idx = lcodes.long()
-        parts = [eo[b][idx[:, b], D:2 * D] for b in range(self.num_branch)]
-        return torch.cat(parts, dim=1) if parts else eo.new_zeros(0, 0)
 
 
 class LowRankGNN(torch.nn.Module):

@@ -130,6 +130,7 @@ class VQBank(nn.Module):
             stats = kernels.vq_assign(X, None, coef, 1.0, self.emb[sl], D, D, idx_out=idx_out,
                                       codes=codes, batch_idx=batch_idx, want_stats=training)
         if comm is not None:
+            stats = kernels.vq_ema_reduce(stats)
             comm.allreduce_(stats)
             if local is not None:
                 comm.allgather_codes_(batch_idx, local, codes, self.comm_max_B)
@@ -182,6 +183,7 @@ class VQBank(nn.Module):
                                       idx_out=idx_out, codes=codes, batch_idx=batch_idx,
                                       want_stats=training)
         if comm is not None:
+            stats = kernels.vq_ema_reduce(stats)
             comm.allreduce_(stats)
             if local is not None:
                 comm.allgather_codes_(batch_idx, local, codes, self.comm_max_B)
