@@ -94,10 +94,19 @@ int vqgnn_bn_finalize(const double* sums, int64_t count, int32_t F, int32_t with
  *    Outputs (each optional):
  *      idx_out   [nb][B] int64   — encoding_indices per branch
  *      codes     [*][ldc] int16  — codes[batch_idx[i]][b] = idx (models.py:63/46)
- *      ema_parts [P][nb][M][W+1] fp32 — P = vqgnn_vq_ema_parts(B, nb, M, W)
- *                partial slabs of (count, sum of normalised x) per codeword;
- *                their sum (in slab order) is the EMA statistic.
+ *      ema_parts [P][nb][M][W+1] int64 — P = vqgnn_vq_ema_parts(B, nb, M, W)
+ *                partial slabs of (count, sum of normalised x) per codeword
+ *                in fixed point; their integer sum is the EMA statistic.
+ *    stat_count: rows the BatchNorm batch statistics were taken over (all
+ *    ranks); it bounds |normalised x| <= sqrt(stat_count) and so fixes the
+ *    fixed-point scale, vqgnn_vq_stat_shifts: column k < D of a slab is in
+ *    units of 2^-shift_f, k >= D of 2^-shift_g, the count column of 1.  Each
+ *    normalised value is rounded once (half an ulp of 2^-shift); the sums are
+ *    exact, so the statistic does not depend on thread order, the number of
+ *    parts or ranks (an int64 all-reduce of the slabs is exact).
  * ------------------------------------------------------------------------ */
+void vqgnn_vq_stat_shifts(int64_t stat_count, float grad_scale, int32_t* shift_f,
+                          int32_t* shift_g);
 int32_t vqgnn_vq_ema_parts(int32_t B, int32_t nb, int32_t M, int32_t W);
 size_t vqgnn_vq_assign_workspace(int32_t B, int32_t nb, int32_t M, int32_t W);
 int vqgnn_vq_assign(const float* X, int64_t ldx, const float* G, int64_t ldg,
@@ -105,13 +114,13 @@ int vqgnn_vq_assign(const float* X, int64_t ldx, const float* G, int64_t ldg,
                     const float* coef, float grad_scale,
                     const float* embedding, int32_t ldw, int64_t emb_bstride,
                     int64_t* idx_out, int16_t* codes, int64_t ldc,
-                    const int64_t* batch_idx, float* ema_parts,
+                    const int64_t* batch_idx, int64_t* ema_parts, int64_t stat_count,
                     void* workspace, vqgnn_stream_t stream);
 
-/* 3b. Fold P partial slabs into one (slab order): out[i] = sum_p parts[p][i].
- *     Multi-GPU callers fold, then all-reduce the single slab.               */
-int vqgnn_vq_ema_reduce(const float* parts, int32_t nparts, int64_t part_elems,
-                        float* out, vqgnn_stream_t stream);
+/* 3b. Fold P partial slabs into one: out[i] = sum_p parts[p][i] (exact).
+ *     Multi-GPU callers fold, then all-reduce (sum) the single int64 slab.    */
+int vqgnn_vq_ema_reduce(const int64_t* parts, int32_t nparts, int64_t part_elems,
+                        int64_t* out, vqgnn_stream_t stream);
 
 /* 4. EMA codebook finalize for nb branches (vq.py:177-200 / :242-277):
  *    cluster size EMA, Laplace smoothing (laplace != 0, vq.py:182-186),
@@ -119,10 +128,12 @@ int vqgnn_vq_ema_reduce(const float* parts, int32_t nparts, int64_t part_elems,
  *    with only cluster_size updated, as the reference raises there), ema_w EMA,
  *    embedding = ema_w / cs, and the de-normalised _embedding_output.  W = D
  *    updates the feature half only (feature_update); W = 2D all columns.
- *    ema_parts: nparts slabs of [nb][M][W+1] (summed in order).
+ *    ema_parts: nparts int64 slabs of [nb][M][W+1] (vqgnn_vq_assign), decoded
+ *    with the shifts of the same stat_count / grad_scale.
  *    Running stats (rm_f, rv_f, rm_g, rv_g) are [nb][D].  Per-branch arrays use
  *    strides cs_bstride (cluster_size) and emb_bstride (ema_w, embedding, out). */
-int vqgnn_vq_ema_finalize(const float* ema_parts, int32_t nparts, int32_t nb, int32_t M,
+int vqgnn_vq_ema_finalize(const int64_t* ema_parts, int32_t nparts, int64_t stat_count,
+                          int32_t nb, int32_t M,
                           int32_t D, int32_t W, int32_t ldw,
                           float decay, int32_t laplace, float grad_scale, float epsilon,
                           float* cluster_size, int64_t cs_bstride,

@@ -36,6 +36,13 @@ def test_host_only_workspace_queries():
     assert h.vqgnn_vq_assign_workspace(84670, 32, 256, 8) >= 256       # fused EMA
     assert h.vqgnn_vq_assign_workspace(30000, 64, 4096, 8) >= 64 * 30000 * 4  # idx scratch
     assert 1 <= h.vqgnn_vq_ema_parts(84670, 32, 256, 8) <= 64
+    import ctypes
+    sf, sg = ctypes.c_int32(), ctypes.c_int32()
+    h.vqgnn_vq_stat_shifts(84670, 1.0, ctypes.byref(sf), ctypes.byref(sg))
+    # |z| <= sqrt(84670) ~ 291 < 2^9  ->  2^(30-9) keeps a row inside int32
+    assert (sf.value, sg.value) == (21, 21)
+    h.vqgnn_vq_stat_shifts(84670, 2.0 ** -10, ctypes.byref(sf), ctypes.byref(sg))
+    assert (sf.value, sg.value) == (21, 31)
     assert h.vqgnn_spmm_workspace(128000, 2_000_000, 128) > 0
 
 
@@ -43,7 +50,7 @@ def test_invalid_arguments_rejected_without_device():
     # argument validation happens before any launch
     h = L.lib()
     rc = h.vqgnn_vq_assign(None, 0, None, 0, 10, 1, 4, 16, 6, None, 1.0, None, 8, 128,
-                           None, None, 0, None, None, None, None)
+                           None, None, 0, None, None, 0, None, None)
     assert rc == 1
     assert b"null" in h.vqgnn_last_error() or b"W" in h.vqgnn_last_error()
     # dummy non-null addresses: validation rejects F before any pointer is used

@@ -46,13 +46,19 @@ def test_assign_bit_exact_given_coefficients(M, D, W, B, tie):
     stats = kernels.vq_assign(X.to(DEV), G.to(DEV) if W == 2 * D else None, coef, scale,
                               emb.view(1, M, 2 * D).to(DEV), D, W, idx_out=idx, want_stats=True)
     assert torch.equal(idx.cpu()[0], idx_ref)
-    # EMA statistics: exact counts, fp32 sums of the normalised rows
+    # EMA statistics: int64 fixed point -> exact counts; sums within the
+    # quantisation (half a unit of 2^-shift per row) of the fp64 sums
+    assert stats.dtype == torch.int64
     xn = torch.cat([X * af + bf, ((G * ag + bg) * scale)], 1)[:, :W]
-    cnt = torch.bincount(idx_ref, minlength=M).float()
+    cnt = torch.bincount(idx_ref, minlength=M).double()
     dw = torch.zeros(M, W, dtype=torch.float64).index_add_(0, idx_ref, xn.double())
-    st = stats.sum(0).cpu()[0]
+    st = kernels.decode_stats(stats.sum(0), D, B, scale).cpu()[0]
     assert torch.equal(st[:, 0], cnt)
-    torch.testing.assert_close(st[:, 1:].double(), dw, rtol=1e-4, atol=1e-4)
+    sf, sg = kernels.stat_shifts(B, scale)
+    unit = torch.tensor([2.0 ** -sf] * D + [2.0 ** -sg] * (W - D), dtype=torch.float64)
+    absw = torch.zeros(M, W, dtype=torch.float64).index_add_(0, idx_ref, xn.double().abs())
+    tol = cnt[:, None] * unit * 0.5 + 1e-6 * absw   # + fp32 rounding of xn itself
+    assert ((st[:, 1:] - dw).abs() <= tol + 1e-7).all()
 
 
 def test_assign_multibranch_strided_views_and_codes():

@@ -17,6 +17,9 @@
 #include <cfloat>
 #include <cstdlib>
 #include <cmath>
+#include <map>
+#include <mutex>
+#include <tuple>
 
 namespace vqgnn {
 
@@ -290,24 +293,108 @@ static size_t cb_lds_bytes(int kc, int chunk) {
   return (size_t)4 * (chunk * kc * 4 + pad) + (size_t)chunk * 4;
 }
 
+// EMA sufficient statistics are int64 fixed point.  Every normalised value
+// is rounded once to an int32 multiple of 2^-shift and the products of the
+// one-hot reduction are integer sums: associative, so the statistic is
+// bit-identical whatever the thread order, the part split or the rank count
+// (an int64 all-reduce is exact).  The shifts follow from the train-mode
+// BatchNorm bound |z| <= sqrt(count - 1) (EMA updates only run in training,
+// vq.py:176/241, with batch statistics): count * 2^shift * bound < 2^62.
+// The count column is in units of 1.
+struct StatShift {
+  int f, g;
+};
+static StatShift stat_shift(int64_t count, float grad_scale) {
+  const double bound = std::sqrt((double)(count > 1 ? count : 1));
+  auto shift_for = [](double vmax) {
+    if (!(vmax > 0.0)) return 30;
+    int e = 0;
+    std::frexp(vmax, &e);          // vmax < 2^e
+    const int s = 30 - e;          // |v| * 2^s < 2^30 (< int32, ties to even)
+    return s < -100 ? -100 : (s > 100 ? 100 : s);
+  };
+  return {shift_for(bound), shift_for(bound * std::fabs((double)grad_scale))};
+}
+
+__device__ __forceinline__ unsigned long long to_fixed(float v, int shift) {
+  // v_ldexp + v_rndne + v_cvt_i32 (saturating); sign-extended to 64 bits
+  const int t = (int)rintf(ldexpf(v, shift));
+  return (unsigned long long)(long long)t;
+}
+
 static int env_int_vq(const char* name, int dflt) {
   const char* v = getenv(name);
   return v && *v ? atoi(v) : dflt;
 }
-static int asg_waves() {
-  static const int w = env_int_vq("VQGNN_ASG_WV", 8) == 16 ? 16 : 8;
-  return w;
+
+constexpr int kAsgWaves = 8;    // waves per workgroup
+constexpr int kAsgGroups = 2;   // 16-row groups per wave and iteration
+
+template <int KC, bool FUSED, int WM>
+__global__ void __launch_bounds__(kAsgWaves * 64)
+vq_assign_kernel(const float* __restrict__ X, int64_t ldx,
+                 const float* __restrict__ Gr, int64_t ldg,
+                 int B, int nb, int D, int M, int W,
+                 const float* __restrict__ coef, float grad_scale,
+                 const float* __restrict__ emb, int ldw, int64_t emb_bstride,
+                 int64_t* __restrict__ idx_out, int16_t* __restrict__ codes, int64_t ldc,
+                 const int64_t* __restrict__ batch_idx,
+                 int* __restrict__ idx32, unsigned long long* __restrict__ partial,
+                 int rows_per_part, int chunk, int shift_f, int shift_g);
+
+// k-slot layout: 0 general (W < 4*KC, padded), 1 W == 4*KC == D (features),
+// 2 W == 4*KC == 2*D (features then grads)
+static int slot_mode(int kc, int W, int D) {
+  if (W != 4 * kc) return 0;
+  return W == D ? 1 : 2;
 }
-static int asg_ng() {
-  static const int g = env_int_vq("VQGNN_ASG_NG", 2) == 4 ? 4 : 2;
-  return g;
+
+template <int KC>
+static const void* assign_fn(bool fused, int wm) {
+  if (fused) return wm == 1 ? (const void*)vq_assign_kernel<KC, true, 1>
+                  : wm == 2 ? (const void*)vq_assign_kernel<KC, true, 2>
+                            : (const void*)vq_assign_kernel<KC, true, 0>;
+  return wm == 1 ? (const void*)vq_assign_kernel<KC, false, 1>
+       : wm == 2 ? (const void*)vq_assign_kernel<KC, false, 2>
+                 : (const void*)vq_assign_kernel<KC, false, 0>;
+}
+
+// Workgroups of the assign kernel the current device holds at once (register
+// and LDS limited), cached per configuration.  Without a device (host-only
+// queries) a static estimate is returned; the value only sizes the grid.
+static int assign_capacity(int kc, bool fused, int wm, size_t lds) {
+  constexpr int wv = kAsgWaves;
+  const int fallback = 512;
+  int dev = 0, cus = 0, per_cu = 0;
+  if (hipGetDevice(&dev) != hipSuccess) {
+    (void)hipGetLastError();
+    return fallback;
+  }
+  static std::mutex mu;
+  static std::map<std::tuple<int, int, bool, size_t>, int> cache;
+  const auto key = std::make_tuple(dev, kc * 4 + wm, fused, lds);
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache.find(key);
+  if (it != cache.end()) return it->second;
+  const void* fn = kc == 1 ? assign_fn<1>(fused, wm)
+                 : kc == 2 ? assign_fn<2>(fused, wm) : assign_fn<4>(fused, wm);
+  if (lds > 64 * 1024)
+    (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  int cap = fallback;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, wv * 64, lds) == hipSuccess &&
+      per_cu > 0 && cus > 0)
+    cap = per_cu * cus;
+  (void)hipGetLastError();
+  cache[key] = cap;
+  return cap;
 }
 
 static AssignGeom assign_geom(int B, int nb, int M, int W) {
   AssignGeom g;
   g.kc = W <= 4 ? 1 : (W <= 8 ? 2 : 4);
   g.mpad = (M + 15) / 16 * 16;
-  const size_t acc = (size_t)M * (W + 1) * 4;
+  const size_t acc = (size_t)M * (W + 1) * sizeof(unsigned long long);
   // fused EMA when codebook + accumulators share the LDS
   g.fused = cb_lds_bytes(g.kc, g.mpad) + acc <= kLdsBudget;
   if (g.fused) {
@@ -317,10 +404,14 @@ static AssignGeom assign_geom(int B, int nb, int M, int W) {
     while (c > 16 && cb_lds_bytes(g.kc, c) > kLdsBudget) c = (c / 2 + 15) / 16 * 16;
     g.chunk = c;
   }
-  const int rows_per_iter = asg_waves() * 16 * asg_ng();
+  const int rows_per_iter = kAsgWaves * 16 * kAsgGroups;
   const int row_blocks = (B + rows_per_iter - 1) / rows_per_iter;
-  const int target = env_int_vq("VQGNN_ASG_TARGET", asg_waves() == 8 ? 768 : 256);
-  int parts = (target + nb - 1) / nb;
+  // one full round of resident workgroups: parts x nb <= what the device
+  // holds at once (every part has the same row count, so no tail round)
+  size_t lds = cb_lds_bytes(g.kc, g.chunk);
+  if (g.fused) lds += acc;
+  const int target = env_int_vq("VQGNN_ASG_TARGET", assign_capacity(g.kc, g.fused, W == 4 * g.kc ? 2 : 0, lds));
+  int parts = target / nb;
   if (parts < 1) parts = 1;
   if (parts > row_blocks) parts = row_blocks;
   g.parts = parts;
@@ -351,6 +442,14 @@ __device__ __forceinline__ Frag<KC> lds_frag(const float* p) {
     f.v[3] = t.w;
   }
   return f;
+}
+
+// plain v_min_f32 (no canonicalising v_max around it); inputs are finite or
+// +inf here
+__device__ __forceinline__ float vmin(float a, float b) {
+  float r;
+  asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
 }
 
 template <int NG>
@@ -390,8 +489,8 @@ __device__ __forceinline__ void stage_chunk(const float* __restrict__ E, int ldw
   }
 }
 
-template <int KC, bool FUSED, int NG, int WV>
-__global__ void __launch_bounds__(WV * 64)
+template <int KC, bool FUSED, int WM>
+__global__ void __launch_bounds__(kAsgWaves * 64)
 vq_assign_kernel(const float* __restrict__ X, int64_t ldx,
                  const float* __restrict__ Gr, int64_t ldg,
                  int B, int nb, int D, int M, int W,
@@ -399,10 +498,10 @@ vq_assign_kernel(const float* __restrict__ X, int64_t ldx,
                  const float* __restrict__ emb, int ldw, int64_t emb_bstride,
                  int64_t* __restrict__ idx_out, int16_t* __restrict__ codes, int64_t ldc,
                  const int64_t* __restrict__ batch_idx,
-                 int* __restrict__ idx32, float* __restrict__ partial,
-                 int rows_per_part, int chunk) {
+                 int* __restrict__ idx32, unsigned long long* __restrict__ partial,
+                 int rows_per_part, int chunk, int shift_f, int shift_g) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  constexpr int NT = WV * 64;
+  constexpr int NG = kAsgGroups, WV = kAsgWaves, NT = WV * 64, K4 = 4 * KC;
   const int F = nb * D;
   const int wg = xcd_remap(blockIdx.x, gridDim.x);
   const int b = wg % nb;
@@ -410,28 +509,36 @@ vq_assign_kernel(const float* __restrict__ X, int64_t ldx,
   const int qs = q_stride_floats<KC>(chunk);
   float* cb = smem;                       // [4][qs]
   float* se = smem + 4 * qs;              // [chunk]
-  float* acc = se + chunk;                // [M][W+1] (FUSED)
+  // [M][W+1] int64 fixed-point accumulators (FUSED), 8-byte aligned
+  unsigned long long* acc =
+      reinterpret_cast<unsigned long long*>(se + ((chunk + 1) & ~1));
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int q = lane >> 4, j = lane & 15;
   const float* E = emb + (int64_t)b * emb_bstride;
   const int nchunks = (M + chunk - 1) / chunk;
+  // whole codeword rows as float4 in the resolve step
+  const bool vec_rows = WM != 0 && (ldw & 3) == 0 && (emb_bstride & 3) == 0 &&
+                        (reinterpret_cast<uintptr_t>(emb) & 15) == 0;
 
   if constexpr (FUSED) {
-    for (int i = tid; i < M * (W + 1); i += NT) acc[i] = 0.f;
+    for (int i = tid; i < M * (W + 1); i += NT) acc[i] = 0ull;
   }
   if (nchunks == 1) stage_chunk<KC, NT>(E, ldw, W, 0, M, chunk, qs, cb, se, tid);
 
-  // per-column normalisation coefficients for this lane's k values
+  // k-slot k = kc*4 + q of this lane: column, normalisation coefficients
   float al[KC], be[KC];
   bool isg[KC], kval[KC];
   int colx[KC];
 #pragma unroll
   for (int kc = 0; kc < KC; ++kc) {
     const int k = kc * 4 + q;
-    kval[kc] = k < W;
-    isg[kc] = k >= D;
-    const int c = isg[kc] ? (b * D + (k - D)) : (b * D + k);
+    kval[kc] = WM != 0 || k < W;
+    if constexpr (WM == 1) isg[kc] = false;
+    else if constexpr (WM == 2) isg[kc] = KC == 1 ? (q >= 2) : (kc >= KC / 2);
+    else isg[kc] = k >= D;
+    const int kk = isg[kc] ? k - D : k;
+    const int c = b * D + kk;
     colx[kc] = c;
     al[kc] = kval[kc] ? coef[(isg[kc] ? 2 * F : 0) + c] : 0.f;
     be[kc] = kval[kc] ? coef[(isg[kc] ? 3 * F : F) + c] : 0.f;
@@ -439,22 +546,24 @@ vq_assign_kernel(const float* __restrict__ X, int64_t ldx,
 
   const int part_begin = part * rows_per_part;
   const int part_end = min(B, part_begin + rows_per_part);
+  const int n_iters = part_end > part_begin ? (part_end - part_begin + NG * 16 * WV - 1) /
+                                                  (NG * 16 * WV)
+                                            : 0;
 
-  // raw row values for one iteration: lane (q, j) of group g holds row
-  // row0 + 16g + j, k = kc*4 + q
+  // lane (q, j) of row group g holds row row0 + 16g + j, k-slots kc*4 + q.
+  // Rows past the part are clamped to its last row: MFMA columns are
+  // independent and those lanes write nothing.
   constexpr int RPW = 16 * NG;                 // rows per wave per iteration
   constexpr int RPI = WV * RPW;                // rows per workgroup iteration
   auto load_rows = [&](int it, float (&raw)[NG][KC]) {
     const int row0 = part_begin + it * RPI + wave * RPW;
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
-      const int row = row0 + g * 16 + j;
-      const bool ok = row < part_end;
+      const int64_t row = min(row0 + g * 16 + j, part_end - 1);
 #pragma unroll
       for (int kc = 0; kc < KC; ++kc) {
         float v = 0.f;
-        if (ok && kval[kc])
-          v = isg[kc] ? Gr[(int64_t)row * ldg + colx[kc]] : X[(int64_t)row * ldx + colx[kc]];
+        if (kval[kc]) v = isg[kc] ? Gr[row * ldg + colx[kc]] : X[row * ldx + colx[kc]];
         raw[g][kc] = v;
       }
     }
@@ -466,27 +575,23 @@ vq_assign_kernel(const float* __restrict__ X, int64_t ldx,
     const int row = part_begin + it * RPI + wave * RPW + q * 16 + j;
     return (codes && q < NG && row < part_end) ? batch_idx[row] : (int64_t)-1;
   };
-  load_rows(0, nxt);
-  nbi = load_bidx(0);
+  if (n_iters > 0) {
+    load_rows(0, nxt);
+    nbi = load_bidx(0);
+  }
   if (nchunks == 1) __syncthreads();
 
-  const int n_iters = (part_end - part_begin + RPI - 1) / RPI;
   for (int it = 0; it < n_iters; ++it) {
     const int row0 = part_begin + it * RPI + wave * RPW;
     float xk[NG][KC];
     float sx[NG];
-    bool rv[NG];
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
-      rv[g] = row0 + g * 16 + j < part_end;
 #pragma unroll
       for (int kc = 0; kc < KC; ++kc) {
-        float v = 0.f;
-        if (rv[g] && kval[kc]) {
-          v = fmaf(nxt[g][kc], al[kc], be[kc]);             // BatchNorm1d (ATen: fma)
-          if (isg[kc]) v = __fmul_rn(v, grad_scale);        // vq.py:224
-        }
-        xk[g][kc] = v;
+        float v = fmaf(nxt[g][kc], al[kc], be[kc]);       // BatchNorm1d (ATen: fma)
+        if (isg[kc]) v = __fmul_rn(v, grad_scale);        // vq.py:224
+        xk[g][kc] = kval[kc] ? v : 0.f;                   // padded k-slots are 0
       }
     }
     const int64_t cur_bi = nbi;
@@ -499,9 +604,9 @@ vq_assign_kernel(const float* __restrict__ X, int64_t ldx,
       // |x|^2 summed sequentially over k = 0..W-1 (torch.sum(x**2, dim=1))
       float s = 0.f;
 #pragma unroll
-      for (int k = 0; k < 4 * KC; ++k) {
+      for (int k = 0; k < K4; ++k) {
         const float v = __shfl(xk[g][k >> 2], j + 16 * (k & 3));
-        if (k < W) s = (k == 0) ? __fmul_rn(v, v) : __fadd_rn(s, __fmul_rn(v, v));
+        if (WM != 0 || k < W) s = (k == 0) ? __fmul_rn(v, v) : __fadd_rn(s, __fmul_rn(v, v));
       }
       sx[g] = s;
     }
@@ -523,6 +628,19 @@ vq_assign_kernel(const float* __restrict__ X, int64_t ldx,
         __syncthreads();
       }
       const float* cbq = cb + q * qs;
+      // Sweep: per lane and row group only the running minimum distance and
+      // the tile that first reached it (strict <: earliest tile wins ties).
+      // Which codeword of the tile it was is resolved after the sweep by an
+      // exact recompute (the f32 MFMA is bit-for-bit a k-ordered fma chain),
+      // which keeps v_cmp/v_cndmask (4-cycle issue) out of the per-element
+      // path: 3 v_min + 1 v_cmp + 1 v_min + 1 v_cndmask per 4 distances.
+      float cbest[NG];
+      int ctile[NG];
+#pragma unroll
+      for (int g = 0; g < NG; ++g) {
+        cbest[g] = INFINITY;
+        ctile[g] = 0;
+      }
       // operands of the next tile are read while this tile computes
       Frag<KC> a_nx = lds_frag<KC>(cbq + j * KC);
       float4 s_nx = *reinterpret_cast<const float4*>(se + 4 * q);
@@ -540,31 +658,68 @@ vq_assign_kernel(const float* __restrict__ X, int64_t ldx,
           for (int kc = 0; kc < KC; ++kc)
             d[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.v[kc], xk[g][kc], d[g], 0, 0, 0);
         }
-        const int mb = mc0 + m0 + 4 * q;
         const float sev[4] = {s4.x, s4.y, s4.z, s4.w};
 #pragma unroll
         for (int g = 0; g < NG; ++g) {
+          float dist[4];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float dist = fmaf(-2.f, d[g][r], __fadd_rn(sx[g], sev[r]));
-            const bool take = dist < best[g];
-            best[g] = take ? dist : best[g];
-            bidx[g] = take ? (mb + r) : bidx[g];
-          }
+          for (int r = 0; r < 4; ++r) dist[r] = fmaf(-2.f, d[g][r], __fadd_rn(sx[g], sev[r]));
+          const float m = vmin(vmin(dist[0], dist[1]), vmin(dist[2], dist[3]));
+          ctile[g] = (m < cbest[g]) ? m0 : ctile[g];
+          cbest[g] = vmin(cbest[g], m);
         }
       }
-    }
-
-    // ---- merge the 4 q-lanes of each row: (d, idx) lexicographic ----
+      // Resolve, spread over the 4 q-lanes of a row: the row minimum, the
+      // first (tile, q-lane) that reached it (index order = (tile, q, r)),
+      // then lane q recomputes candidate r = q of that lane's codewords with
+      // the operations and order of staging + MFMA + epilogue (bit-exact);
+      // the smallest matching r wins.  All 4 lanes of a row end up holding
+      // the same (best, idx).  Codewords come from global memory (L1): the
+      // LDS planes bank-conflict for lane-divergent rows.
 #pragma unroll
-    for (int g = 0; g < NG; ++g) {
+      for (int g = 0; g < NG; ++g) {
+        float rmin = cbest[g];
+        rmin = vmin(rmin, __shfl_xor(rmin, 16));
+        rmin = vmin(rmin, __shfl_xor(rmin, 32));
+        int key = (cbest[g] == rmin) ? ctile[g] + 4 * q : 0x7fffffff;
+        key = min(key, __shfl_xor(key, 16));
+        key = min(key, __shfl_xor(key, 32));
+        float xr[K4];
 #pragma unroll
-      for (int off = 16; off <= 32; off <<= 1) {
-        const float od = __shfl_xor(best[g], off);
-        const int oi = __shfl_xor(bidx[g], off);
-        const bool take = (od < best[g]) || (od == best[g] && oi < bidx[g]);
-        best[g] = take ? od : best[g];
-        bidx[g] = take ? oi : bidx[g];
+        for (int k = 0; k < K4; ++k) xr[k] = __shfl(xk[g][k >> 2], j + 16 * (k & 3));
+        const int c = mc0 + key + q;                 // this lane's candidate codeword
+        const bool cv = c < M;
+        const float* er = E + (int64_t)(cv ? c : M - 1) * ldw;
+        float e[K4];
+        if (vec_rows) {
+#pragma unroll
+          for (int v = 0; v < KC; ++v) {
+            const float4 t = *reinterpret_cast<const float4*>(er + 4 * v);
+            e[4 * v] = t.x;
+            e[4 * v + 1] = t.y;
+            e[4 * v + 2] = t.z;
+            e[4 * v + 3] = t.w;
+          }
+        } else {
+#pragma unroll
+          for (int k = 0; k < K4; ++k) e[k] = (WM != 0 || k < W) ? er[k] : 0.f;
+        }
+        float se_c = 0.f, dot = 0.f;
+#pragma unroll
+        for (int k = 0; k < K4; ++k) {
+          if (WM != 0 || k < W) {
+            se_c = (k == 0) ? __fmul_rn(e[k], e[k]) : __fadd_rn(se_c, __fmul_rn(e[k], e[k]));
+            dot = (k == 0) ? __fmul_rn(e[k], xr[k]) : fmaf(e[k], xr[k], dot);
+          }
+        }
+        const float dist = fmaf(-2.f, dot, __fadd_rn(sx[g], cv ? se_c : INFINITY));
+        int r = (dist == rmin) ? q : 4;
+        r = min(r, __shfl_xor(r, 16));
+        r = min(r, __shfl_xor(r, 32));
+        if (rmin < best[g]) {                        // earlier chunk wins ties
+          best[g] = rmin;
+          bidx[g] = mc0 + key + (r & 3);
+        }
       }
     }
 
@@ -579,15 +734,15 @@ vq_assign_kernel(const float* __restrict__ X, int64_t ldx,
       }
     }
 
-    if constexpr (FUSED) {
+    if constexpr (FUSED) {   // ds_add_u64: ~13x the rate of ds_add_f32 on gfx950
 #pragma unroll
       for (int g = 0; g < NG; ++g) {
-        if (rv[g]) {
-          float* a = acc + bidx[g] * (W + 1);
-          if (q == 0) atomicAdd(a, 1.0f);
+        if (row0 + g * 16 + j < part_end) {
+          unsigned long long* a = acc + bidx[g] * (W + 1);
+          if (q == 0) atomicAdd(a, 1ull);
 #pragma unroll
           for (int kc = 0; kc < KC; ++kc)
-            if (kval[kc]) atomicAdd(a + 1 + kc * 4 + q, xk[g][kc]);
+            if (kval[kc]) atomicAdd(a + 1 + kc * 4 + q, to_fixed(xk[g][kc], isg[kc] ? shift_g : shift_f));
         }
       }
     }
@@ -595,31 +750,31 @@ vq_assign_kernel(const float* __restrict__ X, int64_t ldx,
 
   if constexpr (FUSED) {
     __syncthreads();
-    float* out = partial + ((int64_t)part * nb + b) * M * (W + 1);
+    unsigned long long* out = partial + ((int64_t)part * nb + b) * M * (W + 1);
     for (int i = tid; i < M * (W + 1); i += NT) out[i] = acc[i];
   }
 }
 
 // Separate EMA statistics (codebook too large to share the LDS with the
-// accumulators): LDS accumulators for the whole codebook of one branch; rows
-// re-read and re-normalised.  use_lds == 0: global atomics into partial
-// (caller zeroes it; single slab).
+// accumulators): int64 fixed-point LDS accumulators for the whole codebook of
+// one branch; rows re-read and re-normalised.  use_lds == 0: global int64
+// atomics into partial (caller zeroes it; single slab).
 __global__ void __launch_bounds__(kAssignThreads)
 vq_ema_partial_kernel(const float* __restrict__ X, int64_t ldx,
                       const float* __restrict__ Gr, int64_t ldg,
                       int B, int nb, int D, int M, int W,
                       const float* __restrict__ coef, float grad_scale,
-                      const int* __restrict__ idx32, float* __restrict__ partial,
-                      int rows_per_part, int use_lds) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
+                      const int* __restrict__ idx32, unsigned long long* __restrict__ partial,
+                      int rows_per_part, int use_lds, int shift_f, int shift_g) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long smem64[];
   const int F = nb * D;
   const int wg = xcd_remap(blockIdx.x, gridDim.x);
   const int b = wg % nb;
   const int part = wg / nb;
   const int tid = threadIdx.x;
-  float* acc = use_lds ? smem : (partial + (int64_t)b * M * (W + 1));
+  unsigned long long* acc = use_lds ? smem64 : (partial + (int64_t)b * M * (W + 1));
   if (use_lds) {
-    for (int i = tid; i < M * (W + 1); i += kAssignThreads) acc[i] = 0.f;
+    for (int i = tid; i < M * (W + 1); i += kAssignThreads) acc[i] = 0ull;
     __syncthreads();
   }
   const int row_begin = part * rows_per_part;
@@ -630,9 +785,9 @@ vq_ema_partial_kernel(const float* __restrict__ X, int64_t ldx,
   if (rph < rows_per_pass) {
     for (int r = row_begin + rph; r < row_end; r += rows_per_pass) {
       const int m = idx32[(int64_t)b * B + r];
-      float* a = acc + m * (W + 1);
+      unsigned long long* a = acc + m * (W + 1);
       if (k1 == 0) {
-        atomicAdd(a, 1.0f);
+        atomicAdd(a, 1ull);
       } else {
         const int k = k1 - 1;
         const bool g = k >= D;
@@ -640,24 +795,24 @@ vq_ema_partial_kernel(const float* __restrict__ X, int64_t ldx,
         const float raw = g ? Gr[(int64_t)r * ldg + c] : X[(int64_t)r * ldx + c];
         float v = fmaf(raw, coef[(g ? 2 * F : 0) + c], coef[(g ? 3 * F : F) + c]);
         if (g) v = __fmul_rn(v, grad_scale);
-        atomicAdd(a + k1, v);
+        atomicAdd(a + k1, to_fixed(v, g ? shift_g : shift_f));
       }
     }
   }
   if (use_lds) {
     __syncthreads();
-    float* out = partial + ((int64_t)part * nb + b) * M * (W + 1);
+    unsigned long long* out = partial + ((int64_t)part * nb + b) * M * (W + 1);
     for (int i = tid; i < M * (W + 1); i += kAssignThreads) out[i] = acc[i];
   }
 }
 
-// out[i] = sum over parts (in order) of parts[p][i]
-__global__ void vq_ema_reduce_kernel(const float* __restrict__ parts, int nparts,
-                                     int64_t per_part, float* __restrict__ out) {
+// out[i] = sum over parts of parts[p][i] (integer: exact, order-free)
+__global__ void vq_ema_reduce_kernel(const long long* __restrict__ parts, int nparts,
+                                     int64_t per_part, long long* __restrict__ out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= per_part) return;
-  float s = parts[i];
-  for (int p = 1; p < nparts; ++p) s = __fadd_rn(s, parts[(int64_t)p * per_part + i]);
+  long long s = parts[i];
+  for (int p = 1; p < nparts; ++p) s += parts[(int64_t)p * per_part + i];
   out[i] = s;
 }
 
@@ -667,8 +822,8 @@ __global__ void vq_ema_reduce_kernel(const float* __restrict__ parts, int nparts
 constexpr int kFinThreads = 256;
 
 __global__ void __launch_bounds__(kFinThreads)
-vq_ema_finalize_kernel(const float* __restrict__ stats, int nparts, int64_t part_stride,
-                       int M, int D, int W, int ldw,
+vq_ema_finalize_kernel(const long long* __restrict__ stats, int nparts, int64_t part_stride,
+                       int shift_f, int shift_g, int M, int D, int W, int ldw,
                        float decay, int laplace, float grad_scale, float epsilon,
                        float* __restrict__ cluster_size, int64_t cs_bstride,
                        float* __restrict__ ema_w, float* __restrict__ emb,
@@ -680,12 +835,13 @@ vq_ema_finalize_kernel(const float* __restrict__ stats, int nparts, int64_t part
   __shared__ int bad;
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
-  const float* st = stats + (int64_t)b * M * (W + 1);
-  // statistics = sum of the per-part slabs, in part order (deterministic)
-  auto stat = [&](int64_t i) {
-    float v = st[i];
-    for (int p = 1; p < nparts; ++p) v = __fadd_rn(v, st[(int64_t)p * part_stride + i]);
-    return v;
+  const long long* st = stats + (int64_t)b * M * (W + 1);
+  // statistic = integer sum of the per-part fixed-point slabs, decoded once:
+  // round(exact sum * 2^-shift) to fp32 (count column: shift 0)
+  auto stat = [&](int64_t i, int shift) {
+    long long v = st[i];
+    for (int p = 1; p < nparts; ++p) v += st[(int64_t)p * part_stride + i];
+    return (float)ldexp((double)v, -shift);
   };
   float* cs = cluster_size + (int64_t)b * cs_bstride;
   float* ew = ema_w + (int64_t)b * emb_bstride;
@@ -696,7 +852,7 @@ vq_ema_finalize_kernel(const float* __restrict__ stats, int nparts, int64_t part
 
   // cs = cs*decay + (1-decay)*counts  (vq.py:177-178; fp32 tensor ops)
   for (int m = tid; m < M; m += kFinThreads)
-    cs[m] = __fadd_rn(__fmul_rn(cs[m], decay), __fmul_rn(one_m_decay, stat((int64_t)m * (W + 1))));
+    cs[m] = __fadd_rn(__fmul_rn(cs[m], decay), __fmul_rn(one_m_decay, stat((int64_t)m * (W + 1), 0)));
   __syncthreads();
 
   if (laplace) {  // vq.py:182-186
@@ -730,7 +886,7 @@ vq_ema_finalize_kernel(const float* __restrict__ stats, int nparts, int64_t part
   for (int i = tid; i < nw; i += kFinThreads) {
     const int m = i / W, k = i % W;
     const int64_t o = (int64_t)m * ldw + k;
-    const float dw = stat((int64_t)m * (W + 1) + 1 + k);
+    const float dw = stat((int64_t)m * (W + 1) + 1 + k, k < D ? shift_f : shift_g);
     const float w = __fadd_rn(__fmul_rn(ew[o], decay), __fmul_rn(one_m_decay, dw));
     ew[o] = w;
     const float ev = __fdiv_rn(w, cs[m]);
@@ -809,7 +965,7 @@ extern "C" int vqgnn_bn_finalize(const double* sums, int64_t count, int32_t F, i
 extern "C" int32_t vqgnn_vq_ema_parts(int32_t B, int32_t nb, int32_t M, int32_t W) {
   if (B <= 0 || nb <= 0 || M <= 0 || W <= 0) return 0;
   const AssignGeom g = assign_geom(B, nb, M, W);
-  if (!g.fused && (size_t)M * (W + 1) * 4 > kLdsBudget) return 1;  // global-atomic slab
+  if (!g.fused && (size_t)M * (W + 1) * 8 > kLdsBudget) return 1;  // global-atomic slab
   return g.parts;
 }
 
@@ -823,55 +979,56 @@ template <int KC>
 static int launch_assign(const float* X, int64_t ldx, const float* G, int64_t ldg, int B,
                          int nb, int D, int M, int W, const float* coef, float grad_scale,
                          const float* emb, int ldw, int64_t emb_bstride, int64_t* idx_out,
-                         int16_t* codes, int64_t ldc, const int64_t* batch_idx, float* parts,
-                         void* workspace, hipStream_t s) {
+                         int16_t* codes, int64_t ldc, const int64_t* batch_idx,
+                         unsigned long long* parts, int64_t stat_count, void* workspace,
+                         hipStream_t s) {
   const AssignGeom g = assign_geom(B, nb, M, W);
+  const StatShift sh = stat_shift(stat_count, grad_scale);
   const bool want_ema = parts != nullptr;
   const bool fused = want_ema && g.fused;
   int* idx32 = (want_ema && !g.fused) ? reinterpret_cast<int*>(workspace) : nullptr;
   size_t lds = cb_lds_bytes(KC, g.chunk);
-  if (fused) lds += (size_t)M * (W + 1) * 4;
+  if (fused) lds += (size_t)M * (W + 1) * sizeof(unsigned long long);
   if (lds > kLdsBudget) {
     set_error("vq_assign: LDS %zu B exceeds 160 KiB (M=%d W=%d)", lds, M, W);
     return VQGNN_ERR_UNSUPPORTED;
   }
-  const int ng_env = asg_ng(), wv = asg_waves();
   const int wgs = g.parts * nb;
-#define VQ_LAUNCH(FU, NGV, WVV)                                                               \
+  const int wm = slot_mode(KC, W, D);
+#define VQ_LAUNCH(FU, WMV)                                                                    \
   do {                                                                                        \
-    const void* fn = (const void*)vq_assign_kernel<KC, FU, NGV, WVV>;                         \
+    const void* fn = (const void*)vq_assign_kernel<KC, FU, WMV>;                              \
     if (lds > 64 * 1024)                                                                      \
       (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);    \
-    hipLaunchKernelGGL((vq_assign_kernel<KC, FU, NGV, WVV>), dim3(wgs), dim3(WVV * 64), lds,   \
+    hipLaunchKernelGGL((vq_assign_kernel<KC, FU, WMV>), dim3(wgs), dim3(kAsgWaves * 64), lds, \
                        s, X, ldx, G, ldg, B, nb, D, M, W, coef, grad_scale, emb, ldw,          \
                        emb_bstride, idx_out, codes, ldc, batch_idx, idx32, parts,             \
-                       g.rows_per_part, g.chunk);                                             \
+                       g.rows_per_part, g.chunk, sh.f, sh.g);                                 \
   } while (0)
-#define VQ_LAUNCH_W(FU)                                                                       \
+#define VQ_LAUNCH_WM(FU)                                                                      \
   do {                                                                                        \
-    if (wv == 8) {                                                                            \
-      if (ng_env == 4) VQ_LAUNCH(FU, 4, 8); else VQ_LAUNCH(FU, 2, 8);                         \
-    } else {                                                                                  \
-      if (ng_env == 4) VQ_LAUNCH(FU, 4, 16); else VQ_LAUNCH(FU, 2, 16);                       \
-    }                                                                                         \
+    if (wm == 1) VQ_LAUNCH(FU, 1);                                                            \
+    else if (wm == 2) VQ_LAUNCH(FU, 2);                                                       \
+    else VQ_LAUNCH(FU, 0);                                                                    \
   } while (0)
-  if (fused) VQ_LAUNCH_W(true); else VQ_LAUNCH_W(false);
-#undef VQ_LAUNCH_W
+  if (fused) VQ_LAUNCH_WM(true); else VQ_LAUNCH_WM(false);
+#undef VQ_LAUNCH_WM
 #undef VQ_LAUNCH
   int rc = check_launch("vq_assign");
   if (rc || !want_ema || fused) return rc;
-  const size_t acc_bytes = (size_t)M * (W + 1) * sizeof(float);
+  const size_t acc_bytes = (size_t)M * (W + 1) * sizeof(unsigned long long);
   if (acc_bytes <= kLdsBudget) {
     if (acc_bytes > 64 * 1024)
       (void)hipFuncSetAttribute((const void*)vq_ema_partial_kernel,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)acc_bytes);
     hipLaunchKernelGGL(vq_ema_partial_kernel, dim3(wgs), dim3(kAssignThreads), acc_bytes, s, X,
                        ldx, G, ldg, B, nb, D, M, W, coef, grad_scale, idx32, parts,
-                       g.rows_per_part, 1);
+                       g.rows_per_part, 1, sh.f, sh.g);
   } else {  // one slab, global atomics
-    (void)hipMemsetAsync(parts, 0, (size_t)nb * M * (W + 1) * sizeof(float), s);
+    (void)hipMemsetAsync(parts, 0, (size_t)nb * M * (W + 1) * sizeof(unsigned long long), s);
     hipLaunchKernelGGL(vq_ema_partial_kernel, dim3(wgs), dim3(kAssignThreads), 0, s, X, ldx, G,
-                       ldg, B, nb, D, M, W, coef, grad_scale, idx32, parts, g.rows_per_part, 0);
+                       ldg, B, nb, D, M, W, coef, grad_scale, idx32, parts, g.rows_per_part, 0,
+                       sh.f, sh.g);
   }
   return check_launch("vq_ema_partial");
 }
@@ -881,7 +1038,8 @@ extern "C" int vqgnn_vq_assign(const float* X, int64_t ldx, const float* G, int6
                                const float* coef, float grad_scale, const float* embedding,
                                int32_t ldw, int64_t emb_bstride, int64_t* idx_out,
                                int16_t* codes, int64_t ldc, const int64_t* batch_idx,
-                               float* ema_parts, void* workspace, vqgnn_stream_t stream) {
+                               int64_t* ema_parts, int64_t stat_count, void* workspace,
+                               vqgnn_stream_t stream) {
   clear_error();
   VQGNN_REQUIRE(X && coef && embedding, "vq_assign: null pointer");
   VQGNN_REQUIRE(B > 0 && nb > 0 && D > 0 && M > 0, "vq_assign: bad shape");
@@ -893,28 +1051,42 @@ extern "C" int vqgnn_vq_assign(const float* X, int64_t ldx, const float* G, int6
   VQGNN_REQUIRE(!codes || (batch_idx && ldc >= nb), "vq_assign: codes needs batch_idx, ldc>=nb");
   VQGNN_REQUIRE(!ema_parts || workspace, "vq_assign: workspace required for EMA statistics");
   VQGNN_REQUIRE(M <= 32767 || !codes, "vq_assign: int16 codes need M <= 32767");
+  VQGNN_REQUIRE(!ema_parts || stat_count >= B, "vq_assign: stat_count < B");
   hipStream_t s = as_stream(stream);
+  unsigned long long* parts = reinterpret_cast<unsigned long long*>(ema_parts);
   const int kc = W <= 4 ? 1 : (W <= 8 ? 2 : 4);
   if (kc == 1)
     return launch_assign<1>(X, ldx, G, ldg, B, nb, D, M, W, coef, grad_scale, embedding, ldw,
-                            emb_bstride, idx_out, codes, ldc, batch_idx, ema_parts, workspace, s);
+                            emb_bstride, idx_out, codes, ldc, batch_idx, parts, stat_count,
+                            workspace, s);
   if (kc == 2)
     return launch_assign<2>(X, ldx, G, ldg, B, nb, D, M, W, coef, grad_scale, embedding, ldw,
-                            emb_bstride, idx_out, codes, ldc, batch_idx, ema_parts, workspace, s);
+                            emb_bstride, idx_out, codes, ldc, batch_idx, parts, stat_count,
+                            workspace, s);
   return launch_assign<4>(X, ldx, G, ldg, B, nb, D, M, W, coef, grad_scale, embedding, ldw,
-                          emb_bstride, idx_out, codes, ldc, batch_idx, ema_parts, workspace, s);
+                          emb_bstride, idx_out, codes, ldc, batch_idx, parts, stat_count,
+                          workspace, s);
 }
 
-extern "C" int vqgnn_vq_ema_reduce(const float* parts, int32_t nparts, int64_t part_elems,
-                                   float* out, vqgnn_stream_t stream) {
+extern "C" void vqgnn_vq_stat_shifts(int64_t stat_count, float grad_scale, int32_t* shift_f,
+                                     int32_t* shift_g) {
+  const StatShift sh = stat_shift(stat_count, grad_scale);
+  if (shift_f) *shift_f = sh.f;
+  if (shift_g) *shift_g = sh.g;
+}
+
+extern "C" int vqgnn_vq_ema_reduce(const int64_t* parts, int32_t nparts, int64_t part_elems,
+                                   int64_t* out, vqgnn_stream_t stream) {
   clear_error();
   VQGNN_REQUIRE(parts && out && nparts > 0 && part_elems > 0, "ema_reduce: bad arguments");
   hipLaunchKernelGGL(vq_ema_reduce_kernel, dim3((part_elems + 255) / 256), dim3(256), 0,
-                     as_stream(stream), parts, nparts, part_elems, out);
+                     as_stream(stream), reinterpret_cast<const long long*>(parts), nparts,
+                     part_elems, reinterpret_cast<long long*>(out));
   return check_launch("ema_reduce");
 }
 
-extern "C" int vqgnn_vq_ema_finalize(const float* ema_parts, int32_t nparts, int32_t nb,
+extern "C" int vqgnn_vq_ema_finalize(const int64_t* ema_parts, int32_t nparts,
+                                     int64_t stat_count, int32_t nb,
                                      int32_t M, int32_t D, int32_t W, int32_t ldw, float decay,
                                      int32_t laplace, float grad_scale, float epsilon,
                                      float* cluster_size, int64_t cs_bstride, float* ema_w,
@@ -928,8 +1100,11 @@ extern "C" int vqgnn_vq_ema_finalize(const float* ema_parts, int32_t nparts, int
   VQGNN_REQUIRE(rm_f && rv_f, "ema_finalize: feature running stats required");
   VQGNN_REQUIRE(W == D || (W == 2 * D && rm_g && rv_g), "ema_finalize: W must be D or 2D");
   VQGNN_REQUIRE(nb > 0 && M > 0 && ldw >= W && nparts > 0, "ema_finalize: bad shape");
+  VQGNN_REQUIRE(stat_count > 0, "ema_finalize: stat_count must be > 0");
+  const StatShift sh = stat_shift(stat_count, grad_scale);
   hipLaunchKernelGGL(vq_ema_finalize_kernel, dim3(nb), dim3(kFinThreads), 0, as_stream(stream),
-                     ema_parts, nparts, (int64_t)nb * M * (W + 1), M, D, W, ldw, decay, laplace,
+                     reinterpret_cast<const long long*>(ema_parts), nparts,
+                     (int64_t)nb * M * (W + 1), sh.f, sh.g, M, D, W, ldw, decay, laplace,
                      grad_scale, epsilon, cluster_size, cs_bstride, ema_w, embedding,
                      embedding_output, emb_bstride, rm_f, rv_f, rm_g, rv_g, bad_init);
   return check_launch("ema_finalize");

@@ -52,13 +52,32 @@ def bn_finalize(sums, count, F, with_grad, mode, mom_f, eps_f, mom_g, eps_g, eps
     return coef, batch
 
 
+def stat_shifts(stat_count: int, grad_scale: float) -> tuple[int, int]:
+    """Fixed-point scale of the EMA statistic slabs (include/vqgnn.h §3)."""
+    import ctypes
+    sf, sg = ctypes.c_int32(), ctypes.c_int32()
+    lib().vqgnn_vq_stat_shifts(int(stat_count), float(grad_scale), ctypes.byref(sf),
+                               ctypes.byref(sg))
+    return sf.value, sg.value
+
+
+def decode_stats(stats: torch.Tensor, D: int, stat_count: int, grad_scale: float) -> torch.Tensor:
+    """int64 slab(s) [..., M, W+1] -> float64 (count, sum of normalised x)."""
+    sf, sg = stat_shifts(stat_count, grad_scale)
+    W = stats.shape[-1] - 1
+    scale = torch.tensor([1.0] + [2.0 ** -sf] * D + [2.0 ** -sg] * (W - D), dtype=torch.float64,
+                         device=stats.device)
+    return stats.to(torch.float64) * scale
+
+
 def vq_assign(X, G, coef, grad_scale, emb, D, W, idx_out=None, codes=None, batch_idx=None,
-              want_stats=False):
+              want_stats=False, stat_count=None):
     """Nearest codeword for every (row, branch); optional EMA statistics.
 
     emb: [nb, M, ldw] view (row-major per branch, arbitrary branch stride).
-    Returns the EMA partial slabs [P, nb, M, W+1] (float32) if want_stats,
-    else None; their sum over P is the statistic (vq_ema_reduce)."""
+    Returns the EMA partial slabs [P, nb, M, W+1] (int64 fixed point, see
+    decode_stats) if want_stats, else None; their sum over P is the statistic
+    (vq_ema_reduce).  stat_count: rows behind the BN statistics (default B)."""
     require_gpu(X, "vq_assign")
     B = X.shape[0]
     nb, M, ldw = emb.shape
@@ -69,38 +88,43 @@ def vq_assign(X, G, coef, grad_scale, emb, D, W, idx_out=None, codes=None, batch
     ws = None
     if want_stats:
         P = L.vqgnn_vq_ema_parts(B, nb, M, W)
-        parts = torch.empty(P, nb, M, W + 1, dtype=torch.float32, device=X.device)
         ws = workspace(L.vqgnn_vq_assign_workspace(B, nb, M, W), X.device)
     ldc = 0
     if codes is not None:
         if codes.dtype != torch.int16 or codes.stride(1) != 1:
             raise ValueError("codes must be an int16 [N, ldc] row-major view")
         ldc = codes.stride(0)
+    if want_stats:
+        parts = torch.empty(P, nb, M, W + 1, dtype=torch.int64, device=X.device)
     check(L.vqgnn_vq_assign(ptr(X), _ld(X), ptr(G), _ld(G) if G is not None else 0, B, nb, D,
                             M, W, ptr(coef), float(grad_scale), ptr(emb), ldw, emb.stride(0),
-                            ptr(idx_out), ptr(codes), ldc, ptr(batch_idx), ptr(parts), ptr(ws),
+                            ptr(idx_out), ptr(codes), ldc, ptr(batch_idx), ptr(parts),
+                            int(stat_count if stat_count is not None else B), ptr(ws),
                             stream_ptr()), "vq_assign")
     return parts
 
 
 def vq_ema_reduce(parts):
-    """[P, nb, M, W+1] -> [1, nb, M, W+1] (slab order)."""
+    """[P, nb, M, W+1] -> [1, nb, M, W+1] (exact integer sum)."""
     P = parts.shape[0]
     if P == 1:
         return parts
-    out = torch.empty((1,) + tuple(parts.shape[1:]), dtype=torch.float32, device=parts.device)
+    out = torch.empty((1,) + tuple(parts.shape[1:]), dtype=torch.int64, device=parts.device)
     check(lib().vqgnn_vq_ema_reduce(ptr(parts), P, parts[0].numel(), ptr(out), stream_ptr()),
           "vq_ema_reduce")
     return out
 
 
 def vq_ema_finalize(parts, D, W, decay, laplace, grad_scale, epsilon, cs, ema_w, emb, emb_out,
-                    rm_f, rv_f, rm_g, rv_g, bad_flag):
+                    rm_f, rv_f, rm_g, rv_g, bad_flag, stat_count):
     P, nb, M, _ = parts.shape
     ldw = emb.shape[2]
     if not (ema_w.stride() == emb.stride() == emb_out.stride()):
         raise ValueError("ema_w / embedding / output must share one layout")
-    check(lib().vqgnn_vq_ema_finalize(ptr(parts), P, nb, M, D, W, ldw, float(decay),
+    if parts.dtype != torch.int64:
+        raise ValueError("EMA statistic slabs are int64 fixed point")
+    check(lib().vqgnn_vq_ema_finalize(ptr(parts), P, int(stat_count), nb, M, D, W, ldw,
+                                      float(decay),
                                       int(laplace), float(grad_scale), float(epsilon), ptr(cs),
                                       cs.stride(0), ptr(ema_w), ptr(emb), ptr(emb_out),
                                       emb.stride(0), ptr(rm_f), ptr(rv_f), ptr(rm_g), ptr(rv_g),

@@ -118,6 +118,7 @@ class VQBank(nn.Module):
                                           0.0, self.rm_f[sl], self.rv_f[sl])
             self.nbt_f[sl] += 1
         else:
+            count = B
             coef, _ = kernels.bn_finalize(None, B, F, False, BN_EVAL, 0.1, 1e-5, 0.0, 0.0, 0.0,
                                           self.rm_f[sl], self.rv_f[sl])
         local = None
@@ -125,10 +126,11 @@ class VQBank(nn.Module):
             local = torch.empty(B, nbr, dtype=torch.int16, device=X.device)
             stats = kernels.vq_assign(X, None, coef, 1.0, self.emb[sl], D, D, idx_out=idx_out,
                                       codes=local, batch_idx=self._arange(B, X.device),
-                                      want_stats=training)
+                                      want_stats=training, stat_count=count)
         else:
             stats = kernels.vq_assign(X, None, coef, 1.0, self.emb[sl], D, D, idx_out=idx_out,
-                                      codes=codes, batch_idx=batch_idx, want_stats=training)
+                                      codes=codes, batch_idx=batch_idx, want_stats=training,
+                                      stat_count=count)
         if comm is not None:
             stats = kernels.vq_ema_reduce(stats)
             comm.allreduce_(stats)
@@ -138,7 +140,7 @@ class VQBank(nn.Module):
             kernels.vq_ema_finalize(stats, D, D, self.decay, self.warm_up_flag, 1.0, self.epsilon,
                                     self.cs[sl], self.ema_w[sl], self.emb[sl], self.emb_out[sl],
                                     self.rm_f[sl], self.rv_f[sl], self.rm_g[sl], self.rv_g[sl],
-                                    self.bad_flag)
+                                    self.bad_flag, count)
             self._finish()
 
     def update(self, X, G, b0, nbr, training, idx_out=None, codes=None, batch_idx=None):
@@ -177,11 +179,12 @@ class VQBank(nn.Module):
             local = torch.empty(B, nbr, dtype=torch.int16, device=X.device)
             stats = kernels.vq_assign(X, G, coef, scale, self.emb[sl], D, 2 * D,
                                       idx_out=idx_out, codes=local,
-                                      batch_idx=self._arange(B, X.device), want_stats=training)
+                                      batch_idx=self._arange(B, X.device), want_stats=training,
+                                      stat_count=count)
         else:
             stats = kernels.vq_assign(X, G, coef, scale, self.emb[sl], D, 2 * D,
                                       idx_out=idx_out, codes=codes, batch_idx=batch_idx,
-                                      want_stats=training)
+                                      want_stats=training, stat_count=count)
         if comm is not None:
             stats = kernels.vq_ema_reduce(stats)
             comm.allreduce_(stats)
@@ -191,7 +194,7 @@ class VQBank(nn.Module):
             kernels.vq_ema_finalize(stats, D, 2 * D, self.decay, self.warm_up_flag, scale,
                                     self.epsilon, self.cs[sl], self.ema_w[sl], self.emb[sl],
                                     self.emb_out[sl], self.rm_f[sl], self.rv_f[sl],
-                                    self.rm_g[sl], self.rv_g[sl], self.bad_flag)
+                                    self.rm_g[sl], self.rv_g[sl], self.bad_flag, count)
             self._finish()
 
 
