@@ -95,8 +95,9 @@ int vqgnn_bn_finalize(const double* sums, int64_t count, int32_t F, int32_t with
  *      idx_out   [nb][B] int64   — encoding_indices per branch
  *      codes     [*][ldc] int16  — codes[batch_idx[i]][b] = idx (models.py:63/46)
  *      ema_parts [P][nb][M][W+1] int64 — P = vqgnn_vq_ema_parts(B, nb, M, W)
- *                partial slabs of (count, sum of normalised x) per codeword
- *                in fixed point; their integer sum is the EMA statistic.
+ *                (currently 1): (count, sum of normalised x) per codeword in
+ *                fixed point; written whole by the call (zeroed, then the
+ *                workgroups' partials are added with int64 atomics).
  *    stat_count: rows the BatchNorm batch statistics were taken over (all
  *    ranks); it bounds |normalised x| <= sqrt(stat_count) and so fixes the
  *    fixed-point scale, vqgnn_vq_stat_shifts: column k < D of a slab is in

@@ -151,35 +151,25 @@ bn_stats_partial_scalar_kernel(const float* __restrict__ X, int64_t ldx,
   }
 }
 
-// Fold chunk partials (16 phases per column, fixed tree) -> sums[4][F].
-__global__ void __launch_bounds__(256)
+// Fold chunk partials -> sums[4][F]: one wave per value column (sum or sum
+// of squares of one data column); lanes stride the chunks, then a fixed
+// butterfly across the wave (deterministic).
+constexpr int kReduceWaves = 4;
+__global__ void __launch_bounds__(kReduceWaves * 64)
 bn_stats_reduce_kernel(const double* __restrict__ part, int chunks, int F, int C,
                        double* __restrict__ sums) {
-  __shared__ double red[2][16][17];
-  const int cl = threadIdx.x & 15, ph = threadIdx.x >> 4;
-  const int c = blockIdx.x * 16 + cl;
-  double a = 0.0, b = 0.0;
-  if (c < C) {
-    for (int p = ph; p < chunks; p += 16) {
-      a += part[(int64_t)p * 2 * C + c];
-      b += part[(int64_t)p * 2 * C + C + c];
-    }
-  }
-  red[0][ph][cl] = a;
-  red[1][ph][cl] = b;
-  __syncthreads();
-  if (ph == 0 && c < C) {
-    for (int p = 1; p < 16; ++p) {
-      a += red[0][p][cl];
-      b += red[1][p][cl];
-    }
-    if (c < F) {
-      sums[c] = a;
-      sums[F + c] = b;
-    } else {
-      sums[2 * F + (c - F)] = a;
-      sums[3 * F + (c - F)] = b;
-    }
+  const int lane = threadIdx.x & 63;
+  const int v = blockIdx.x * kReduceWaves + (threadIdx.x >> 6);   // value column in [0, 2C)
+  if (v >= 2 * C) return;
+  double a = 0.0;
+  for (int p = lane; p < chunks; p += 64) a += part[(int64_t)p * 2 * C + v];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) a += __shfl_xor(a, off);
+  if (lane == 0) {
+    const bool sq = v >= C;
+    const int c = sq ? v - C : v;
+    if (c < F) sums[(sq ? F : 0) + c] = a;
+    else sums[(sq ? 3 * F : 2 * F) + (c - F)] = a;
   }
 }
 
@@ -748,10 +738,11 @@ vq_assign_kernel(const float* __restrict__ X, int64_t ldx,
     }
   }
 
-  if constexpr (FUSED) {
+  if constexpr (FUSED) {   // fold into the single zeroed slab: integer, exact, order-free
     __syncthreads();
-    unsigned long long* out = partial + ((int64_t)part * nb + b) * M * (W + 1);
-    for (int i = tid; i < M * (W + 1); i += NT) out[i] = acc[i];
+    unsigned long long* out = partial + (int64_t)b * M * (W + 1);
+    for (int i = tid; i < M * (W + 1); i += NT)
+      if (acc[i]) atomicAdd(out + i, acc[i]);
   }
 }
 
@@ -801,8 +792,9 @@ vq_ema_partial_kernel(const float* __restrict__ X, int64_t ldx,
   }
   if (use_lds) {
     __syncthreads();
-    unsigned long long* out = partial + ((int64_t)part * nb + b) * M * (W + 1);
-    for (int i = tid; i < M * (W + 1); i += kAssignThreads) out[i] = acc[i];
+    unsigned long long* out = partial + (int64_t)b * M * (W + 1);
+    for (int i = tid; i < M * (W + 1); i += kAssignThreads)
+      if (acc[i]) atomicAdd(out + i, acc[i]);
   }
 }
 
@@ -941,7 +933,8 @@ extern "C" int vqgnn_bn_stats(const float* X, int64_t ldx, const float* G, int64
     hipLaunchKernelGGL(bn_stats_partial_scalar_kernel, dim3(chunks), dim3(kStatsThreads), 0, s,
                        X, ldx, G, ldg, B, F, C, rpc, part);
   }
-  hipLaunchKernelGGL(bn_stats_reduce_kernel, dim3((C + 15) / 16), dim3(256), 0, s, part,
+  hipLaunchKernelGGL(bn_stats_reduce_kernel, dim3((2 * C + kReduceWaves - 1) / kReduceWaves),
+                     dim3(kReduceWaves * 64), 0, s, part,
                      chunks, F, C, sums);
   return check_launch("bn_stats");
 }
@@ -963,10 +956,9 @@ extern "C" int vqgnn_bn_finalize(const double* sums, int64_t count, int32_t F, i
 }
 
 extern "C" int32_t vqgnn_vq_ema_parts(int32_t B, int32_t nb, int32_t M, int32_t W) {
-  if (B <= 0 || nb <= 0 || M <= 0 || W <= 0) return 0;
-  const AssignGeom g = assign_geom(B, nb, M, W);
-  if (!g.fused && (size_t)M * (W + 1) * 8 > kLdsBudget) return 1;  // global-atomic slab
-  return g.parts;
+  // the workgroups fold their partial statistics into one slab (int64
+  // atomics: exact); kept as a query so callers need not assume it
+  return (B <= 0 || nb <= 0 || M <= 0 || W <= 0) ? 0 : 1;
 }
 
 extern "C" size_t vqgnn_vq_assign_workspace(int32_t B, int32_t nb, int32_t M, int32_t W) {
@@ -995,6 +987,8 @@ static int launch_assign(const float* X, int64_t ldx, const float* G, int64_t ld
   }
   const int wgs = g.parts * nb;
   const int wm = slot_mode(KC, W, D);
+  if (want_ema)
+    (void)hipMemsetAsync(parts, 0, (size_t)nb * M * (W + 1) * sizeof(unsigned long long), s);
 #define VQ_LAUNCH(FU, WMV)                                                                    \
   do {                                                                                        \
     const void* fn = (const void*)vq_assign_kernel<KC, FU, WMV>;                              \
@@ -1024,8 +1018,7 @@ static int launch_assign(const float* X, int64_t ldx, const float* G, int64_t ld
     hipLaunchKernelGGL(vq_ema_partial_kernel, dim3(wgs), dim3(kAssignThreads), acc_bytes, s, X,
                        ldx, G, ldg, B, nb, D, M, W, coef, grad_scale, idx32, parts,
                        g.rows_per_part, 1, sh.f, sh.g);
-  } else {  // one slab, global atomics
-    (void)hipMemsetAsync(parts, 0, (size_t)nb * M * (W + 1) * sizeof(unsigned long long), s);
+  } else {  // global atomics
     hipLaunchKernelGGL(vq_ema_partial_kernel, dim3(wgs), dim3(kAssignThreads), 0, s, X, ldx, G,
                        ldg, B, nb, D, M, W, coef, grad_scale, idx32, parts, g.rows_per_part, 0,
                        sh.f, sh.g);
