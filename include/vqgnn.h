@@ -172,13 +172,14 @@ int vqgnn_scatter_codes(const int64_t* batch_idx, int32_t B, const int16_t* loca
  *    with xin[j] = X[j] for j < B and X2[j - B] for j >= B, i.e.
  *    x_input = cat([x, x_first_order]) (models.py:174) without the copy.
  *    X2 == NULL: xin = X (plain SpMM; B ignored) — also the transpose product
- *    of the backward pass.  Rows of at most L edges (L >= 128) are summed in CSR
+ *    of the backward pass.  n_cols = rows of xin (X rows, or B + X2 rows);
+ *    every col[e] must be < n_cols.  Rows of at most L edges (L >= 128) are summed in CSR
  *    order with separate mul and add, bit-identical to spmm_sum's loop; longer
  *    rows are split into edge chunks whose partials are added in chunk order.
  *    F must be a multiple of 4; X/X2/out 16-byte aligned; out [n_rows][ldo]. */
 size_t vqgnn_spmm_workspace(int32_t n_rows, int64_t nnz, int32_t F);
 int vqgnn_spmm(const int32_t* rowptr, const int32_t* col, const float* val,
-               int32_t n_rows, int64_t nnz, int32_t B,
+               int32_t n_rows, int32_t n_cols, int64_t nnz, int32_t B,
                const float* X, int64_t ldx, const float* X2, int64_t ldx2,
                int32_t F, float* out, int64_t ldo, void* workspace, vqgnn_stream_t stream);
 

@@ -59,6 +59,11 @@ struct SpmmArgs {
   int64_t ldo4;
   float* carry;   // [nchunks][2][F]
   int* carry_row; // [nchunks]
+  // wave kernel: X and X2 addressed as one 32-bit byte range from ubase
+  const char* ubase;
+  uint32_t span;  // bytes (buffer range; loads outside it return 0)
+  uint32_t offx, ldxb;    // X row j at offx + j*ldxb
+  uint32_t offx2, ldx2b;  // X2 row j-B at offx2 + (j-B)*ldx2b
 };
 
 template <int NCH>
@@ -209,30 +214,39 @@ spmm_merge_kernel(SpmmArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// Wave-uniform variant for F = 64*V (V = 1, 2, 4): one wave owns a chunk, the
-// edge stream (col, val, row base address) is wave-uniform and lives in
-// scalar registers, and each lane owns V consecutive columns of every row:
-// per edge one vector load of 4*F bytes per wave and 2V VALU (mul, add).
+// Wave kernel for F = 64*V (V = 1, 2, 4): one wave owns a chunk (same row
+// ownership and carries as the merge kernel) and each lane owns V consecutive
+// columns of every row.  The edge stream is wave-uniform and costs no per-lane
+// address arithmetic: a 64-edge window of (input-row byte offset, weight) is
+// staged with one coalesced load per 64 edges (lane l holds edge wb + l), and
+// edge k is read back with v_readlane into SGPRs, which feed the buffer
+// load's scalar offset and the multiply directly.  X and X2 (the two input
+// sources) are one 32-bit byte range from ubase, so there is no per-edge
+// source select.  Per edge and wave: 2 v_readlane, 1 buffer load of 4*F
+// bytes, V v_mul + V v_add (spmm_sum order) — against ~30 VALU per edge for
+// the lane-group kernel, which is VALU-bound on address math and shuffles.
 // ---------------------------------------------------------------------------
-template <int V>
-struct VecT;
-template <>
-struct VecT<1> { using T = float; };
-template <>
-struct VecT<2> { using T = float2; };
-template <>
-struct VecT<4> { using T = float4; };
+__device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
 
 template <int V>
-__device__ __forceinline__ void vload(const float* p, float (&v)[V]) {
+__device__ __forceinline__ void buf_load(__amdgpu_buffer_rsrc_t rs, uint32_t vo, uint32_t so,
+                                         float (&v)[V]) {
+  // bit_cast the builtin's result straight to float2/float4: extracting the
+  // elements of its integer-vector type miscompiles here (ROCm 7.2 clang
+  // loads only the first dword)
   if constexpr (V == 1) {
-    v[0] = *p;
+    v[0] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, vo, so, 0));
   } else if constexpr (V == 2) {
-    const float2 t = *reinterpret_cast<const float2*>(p);
-    v[0] = t.x; v[1] = t.y;
+    const float2 t = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rs, vo, so, 0));
+    v[0] = t.x;
+    v[1] = t.y;
   } else {
-    const float4 t = *reinterpret_cast<const float4*>(p);
-    v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+    const float4 t =
+        __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, vo, so, 0));
+    v[0] = t.x;
+    v[1] = t.y;
+    v[2] = t.z;
+    v[3] = t.w;
   }
 }
 
@@ -247,68 +261,94 @@ __device__ __forceinline__ void vstore(float* p, const float (&v)[V]) {
   }
 }
 
-__device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
+// lane l of the window holds edge wb + l: byte offset of its input row, weight
+struct EdgeWindow {
+  int wb;
+  uint32_t off;
+  float w;
+};
 
-template <int V, bool TWO>
-__device__ __forceinline__ void wave_segment(const SpmmArgs& a, int eb, int ee, int lane,
+__device__ __forceinline__ void window_stage(const SpmmArgs& a, EdgeWindow& win, int wb,
+                                             int lane) {
+  win.wb = wb;
+  const int e = wb + lane;
+  const bool ok = e < a.nnz;
+  const int j = ok ? a.col[e] : 0;
+  win.w = ok ? a.val[e] : 0.f;
+  win.off = j < a.B ? a.offx + (uint32_t)j * a.ldxb : a.offx2 + (uint32_t)(j - a.B) * a.ldx2b;
+}
+
+template <int V>
+__device__ __forceinline__ void wave_segment(const SpmmArgs& a, __amdgpu_buffer_rsrc_t rs,
+                                             EdgeWindow& win, int eb, int ee, int lane,
                                              float (&acc)[V]) {
 #pragma unroll
   for (int k = 0; k < V; ++k) acc[k] = 0.f;
-  constexpr int U = V == 4 ? 8 : 16;
-  const int64_t ldx = a.ldx4 * 4, ldx2 = a.ldx24 * 4;
-  for (int e = eb; e < ee; e += U) {
-    int jj[U];
-    float ww[U];
+  constexpr int U = V == 4 ? 4 : 8;
+  const uint32_t lo = (uint32_t)lane * V * 4;
+  int e = eb;
+  while (e < ee) {
+    if (e < win.wb || e >= win.wb + 64) window_stage(a, win, e, lane);
+    const int lim = min(ee, win.wb + 64);
+    for (; e + U <= lim; e += U) {
+      const int k0 = e - win.wb;
+      float v[U][V];
+      float ww[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const bool ok = e + u < ee;   // wave-uniform
-      jj[u] = ok ? uni(a.col[e + u]) : -1;
-      ww[u] = ok ? __builtin_bit_cast(float, uni(__builtin_bit_cast(int, a.val[e + u]))) : 0.f;
-    }
-    float v[U][V];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int j = jj[u];
-      if (j >= 0) {
-        const float* row = (!TWO || j < a.B) ? a.X + (int64_t)j * ldx
-                                             : a.X2 + (int64_t)(j - a.B) * ldx2;
-        vload<V>(row + lane * V, v[u]);
+      for (int u = 0; u < U; ++u) {
+        const uint32_t so = __builtin_amdgcn_readlane(win.off, k0 + u);
+        ww[u] = __builtin_bit_cast(float,
+                                   __builtin_amdgcn_readlane(__builtin_bit_cast(int, win.w), k0 + u));
+        buf_load<V>(rs, lo, so, v[u]);
       }
-    }
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (jj[u] >= 0) {
+      for (int u = 0; u < U; ++u) {
 #pragma unroll
         for (int k = 0; k < V; ++k) acc[k] = __fadd_rn(acc[k], __fmul_rn(ww[u], v[u][k]));
       }
     }
+    for (; e < lim; ++e) {
+      const int k0 = e - win.wb;
+      const uint32_t so = __builtin_amdgcn_readlane(win.off, k0);
+      const float w =
+          __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, win.w), k0));
+      float v[V];
+      buf_load<V>(rs, lo, so, v);
+#pragma unroll
+      for (int k = 0; k < V; ++k) acc[k] = __fadd_rn(acc[k], __fmul_rn(w, v[k]));
+    }
   }
 }
 
-template <int V, bool TWO>
+template <int V>
 __global__ void __launch_bounds__(kSpmmThreads)
 spmm_wave_kernel(SpmmArgs a) {
   const int lane = threadIdx.x & 63;
   const int wave = uni(threadIdx.x >> 6);
   int split = a.nchunks;
-  if (TWO && a.B < a.n_rows) split = min(a.nchunks, uni(a.rowptr[a.B]) / a.S);
+  if (a.B < a.n_rows) split = min(a.nchunks, uni(a.rowptr[a.B]) / a.S);
   const int chunk = spmm_chunk_of(blockIdx.x, wave, kSpmmThreads / 64, a.nchunks, split);
   if (chunk < 0) return;
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.ubase, 0, a.span, 0x00020000);
   const int e0 = chunk * a.S;
   const int e1 = min(e0 + a.S, a.nnz);
   const bool last = e1 == a.nnz;
+  const int F = a.F4 * 4;
   const int ldo = (int)(a.ldo4 * 4);
+  EdgeWindow win;
+  win.wb = INT32_MIN / 2;
   int i = uni(lower_bound_i32(a.rowptr, a.n_rows, e0));
   int crow = -1;
   float acc[V];
   if (i > 0) {
     const int ri = uni(a.rowptr[i]);
     if (ri > e0) {  // row i-1 started before this chunk
-      const int rs = uni(a.rowptr[i - 1]);
-      if (ri - rs > a.L) {
+      const int rs0 = uni(a.rowptr[i - 1]);
+      if (ri - rs0 > a.L) {
         const int re = min(ri, e1);
-        wave_segment<V, TWO>(a, e0, re, lane, acc);
-        vstore<V>(a.carry + (int64_t)chunk * 2 * (a.F4 * 4) + lane * V, acc);
+        wave_segment<V>(a, rs, win, e0, re, lane, acc);
+        vstore<V>(a.carry + (int64_t)chunk * 2 * F + lane * V, acc);
         crow = i - 1;
       }
     }
@@ -318,15 +358,15 @@ spmm_wave_kernel(SpmmArgs a) {
     if (!(rb < e1 || last)) break;
     const int re_full = uni(a.rowptr[i + 1]);
     if (re_full - rb <= a.L) {
-      wave_segment<V, TWO>(a, rb, re_full, lane, acc);
+      wave_segment<V>(a, rs, win, rb, re_full, lane, acc);
       vstore<V>(a.out + (int64_t)i * ldo + lane * V, acc);
     } else {
       const int re = min(re_full, e1);
-      wave_segment<V, TWO>(a, rb, re, lane, acc);
+      wave_segment<V>(a, rs, win, rb, re, lane, acc);
       if (re_full <= e1) {
         vstore<V>(a.out + (int64_t)i * ldo + lane * V, acc);
       } else {
-        vstore<V>(a.carry + ((int64_t)chunk * 2 + 1) * (a.F4 * 4) + lane * V, acc);
+        vstore<V>(a.carry + ((int64_t)chunk * 2 + 1) * F + lane * V, acc);
         break;
       }
     }
@@ -492,36 +532,56 @@ static void launch_spmm(const SpmmArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(spmm_fixup_kernel, dim3((a.nchunks + 255) / 256), dim3(256), 0, s, a);
 }
 
-template <int V, bool TWO>
+template <int V>
 static void launch_spmm_wave(const SpmmArgs& a, hipStream_t s) {
   constexpr int WPB = kSpmmThreads / 64;
   const int per_xcd = (a.nchunks + kNumXcd - 1) / kNumXcd + 1;
   const int grid = kNumXcd * ((per_xcd + WPB - 1) / WPB);
-  hipLaunchKernelGGL((spmm_wave_kernel<V, TWO>), dim3(grid), dim3(kSpmmThreads), 0, s, a);
+  hipLaunchKernelGGL((spmm_wave_kernel<V>), dim3(grid), dim3(kSpmmThreads), 0, s, a);
   hipLaunchKernelGGL(spmm_fixup_kernel, dim3((a.nchunks + 255) / 256), dim3(256), 0, s, a);
 }
 
+// 0 = automatic (wave kernel where it applies), 1 = lane-group kernel only
 static int spmm_mode() {
-  static const int m = env_int("VQGNN_SPMM_MODE", 0);  // 0 = merge kernel, 1 = wave-uniform
+  static const int m = env_int("VQGNN_SPMM_MODE", 0);
   return m;
 }
 
+// X rows [0, rows_x) and X2 rows [0, rows_x2) as one byte range of < 4 GiB
+static bool wave_layout(SpmmArgs& a, int64_t rows_x, int64_t rows_x2) {
+  const uint64_t x0 = (uint64_t)(uintptr_t)a.X;
+  const uint64_t x1 = x0 + (uint64_t)rows_x * (uint64_t)a.ldx4 * 16;
+  uint64_t lo = x0, hi = x1, y0 = x0;
+  if (a.X2 && rows_x2 > 0) {
+    y0 = (uint64_t)(uintptr_t)a.X2;
+    const uint64_t y1 = y0 + (uint64_t)rows_x2 * (uint64_t)a.ldx24 * 16;
+    lo = y0 < lo ? y0 : lo;
+    hi = y1 > hi ? y1 : hi;
+  }
+  if (hi - lo >= 0xFFFFFFFFull || (uint64_t)a.ldx4 * 16 > 0xFFFFFFFFull ||
+      (uint64_t)a.ldx24 * 16 > 0xFFFFFFFFull)
+    return false;
+  a.ubase = reinterpret_cast<const char*>((uintptr_t)lo);
+  a.span = (uint32_t)(hi - lo);
+  a.offx = (uint32_t)(x0 - lo);
+  a.ldxb = (uint32_t)(a.ldx4 * 16);
+  a.offx2 = (uint32_t)(y0 - lo);
+  a.ldx2b = (uint32_t)(a.ldx24 * 16);
+  return true;
+}
+
 template <bool TWO>
-static int dispatch_spmm(const SpmmArgs& a, hipStream_t s) {
+static int dispatch_spmm(SpmmArgs& a, int64_t rows_x, int64_t rows_x2, hipStream_t s) {
+  const int F = a.F4 * 4;
+  const bool al = (((uintptr_t)a.out | (uintptr_t)a.carry | (uintptr_t)(a.ldo4 * 16)) & 15) == 0;
+  if (spmm_mode() == 0 && al && (F == 64 || F == 128 || F == 256) &&
+      wave_layout(a, rows_x, rows_x2)) {
+    if (F == 128) launch_spmm_wave<2>(a, s);
+    else if (F == 256) launch_spmm_wave<4>(a, s);
+    else launch_spmm_wave<1>(a, s);
+    return check_launch("spmm");
+  }
   const int F4 = a.F4;
-  const bool al2 = (((uintptr_t)a.X | (uintptr_t)a.out | (uintptr_t)a.carry) & 7) == 0;
-  if (spmm_mode() == 1 && F4 * 4 == 64 * 2 && al2) {
-    launch_spmm_wave<2, TWO>(a, s);
-    return check_launch("spmm");
-  }
-  if (spmm_mode() == 1 && F4 * 4 == 64 * 4) {
-    launch_spmm_wave<4, TWO>(a, s);
-    return check_launch("spmm");
-  }
-  if (spmm_mode() == 1 && F4 * 4 == 64) {
-    launch_spmm_wave<1, TWO>(a, s);
-    return check_launch("spmm");
-  }
   if (F4 <= 16) launch_spmm<16, 1, TWO>(a, s);
   else if (F4 <= 32) launch_spmm<32, 1, TWO>(a, s);
   else if (F4 <= 64) launch_spmm<64, 1, TWO>(a, s);
@@ -537,7 +597,8 @@ static int dispatch_spmm(const SpmmArgs& a, hipStream_t s) {
 }
 
 extern "C" int vqgnn_spmm(const int32_t* rowptr, const int32_t* col, const float* val,
-                          int32_t n_rows, int64_t nnz, int32_t B, const float* X, int64_t ldx,
+                          int32_t n_rows, int32_t n_cols, int64_t nnz, int32_t B,
+                          const float* X, int64_t ldx,
                           const float* X2, int64_t ldx2, int32_t F, float* out, int64_t ldo,
                           void* workspace, vqgnn_stream_t stream) {
   clear_error();
@@ -550,6 +611,8 @@ extern "C" int vqgnn_spmm(const int32_t* rowptr, const int32_t* col, const float
   VQGNN_REQUIRE(((uintptr_t)X & 15) == 0 && ((uintptr_t)out & 15) == 0,
                 "spmm: X/out must be 16-byte aligned");
   VQGNN_REQUIRE(nnz < (int64_t)INT32_MAX, "spmm: nnz >= 2^31");
+  VQGNN_REQUIRE(n_cols >= 0 && (!X2 || (B >= 0 && B <= n_cols)),
+                "spmm: need 0 <= B <= n_cols with X2 (n_cols=%d B=%d)", n_cols, B);
   hipStream_t s = as_stream(stream);
   if (n_rows == 0) return VQGNN_OK;
   if (nnz == 0) {
@@ -579,7 +642,10 @@ extern "C" int vqgnn_spmm(const int32_t* rowptr, const int32_t* col, const float
   a.carry = reinterpret_cast<float*>(workspace);
   a.carry_row = reinterpret_cast<int*>(reinterpret_cast<char*>(workspace) +
                                        align_up((size_t)a.nchunks * 2 * F * sizeof(float), 256));
-  return X2 ? dispatch_spmm<true>(a, s) : dispatch_spmm<false>(a, s);
+  a.ubase = nullptr;
+  a.span = a.offx = a.ldxb = a.offx2 = a.ldx2b = 0;
+  return X2 ? dispatch_spmm<true>(a, B, (int64_t)n_cols - B, s)
+            : dispatch_spmm<false>(a, n_cols, 0, s);
 }
 
 extern "C" int vqgnn_gather_codewords(const int64_t* subset, int32_t B, int32_t n,

@@ -157,7 +157,8 @@ def scatter_codes(batch_idx: torch.Tensor, local: torch.Tensor, codes: torch.Ten
 
 
 def spmm(rowptr, col, val, n_rows, nnz, X, F, X2=None, B=None, out=None):
-    """out[i] = sum_e val[e] * xin[col[e]]; xin = X rows (< B), X2 rows (>= B)."""
+    """out[i] = sum_e val[e] * xin[col[e]]; xin = X rows (< B), X2 rows (>= B).
+    Every column index must be < the rows of xin (X rows, or B + X2 rows)."""
     require_gpu(X, "spmm")
     dev = X.device
     if out is None:
@@ -165,7 +166,11 @@ def spmm(rowptr, col, val, n_rows, nnz, X, F, X2=None, B=None, out=None):
     L = lib()
     ws = workspace(L.vqgnn_spmm_workspace(n_rows, nnz, F), dev)
     Bv = int(B) if X2 is not None else 0
-    check(L.vqgnn_spmm(ptr(rowptr), ptr(col), ptr(val), int(n_rows), int(nnz), Bv, ptr(X), _ld(X),
+    n_cols = Bv + X2.shape[0] if X2 is not None else X.shape[0]
+    if X2 is not None and X.shape[0] < Bv:
+        raise ValueError(f"spmm: X has {X.shape[0]} rows < B={Bv}")
+    check(L.vqgnn_spmm(ptr(rowptr), ptr(col), ptr(val), int(n_rows), int(n_cols), int(nnz), Bv,
+                       ptr(X), _ld(X),
                        ptr(X2), _ld(X2) if X2 is not None else 0, F, ptr(out), _ld(out), ptr(ws),
                        stream_ptr()), "spmm")
     return out
