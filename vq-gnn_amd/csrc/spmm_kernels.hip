@@ -64,6 +64,7 @@ struct SpmmArgs {
   uint32_t span;  // bytes (buffer range; loads outside it return 0)
   uint32_t offx, ldxb;    // X row j at offx + j*ldxb
   uint32_t offx2, ldx2b;  // X2 row j-B at offx2 + (j-B)*ldx2b
+  int kpw;                // wave kernel: consecutive chunks per wave
 };
 
 template <int NCH>
@@ -228,6 +229,7 @@ spmm_merge_kernel(SpmmArgs a) {
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
 
+
 template <int V>
 __device__ __forceinline__ void buf_load(__amdgpu_buffer_rsrc_t rs, uint32_t vo, uint32_t so,
                                          float (&v)[V]) {
@@ -278,13 +280,12 @@ __device__ __forceinline__ void window_stage(const SpmmArgs& a, EdgeWindow& win,
   win.off = j < a.B ? a.offx + (uint32_t)j * a.ldxb : a.offx2 + (uint32_t)(j - a.B) * a.ldx2b;
 }
 
-template <int V>
+template <int V, int U>
 __device__ __forceinline__ void wave_segment(const SpmmArgs& a, __amdgpu_buffer_rsrc_t rs,
                                              EdgeWindow& win, int eb, int ee, int lane,
                                              float (&acc)[V]) {
 #pragma unroll
   for (int k = 0; k < V; ++k) acc[k] = 0.f;
-  constexpr int U = V == 4 ? 4 : 8;
   const uint32_t lo = (uint32_t)lane * V * 4;
   int e = eb;
   while (e < ee) {
@@ -320,25 +321,16 @@ __device__ __forceinline__ void wave_segment(const SpmmArgs& a, __amdgpu_buffer_
   }
 }
 
-template <int V>
-__global__ void __launch_bounds__(kSpmmThreads)
-spmm_wave_kernel(SpmmArgs a) {
-  const int lane = threadIdx.x & 63;
-  const int wave = uni(threadIdx.x >> 6);
-  int split = a.nchunks;
-  if (a.B < a.n_rows) split = min(a.nchunks, uni(a.rowptr[a.B]) / a.S);
-  const int chunk = spmm_chunk_of(blockIdx.x, wave, kSpmmThreads / 64, a.nchunks, split);
-  if (chunk < 0) return;
-  const __amdgpu_buffer_rsrc_t rs =
-      __builtin_amdgcn_make_buffer_rsrc((void*)a.ubase, 0, a.span, 0x00020000);
+// One chunk (rows owned by chunk, carries) starting at row i; returns the
+// first row of the next chunk.
+template <int V, int U>
+__device__ __forceinline__ int wave_chunk(const SpmmArgs& a, __amdgpu_buffer_rsrc_t rs,
+                                          EdgeWindow& win, int chunk, int i, int lane) {
   const int e0 = chunk * a.S;
   const int e1 = min(e0 + a.S, a.nnz);
   const bool last = e1 == a.nnz;
   const int F = a.F4 * 4;
   const int ldo = (int)(a.ldo4 * 4);
-  EdgeWindow win;
-  win.wb = INT32_MIN / 2;
-  int i = uni(lower_bound_i32(a.rowptr, a.n_rows, e0));
   int crow = -1;
   float acc[V];
   if (i > 0) {
@@ -347,32 +339,57 @@ spmm_wave_kernel(SpmmArgs a) {
       const int rs0 = uni(a.rowptr[i - 1]);
       if (ri - rs0 > a.L) {
         const int re = min(ri, e1);
-        wave_segment<V>(a, rs, win, e0, re, lane, acc);
+        wave_segment<V, U>(a, rs, win, e0, re, lane, acc);
         vstore<V>(a.carry + (int64_t)chunk * 2 * F + lane * V, acc);
         crow = i - 1;
       }
     }
   }
+  int next = -1;
   int rb = (i < a.n_rows) ? uni(a.rowptr[i]) : 0;
   for (; i < a.n_rows; ++i) {
     if (!(rb < e1 || last)) break;
     const int re_full = uni(a.rowptr[i + 1]);
     if (re_full - rb <= a.L) {
-      wave_segment<V>(a, rs, win, rb, re_full, lane, acc);
+      wave_segment<V, U>(a, rs, win, rb, re_full, lane, acc);
       vstore<V>(a.out + (int64_t)i * ldo + lane * V, acc);
     } else {
       const int re = min(re_full, e1);
-      wave_segment<V>(a, rs, win, rb, re, lane, acc);
+      wave_segment<V, U>(a, rs, win, rb, re, lane, acc);
       if (re_full <= e1) {
         vstore<V>(a.out + (int64_t)i * ldo + lane * V, acc);
       } else {
         vstore<V>(a.carry + ((int64_t)chunk * 2 + 1) * F + lane * V, acc);
+        next = i + 1;   // the row continues into the next chunk
         break;
       }
     }
     rb = re_full;
   }
   if (lane == 0) a.carry_row[chunk] = crow;
+  return next >= 0 ? next : i;
+}
+
+// Each wave walks K consecutive chunks (its edge window and row cursor carry
+// over; only the first chunk needs the row search).
+template <int V, int U>
+__global__ void __launch_bounds__(kSpmmThreads)
+spmm_wave_kernel(SpmmArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int wave = uni(threadIdx.x >> 6);
+  const int K = a.kpw;
+  const int nsuper = (a.nchunks + K - 1) / K;
+  int split = nsuper;
+  if (a.B < a.n_rows) split = min(nsuper, uni(a.rowptr[a.B]) / (a.S * K));
+  const int sc = spmm_chunk_of(blockIdx.x, wave, kSpmmThreads / 64, nsuper, split);
+  if (sc < 0) return;
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.ubase, 0, a.span, 0x00020000);
+  EdgeWindow win;
+  win.wb = INT32_MIN / 2;
+  const int c0 = sc * K, c1 = min(a.nchunks, c0 + K);
+  int i = uni(lower_bound_i32(a.rowptr, a.n_rows, c0 * a.S));
+  for (int c = c0; c < c1; ++c) i = uni(wave_chunk<V, U>(a, rs, win, c, i, lane));
 }
 
 // For every row that spans chunks, the chunk where it ends adds the partials:
@@ -532,12 +549,15 @@ static void launch_spmm(const SpmmArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(spmm_fixup_kernel, dim3((a.nchunks + 255) / 256), dim3(256), 0, s, a);
 }
 
-template <int V>
-static void launch_spmm_wave(const SpmmArgs& a, hipStream_t s) {
+template <int V, int U>
+static void launch_spmm_wave(SpmmArgs& a, hipStream_t s) {
   constexpr int WPB = kSpmmThreads / 64;
-  const int per_xcd = (a.nchunks + kNumXcd - 1) / kNumXcd + 1;
+  static const int kpw = env_int("VQGNN_SPMM_K", 1);
+  a.kpw = kpw < 1 ? 1 : kpw;
+  const int nsuper = (a.nchunks + a.kpw - 1) / a.kpw;
+  const int per_xcd = (nsuper + kNumXcd - 1) / kNumXcd + 1;
   const int grid = kNumXcd * ((per_xcd + WPB - 1) / WPB);
-  hipLaunchKernelGGL((spmm_wave_kernel<V>), dim3(grid), dim3(kSpmmThreads), 0, s, a);
+  hipLaunchKernelGGL((spmm_wave_kernel<V, U>), dim3(grid), dim3(kSpmmThreads), 0, s, a);
   hipLaunchKernelGGL(spmm_fixup_kernel, dim3((a.nchunks + 255) / 256), dim3(256), 0, s, a);
 }
 
@@ -576,9 +596,16 @@ static int dispatch_spmm(SpmmArgs& a, int64_t rows_x, int64_t rows_x2, hipStream
   const bool al = (((uintptr_t)a.out | (uintptr_t)a.carry | (uintptr_t)(a.ldo4 * 16)) & 15) == 0;
   if (spmm_mode() == 0 && al && (F == 64 || F == 128 || F == 256) &&
       wave_layout(a, rows_x, rows_x2)) {
-    if (F == 128) launch_spmm_wave<2>(a, s);
-    else if (F == 256) launch_spmm_wave<4>(a, s);
-    else launch_spmm_wave<1>(a, s);
+    static const int u = env_int("VQGNN_SPMM_U", 8);
+    if (F == 128) {
+      if (u == 16) launch_spmm_wave<2, 16>(a, s);
+      else if (u == 4) launch_spmm_wave<2, 4>(a, s);
+      else launch_spmm_wave<2, 8>(a, s);
+    } else if (F == 256) {
+      launch_spmm_wave<4, 4>(a, s);
+    } else {
+      launch_spmm_wave<1, 8>(a, s);
+    }
     return check_launch("spmm");
   }
   const int F4 = a.F4;
