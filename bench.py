@@ -121,6 +121,7 @@ def main():
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
+    bank.assign_events = []          # HIP events around each vq_assign_kernel launch
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step(True)
@@ -128,6 +129,7 @@ def main():
     barrier()
     t1 = time.perf_counter()
     torch.cuda.synchronize()
+    assign_ev, bank.assign_events = bank.assign_events, None
     bank.check_bad_init()
 
     dt = t1 - t0
@@ -146,31 +148,35 @@ def main():
     vq_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
     gather_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in ev]))
     spmm_ms = float(np.mean([e[2].elapsed_time(e[3]) for e in ev]))
+    assign_ms = float(np.mean([a.elapsed_time(b) for a, b in assign_ev]))
 
-    # SpMM compulsory bytes: rowptr + (col, val) + every input row once (x and
-    # x_first_order) + the output; the codeword gather kernel is counted apart
+    # Algorithmic work per launch:
+    #  vq_assign_kernel: 2*B*M*W flops per branch (the distance contraction);
+    #  SpMM (spmm_wave_kernel + spmm_fixup_kernel): rowptr + (col, val) + every
+    #  input row once (x and x_first_order) + the output rows.
     spmm_bytes = 4 * (n + 1) + 8 * nnz + 4 * n * F + 4 * n * F
     vq_flops = 2.0 * B * M * W * nb
-    rl_spmm = dict(kernel="spmm_merge_kernel", bound="hbm",
-                   achieved=spmm_bytes / (spmm_ms * 1e-3) / 1e9, peak=8000.0, unit="GB/s",
-                   bytes_per_launch=spmm_bytes, ms_per_launch=spmm_ms)
-    rl_spmm["frac"] = rl_spmm["achieved"] / rl_spmm["peak"]
-    rl_vq = dict(kernel="vq step (bn_stats+finalize+assign+ema)", bound="mfma",
-                 achieved=vq_flops / (vq_ms * 1e-3) / 1e12, peak=157.3, unit="TFLOP/s",
-                 flops_per_launch=vq_flops, ms_per_launch=vq_ms)
-    rl_vq["frac"] = rl_vq["achieved"] / rl_vq["peak"]
-    dominant = rl_spmm if spmm_ms >= vq_ms else rl_vq
-    traffic = None
+    pmc = {}
     if os.path.exists(args.pmc_json):
         try:
             pm = json.load(open(args.pmc_json))
-            if pm.get("config") == args.config:
-                traffic = pm.get("hbm_bytes_per_launch", {}).get(
-                    "spmm" if dominant is rl_spmm else "vq")
-        except Exception:
-            traffic = None
+            if pm.get("config") == args.config and pm.get("semantics", "update") == args.semantics:
+                pmc = pm.get("hbm_bytes_per_launch", {})
+        except (OSError, ValueError):
+            pmc = {}
+    rl_spmm = dict(kernel="spmm_wave_kernel+spmm_fixup_kernel", bound="hbm",
+                   achieved=spmm_bytes / (spmm_ms * 1e-3) / 1e9, peak=8000.0, unit="GB/s",
+                   bytes_per_launch=spmm_bytes, ms_per_launch=spmm_ms,
+                   traffic=pmc.get("spmm_wave_kernel"))
+    rl_spmm["frac"] = rl_spmm["achieved"] / rl_spmm["peak"]
+    rl_vq = dict(kernel="vq_assign_kernel", bound="mfma",
+                 achieved=vq_flops / (assign_ms * 1e-3) / 1e12, peak=157.3, unit="TFLOP/s",
+                 flops_per_launch=vq_flops, ms_per_launch=assign_ms,
+                 traffic=pmc.get("vq_assign_kernel"))
+    rl_vq["frac"] = rl_vq["achieved"] / rl_vq["peak"]
+    dominant = rl_spmm if spmm_ms >= assign_ms else rl_vq
     roofline = dict(bound=dominant["bound"], achieved=dominant["achieved"], peak=dominant["peak"],
-                    unit=dominant["unit"], frac=dominant["frac"], traffic=traffic,
+                    unit=dominant["unit"], frac=dominant["frac"], traffic=dominant["traffic"],
                     kernel=dominant["kernel"])
 
     cpu = None
@@ -195,8 +201,8 @@ def main():
                         B=B, B_prime=n - B, nnz=nnz, F=F, M=M, D=D, W=W,
                         parallelism=f"dp{world}"),
             roofline=roofline,
-            kernels=dict(vq_ms=vq_ms, codeword_gather_ms=gather_ms, spmm_ms=spmm_ms,
-                         spmm=rl_spmm, vq=rl_vq),
+            kernels=dict(vq_update_ms=vq_ms, codeword_gather_ms=gather_ms, spmm_ms=spmm_ms,
+                         spmm=rl_spmm, vq_assign=rl_vq),
             cpu_baseline=cpu,
         )
         print(json.dumps(out))

@@ -96,8 +96,10 @@ int vqgnn_bn_finalize(const double* sums, int64_t count, int32_t F, int32_t with
  *      codes     [*][ldc] int16  — codes[batch_idx[i]][b] = idx (models.py:63/46)
  *      ema_parts [P][nb][M][W+1] int64 — P = vqgnn_vq_ema_parts(B, nb, M, W)
  *                (currently 1): (count, sum of normalised x) per codeword in
- *                fixed point; written whole by the call (zeroed, then the
- *                workgroups' partials are added with int64 atomics).
+ *                fixed point; the workgroups' partials are added into it with
+ *                int64 atomics.  ema_zeroed = 0: the call zeroes it first;
+ *                1: the caller guarantees it is zero (e.g. left so by
+ *                vqgnn_vq_ema_finalize with zero_after = 1).
  *    stat_count: rows the BatchNorm batch statistics were taken over (all
  *    ranks); it bounds |normalised x| <= sqrt(stat_count) and so fixes the
  *    fixed-point scale, vqgnn_vq_stat_shifts: column k < D of a slab is in
@@ -115,8 +117,8 @@ int vqgnn_vq_assign(const float* X, int64_t ldx, const float* G, int64_t ldg,
                     const float* coef, float grad_scale,
                     const float* embedding, int32_t ldw, int64_t emb_bstride,
                     int64_t* idx_out, int16_t* codes, int64_t ldc,
-                    const int64_t* batch_idx, int64_t* ema_parts, int64_t stat_count,
-                    void* workspace, vqgnn_stream_t stream);
+                    const int64_t* batch_idx, int64_t* ema_parts, int32_t ema_zeroed,
+                    int64_t stat_count, void* workspace, vqgnn_stream_t stream);
 
 /* 3b. Fold P partial slabs into one: out[i] = sum_p parts[p][i] (exact).
  *     Multi-GPU callers fold, then all-reduce (sum) the single int64 slab.    */
@@ -130,10 +132,12 @@ int vqgnn_vq_ema_reduce(const int64_t* parts, int32_t nparts, int64_t part_elems
  *    embedding = ema_w / cs, and the de-normalised _embedding_output.  W = D
  *    updates the feature half only (feature_update); W = 2D all columns.
  *    ema_parts: nparts int64 slabs of [nb][M][W+1] (vqgnn_vq_assign), decoded
- *    with the shifts of the same stat_count / grad_scale.
+ *    with the shifts of the same stat_count / grad_scale; zero_after != 0
+ *    clears every entry once read (ready for the next assign).
  *    Running stats (rm_f, rv_f, rm_g, rv_g) are [nb][D].  Per-branch arrays use
  *    strides cs_bstride (cluster_size) and emb_bstride (ema_w, embedding, out). */
-int vqgnn_vq_ema_finalize(const int64_t* ema_parts, int32_t nparts, int64_t stat_count,
+int vqgnn_vq_ema_finalize(int64_t* ema_parts, int32_t nparts, int32_t zero_after,
+                          int64_t stat_count,
                           int32_t nb, int32_t M,
                           int32_t D, int32_t W, int32_t ldw,
                           float decay, int32_t laplace, float grad_scale, float epsilon,

@@ -50,7 +50,7 @@ def test_invalid_arguments_rejected_without_device():
     # argument validation happens before any launch
     h = L.lib()
     rc = h.vqgnn_vq_assign(None, 0, None, 0, 10, 1, 4, 16, 6, None, 1.0, None, 8, 128,
-                           None, None, 0, None, None, 0, None, None)
+                           None, None, 0, None, None, 0, 0, None, None)
     assert rc == 1
     assert b"null" in h.vqgnn_last_error() or b"W" in h.vqgnn_last_error()
     # dummy non-null addresses: validation rejects F before any pointer is used

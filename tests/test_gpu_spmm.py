@@ -101,6 +101,26 @@ def test_codeword_gather_and_two_source_spmm_vs_oracle(F, D):
     assert np.array_equal(out.cpu().numpy()[inside], ref[inside])
 
 
+def test_two_source_far_apart_inputs():
+    """x and x_first_order more than 4 GiB apart: the wave kernel switches
+    from one 32-bit buffer range to 64-bit row addresses; same results."""
+    rng = np.random.default_rng(7)
+    n, B, F = 900, 500, 128
+    rowptr, col, val = _random_csr(n, n, 14, rng)
+    x = rng.standard_normal((n, F)).astype(np.float32)
+    a = _dev_csr(rowptr, col, val, n, n)
+    xd = torch.from_numpy(x[:B]).to(DEV)
+    gap = torch.empty(5 << 30, dtype=torch.uint8, device=DEV)       # 5 GiB in between
+    x2d = torch.from_numpy(x[B:]).to(DEV)
+    assert abs(x2d.data_ptr() - xd.data_ptr()) > (4 << 30) or gap.numel() == 0
+    out = kernels.spmm(a.rowptr, a.col, a.value, n, a.nnz(), xd, F, X2=x2d, B=B)
+    ref = conv_ref.spmm_seq(rowptr, col, val, x)
+    inside = np.diff(rowptr) <= 128
+    assert np.array_equal(out.cpu().numpy()[inside], ref[inside])
+    np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=1e-5, atol=1e-5)
+    del gap
+
+
 def test_scatter_codes():
     N, nb, B = 100, 5, 30
     codes = torch.zeros(N, nb, dtype=torch.int16, device=DEV)

@@ -40,9 +40,9 @@ SIGNATURES = {
     "vqgnn_vq_assign": (ctypes.c_int, [_c_void_p, _i64, _c_void_p, _i64, _i32, _i32, _i32,
                                        _i32, _i32, _c_void_p, _f32, _c_void_p, _i32, _i64,
                                        _c_void_p, _c_void_p, _i64, _c_void_p, _c_void_p,
-                                       _i64, _c_void_p, _c_void_p]),
-    "vqgnn_vq_ema_finalize": (ctypes.c_int, [_c_void_p, _i32, _i64, _i32, _i32, _i32, _i32, _i32,
-                                             _f32,
+                                       _i32, _i64, _c_void_p, _c_void_p]),
+    "vqgnn_vq_ema_finalize": (ctypes.c_int, [_c_void_p, _i32, _i32, _i64, _i32, _i32, _i32, _i32,
+                                             _i32, _f32,
                                              _i32, _f32, _f32, _c_void_p, _i64, _c_void_p,
                                              _c_void_p, _c_void_p, _i64, _c_void_p, _c_void_p,
                                              _c_void_p, _c_void_p, _c_void_p, _c_void_p]),

@@ -263,26 +263,58 @@ __device__ __forceinline__ void vstore(float* p, const float (&v)[V]) {
   }
 }
 
-// lane l of the window holds edge wb + l: byte offset of its input row, weight
+// lane l of the window holds edge wb + l: where its input row is (a 32-bit
+// offset into the buffer range, or — FAR — the row's 64-bit address when X
+// and X2 are more than 4 GiB apart) and its weight
+template <bool FAR>
 struct EdgeWindow {
   int wb;
-  uint32_t off;
+  uint32_t off;   // FAR: low half of the address
+  uint32_t hi;    // FAR: high half
   float w;
 };
 
-__device__ __forceinline__ void window_stage(const SpmmArgs& a, EdgeWindow& win, int wb,
+template <bool FAR>
+__device__ __forceinline__ void window_stage(const SpmmArgs& a, EdgeWindow<FAR>& win, int wb,
                                              int lane) {
   win.wb = wb;
   const int e = wb + lane;
   const bool ok = e < a.nnz;
   const int j = ok ? a.col[e] : 0;
   win.w = ok ? a.val[e] : 0.f;
-  win.off = j < a.B ? a.offx + (uint32_t)j * a.ldxb : a.offx2 + (uint32_t)(j - a.B) * a.ldx2b;
+  if constexpr (FAR) {
+    const float* row = j < a.B ? a.X + (int64_t)j * a.ldx4 * 4
+                               : a.X2 + (int64_t)(j - a.B) * a.ldx24 * 4;
+    const uint64_t p = (uint64_t)(uintptr_t)row;
+    win.off = (uint32_t)p;
+    win.hi = (uint32_t)(p >> 32);
+  } else {
+    win.off = j < a.B ? a.offx + (uint32_t)j * a.ldxb : a.offx2 + (uint32_t)(j - a.B) * a.ldx2b;
+    win.hi = 0;
+  }
 }
 
-template <int V, int U>
+// row k of the window, this lane's V columns
+template <int V, bool FAR>
+__device__ __forceinline__ void window_load(__amdgpu_buffer_rsrc_t rs, const EdgeWindow<FAR>& win,
+                                            int k, uint32_t lo, int lane, float (&v)[V]) {
+  if constexpr (FAR) {
+    const uint32_t plo = __builtin_amdgcn_readlane(win.off, k);
+    const uint32_t phi = __builtin_amdgcn_readlane(win.hi, k);
+    // a buffer descriptor over this one row (built in SGPRs from the
+    // read-back address): the same scalar-base load as the near path
+    const uint64_t p = ((uint64_t)phi << 32) | plo;
+    const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void*>((uintptr_t)p), 0, 64 * V * 4, 0x00020000);
+    buf_load<V>(rr, lo, 0, v);
+  } else {
+    buf_load<V>(rs, lo, __builtin_amdgcn_readlane(win.off, k), v);
+  }
+}
+
+template <int V, int U, bool FAR>
 __device__ __forceinline__ void wave_segment(const SpmmArgs& a, __amdgpu_buffer_rsrc_t rs,
-                                             EdgeWindow& win, int eb, int ee, int lane,
+                                             EdgeWindow<FAR>& win, int eb, int ee, int lane,
                                              float (&acc)[V]) {
 #pragma unroll
   for (int k = 0; k < V; ++k) acc[k] = 0.f;
@@ -297,10 +329,9 @@ __device__ __forceinline__ void wave_segment(const SpmmArgs& a, __amdgpu_buffer_
       float ww[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const uint32_t so = __builtin_amdgcn_readlane(win.off, k0 + u);
         ww[u] = __builtin_bit_cast(float,
                                    __builtin_amdgcn_readlane(__builtin_bit_cast(int, win.w), k0 + u));
-        buf_load<V>(rs, lo, so, v[u]);
+        window_load<V, FAR>(rs, win, k0 + u, lo, lane, v[u]);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -310,11 +341,10 @@ __device__ __forceinline__ void wave_segment(const SpmmArgs& a, __amdgpu_buffer_
     }
     for (; e < lim; ++e) {
       const int k0 = e - win.wb;
-      const uint32_t so = __builtin_amdgcn_readlane(win.off, k0);
       const float w =
           __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, win.w), k0));
       float v[V];
-      buf_load<V>(rs, lo, so, v);
+      window_load<V, FAR>(rs, win, k0, lo, lane, v);
 #pragma unroll
       for (int k = 0; k < V; ++k) acc[k] = __fadd_rn(acc[k], __fmul_rn(w, v[k]));
     }
@@ -323,9 +353,9 @@ __device__ __forceinline__ void wave_segment(const SpmmArgs& a, __amdgpu_buffer_
 
 // One chunk (rows owned by chunk, carries) starting at row i; returns the
 // first row of the next chunk.
-template <int V, int U>
+template <int V, int U, bool FAR>
 __device__ __forceinline__ int wave_chunk(const SpmmArgs& a, __amdgpu_buffer_rsrc_t rs,
-                                          EdgeWindow& win, int chunk, int i, int lane) {
+                                          EdgeWindow<FAR>& win, int chunk, int i, int lane) {
   const int e0 = chunk * a.S;
   const int e1 = min(e0 + a.S, a.nnz);
   const bool last = e1 == a.nnz;
@@ -339,7 +369,7 @@ __device__ __forceinline__ int wave_chunk(const SpmmArgs& a, __amdgpu_buffer_rsr
       const int rs0 = uni(a.rowptr[i - 1]);
       if (ri - rs0 > a.L) {
         const int re = min(ri, e1);
-        wave_segment<V, U>(a, rs, win, e0, re, lane, acc);
+        wave_segment<V, U, FAR>(a, rs, win, e0, re, lane, acc);
         vstore<V>(a.carry + (int64_t)chunk * 2 * F + lane * V, acc);
         crow = i - 1;
       }
@@ -351,11 +381,11 @@ __device__ __forceinline__ int wave_chunk(const SpmmArgs& a, __amdgpu_buffer_rsr
     if (!(rb < e1 || last)) break;
     const int re_full = uni(a.rowptr[i + 1]);
     if (re_full - rb <= a.L) {
-      wave_segment<V, U>(a, rs, win, rb, re_full, lane, acc);
+      wave_segment<V, U, FAR>(a, rs, win, rb, re_full, lane, acc);
       vstore<V>(a.out + (int64_t)i * ldo + lane * V, acc);
     } else {
       const int re = min(re_full, e1);
-      wave_segment<V, U>(a, rs, win, rb, re, lane, acc);
+      wave_segment<V, U, FAR>(a, rs, win, rb, re, lane, acc);
       if (re_full <= e1) {
         vstore<V>(a.out + (int64_t)i * ldo + lane * V, acc);
       } else {
@@ -372,7 +402,7 @@ __device__ __forceinline__ int wave_chunk(const SpmmArgs& a, __amdgpu_buffer_rsr
 
 // Each wave walks K consecutive chunks (its edge window and row cursor carry
 // over; only the first chunk needs the row search).
-template <int V, int U>
+template <int V, int U, bool FAR>
 __global__ void __launch_bounds__(kSpmmThreads)
 spmm_wave_kernel(SpmmArgs a) {
   const int lane = threadIdx.x & 63;
@@ -385,11 +415,11 @@ spmm_wave_kernel(SpmmArgs a) {
   if (sc < 0) return;
   const __amdgpu_buffer_rsrc_t rs =
       __builtin_amdgcn_make_buffer_rsrc((void*)a.ubase, 0, a.span, 0x00020000);
-  EdgeWindow win;
+  EdgeWindow<FAR> win;
   win.wb = INT32_MIN / 2;
   const int c0 = sc * K, c1 = min(a.nchunks, c0 + K);
   int i = uni(lower_bound_i32(a.rowptr, a.n_rows, c0 * a.S));
-  for (int c = c0; c < c1; ++c) i = uni(wave_chunk<V, U>(a, rs, win, c, i, lane));
+  for (int c = c0; c < c1; ++c) i = uni(wave_chunk<V, U, FAR>(a, rs, win, c, i, lane));
 }
 
 // For every row that spans chunks, the chunk where it ends adds the partials:
@@ -549,7 +579,7 @@ static void launch_spmm(const SpmmArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(spmm_fixup_kernel, dim3((a.nchunks + 255) / 256), dim3(256), 0, s, a);
 }
 
-template <int V, int U>
+template <int V, int U, bool FAR>
 static void launch_spmm_wave(SpmmArgs& a, hipStream_t s) {
   constexpr int WPB = kSpmmThreads / 64;
   static const int kpw = env_int("VQGNN_SPMM_K", 1);
@@ -557,11 +587,12 @@ static void launch_spmm_wave(SpmmArgs& a, hipStream_t s) {
   const int nsuper = (a.nchunks + a.kpw - 1) / a.kpw;
   const int per_xcd = (nsuper + kNumXcd - 1) / kNumXcd + 1;
   const int grid = kNumXcd * ((per_xcd + WPB - 1) / WPB);
-  hipLaunchKernelGGL((spmm_wave_kernel<V, U>), dim3(grid), dim3(kSpmmThreads), 0, s, a);
+  hipLaunchKernelGGL((spmm_wave_kernel<V, U, FAR>), dim3(grid), dim3(kSpmmThreads), 0, s, a);
   hipLaunchKernelGGL(spmm_fixup_kernel, dim3((a.nchunks + 255) / 256), dim3(256), 0, s, a);
 }
 
-// 0 = automatic (wave kernel where it applies), 1 = lane-group kernel only
+// 0 = automatic (wave kernel where it applies), 1 = lane-group kernel only,
+// 2 = wave kernel with 64-bit row addresses (FAR) even when the range fits
 static int spmm_mode() {
   static const int m = env_int("VQGNN_SPMM_MODE", 0);
   return m;
@@ -594,17 +625,20 @@ template <bool TWO>
 static int dispatch_spmm(SpmmArgs& a, int64_t rows_x, int64_t rows_x2, hipStream_t s) {
   const int F = a.F4 * 4;
   const bool al = (((uintptr_t)a.out | (uintptr_t)a.carry | (uintptr_t)(a.ldo4 * 16)) & 15) == 0;
-  if (spmm_mode() == 0 && al && (F == 64 || F == 128 || F == 256) &&
-      wave_layout(a, rows_x, rows_x2)) {
-    static const int u = env_int("VQGNN_SPMM_U", 8);
+  if (spmm_mode() != 1 && al && (F == 64 || F == 128 || F == 256)) {
+    // one 32-bit buffer range over X and X2 when they are within 4 GiB of
+    // each other (the usual case); else 64-bit row addresses (FAR)
+    const bool near = spmm_mode() != 2 && wave_layout(a, rows_x, rows_x2);
+    if (!near) {
+      a.ubase = nullptr;
+      a.span = 0;
+    }
     if (F == 128) {
-      if (u == 16) launch_spmm_wave<2, 16>(a, s);
-      else if (u == 4) launch_spmm_wave<2, 4>(a, s);
-      else launch_spmm_wave<2, 8>(a, s);
+      if (near) launch_spmm_wave<2, 8, false>(a, s); else launch_spmm_wave<2, 8, true>(a, s);
     } else if (F == 256) {
-      launch_spmm_wave<4, 4>(a, s);
+      if (near) launch_spmm_wave<4, 4, false>(a, s); else launch_spmm_wave<4, 4, true>(a, s);
     } else {
-      launch_spmm_wave<1, 8>(a, s);
+      if (near) launch_spmm_wave<1, 8, false>(a, s); else launch_spmm_wave<1, 8, true>(a, s);
     }
     return check_launch("spmm");
   }

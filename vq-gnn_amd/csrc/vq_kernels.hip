@@ -814,8 +814,8 @@ __global__ void vq_ema_reduce_kernel(const long long* __restrict__ parts, int np
 constexpr int kFinThreads = 256;
 
 __global__ void __launch_bounds__(kFinThreads)
-vq_ema_finalize_kernel(const long long* __restrict__ stats, int nparts, int64_t part_stride,
-                       int shift_f, int shift_g, int M, int D, int W, int ldw,
+vq_ema_finalize_kernel(long long* __restrict__ stats, int nparts, int64_t part_stride,
+                       int zero_after, int shift_f, int shift_g, int M, int D, int W, int ldw,
                        float decay, int laplace, float grad_scale, float epsilon,
                        float* __restrict__ cluster_size, int64_t cs_bstride,
                        float* __restrict__ ema_w, float* __restrict__ emb,
@@ -827,12 +827,18 @@ vq_ema_finalize_kernel(const long long* __restrict__ stats, int nparts, int64_t 
   __shared__ int bad;
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
-  const long long* st = stats + (int64_t)b * M * (W + 1);
+  long long* st = stats + (int64_t)b * M * (W + 1);
   // statistic = integer sum of the per-part fixed-point slabs, decoded once:
-  // round(exact sum * 2^-shift) to fp32 (count column: shift 0)
+  // round(exact sum * 2^-shift) to fp32 (count column: shift 0).  Every entry
+  // is read by exactly one thread; zero_after clears it behind the read so
+  // the slab is zero for the next vqgnn_vq_assign (ema_zeroed = 1).
   auto stat = [&](int64_t i, int shift) {
     long long v = st[i];
-    for (int p = 1; p < nparts; ++p) v += st[(int64_t)p * part_stride + i];
+    if (zero_after) st[i] = 0;
+    for (int p = 1; p < nparts; ++p) {
+      v += st[(int64_t)p * part_stride + i];
+      if (zero_after) st[(int64_t)p * part_stride + i] = 0;
+    }
     return (float)ldexp((double)v, -shift);
   };
   float* cs = cluster_size + (int64_t)b * cs_bstride;
@@ -870,6 +876,10 @@ vq_ema_finalize_kernel(const long long* __restrict__ stats, int nparts, int64_t 
   __syncthreads();
   if (bad) {  // reference raises before touching ema_w / embedding
     if (tid == 0) atomicOr(bad_init, 1);
+    if (zero_after)
+      for (int i = tid; i < M * W; i += kFinThreads)
+        for (int p = 0; p < nparts; ++p)
+          st[(int64_t)p * part_stride + (int64_t)(i / W) * (W + 1) + 1 + i % W] = 0;
     return;
   }
 
@@ -972,8 +982,8 @@ static int launch_assign(const float* X, int64_t ldx, const float* G, int64_t ld
                          int nb, int D, int M, int W, const float* coef, float grad_scale,
                          const float* emb, int ldw, int64_t emb_bstride, int64_t* idx_out,
                          int16_t* codes, int64_t ldc, const int64_t* batch_idx,
-                         unsigned long long* parts, int64_t stat_count, void* workspace,
-                         hipStream_t s) {
+                         unsigned long long* parts, int ema_zeroed, int64_t stat_count,
+                         void* workspace, hipStream_t s) {
   const AssignGeom g = assign_geom(B, nb, M, W);
   const StatShift sh = stat_shift(stat_count, grad_scale);
   const bool want_ema = parts != nullptr;
@@ -987,7 +997,7 @@ static int launch_assign(const float* X, int64_t ldx, const float* G, int64_t ld
   }
   const int wgs = g.parts * nb;
   const int wm = slot_mode(KC, W, D);
-  if (want_ema)
+  if (want_ema && !ema_zeroed)
     (void)hipMemsetAsync(parts, 0, (size_t)nb * M * (W + 1) * sizeof(unsigned long long), s);
 #define VQ_LAUNCH(FU, WMV)                                                                    \
   do {                                                                                        \
@@ -1031,8 +1041,8 @@ extern "C" int vqgnn_vq_assign(const float* X, int64_t ldx, const float* G, int6
                                const float* coef, float grad_scale, const float* embedding,
                                int32_t ldw, int64_t emb_bstride, int64_t* idx_out,
                                int16_t* codes, int64_t ldc, const int64_t* batch_idx,
-                               int64_t* ema_parts, int64_t stat_count, void* workspace,
-                               vqgnn_stream_t stream) {
+                               int64_t* ema_parts, int32_t ema_zeroed, int64_t stat_count,
+                               void* workspace, vqgnn_stream_t stream) {
   clear_error();
   VQGNN_REQUIRE(X && coef && embedding, "vq_assign: null pointer");
   VQGNN_REQUIRE(B > 0 && nb > 0 && D > 0 && M > 0, "vq_assign: bad shape");
@@ -1050,14 +1060,14 @@ extern "C" int vqgnn_vq_assign(const float* X, int64_t ldx, const float* G, int6
   const int kc = W <= 4 ? 1 : (W <= 8 ? 2 : 4);
   if (kc == 1)
     return launch_assign<1>(X, ldx, G, ldg, B, nb, D, M, W, coef, grad_scale, embedding, ldw,
-                            emb_bstride, idx_out, codes, ldc, batch_idx, parts, stat_count,
+                            emb_bstride, idx_out, codes, ldc, batch_idx, parts, ema_zeroed, stat_count,
                             workspace, s);
   if (kc == 2)
     return launch_assign<2>(X, ldx, G, ldg, B, nb, D, M, W, coef, grad_scale, embedding, ldw,
-                            emb_bstride, idx_out, codes, ldc, batch_idx, parts, stat_count,
+                            emb_bstride, idx_out, codes, ldc, batch_idx, parts, ema_zeroed, stat_count,
                             workspace, s);
   return launch_assign<4>(X, ldx, G, ldg, B, nb, D, M, W, coef, grad_scale, embedding, ldw,
-                          emb_bstride, idx_out, codes, ldc, batch_idx, parts, stat_count,
+                          emb_bstride, idx_out, codes, ldc, batch_idx, parts, ema_zeroed, stat_count,
                           workspace, s);
 }
 
@@ -1078,7 +1088,7 @@ extern "C" int vqgnn_vq_ema_reduce(const int64_t* parts, int32_t nparts, int64_t
   return check_launch("ema_reduce");
 }
 
-extern "C" int vqgnn_vq_ema_finalize(const int64_t* ema_parts, int32_t nparts,
+extern "C" int vqgnn_vq_ema_finalize(int64_t* ema_parts, int32_t nparts, int32_t zero_after,
                                      int64_t stat_count, int32_t nb,
                                      int32_t M, int32_t D, int32_t W, int32_t ldw, float decay,
                                      int32_t laplace, float grad_scale, float epsilon,
@@ -1096,8 +1106,9 @@ extern "C" int vqgnn_vq_ema_finalize(const int64_t* ema_parts, int32_t nparts,
   VQGNN_REQUIRE(stat_count > 0, "ema_finalize: stat_count must be > 0");
   const StatShift sh = stat_shift(stat_count, grad_scale);
   hipLaunchKernelGGL(vq_ema_finalize_kernel, dim3(nb), dim3(kFinThreads), 0, as_stream(stream),
-                     reinterpret_cast<const long long*>(ema_parts), nparts,
-                     (int64_t)nb * M * (W + 1), sh.f, sh.g, M, D, W, ldw, decay, laplace,
+                     reinterpret_cast<long long*>(ema_parts), nparts,
+                     (int64_t)nb * M * (W + 1), zero_after, sh.f, sh.g, M, D, W, ldw, decay,
+                     laplace,
                      grad_scale, epsilon, cluster_size, cs_bstride, ema_w, embedding,
                      embedding_output, emb_bstride, rm_f, rv_f, rm_g, rv_g, bad_init);
   return check_launch("ema_finalize");

@@ -71,13 +71,16 @@ def decode_stats(stats: torch.Tensor, D: int, stat_count: int, grad_scale: float
 
 
 def vq_assign(X, G, coef, grad_scale, emb, D, W, idx_out=None, codes=None, batch_idx=None,
-              want_stats=False, stat_count=None):
+              want_stats=False, stat_count=None, stats_out=None):
     """Nearest codeword for every (row, branch); optional EMA statistics.
 
     emb: [nb, M, ldw] view (row-major per branch, arbitrary branch stride).
     Returns the EMA partial slabs [P, nb, M, W+1] (int64 fixed point, see
     decode_stats) if want_stats, else None; their sum over P is the statistic
-    (vq_ema_reduce).  stat_count: rows behind the BN statistics (default B)."""
+    (vq_ema_reduce).  stat_count: rows behind the BN statistics (default B).
+    stats_out: a caller-owned slab [P, nb, M, W+1] int64 that is already ZERO
+    (e.g. left so by vq_ema_finalize(zero_after=True)); it is filled and
+    returned, and the call skips zeroing it."""
     require_gpu(X, "vq_assign")
     B = X.shape[0]
     nb, M, ldw = emb.shape
@@ -94,11 +97,18 @@ def vq_assign(X, G, coef, grad_scale, emb, D, W, idx_out=None, codes=None, batch
         if codes.dtype != torch.int16 or codes.stride(1) != 1:
             raise ValueError("codes must be an int16 [N, ldc] row-major view")
         ldc = codes.stride(0)
+    zeroed = 0
     if want_stats:
-        parts = torch.empty(P, nb, M, W + 1, dtype=torch.int64, device=X.device)
+        if stats_out is not None:
+            if (stats_out.dtype != torch.int64 or tuple(stats_out.shape) != (P, nb, M, W + 1)
+                    or not stats_out.is_contiguous()):
+                raise ValueError(f"stats_out must be a contiguous int64 [{P}, {nb}, {M}, {W + 1}]")
+            parts, zeroed = stats_out, 1
+        else:
+            parts = torch.empty(P, nb, M, W + 1, dtype=torch.int64, device=X.device)
     check(L.vqgnn_vq_assign(ptr(X), _ld(X), ptr(G), _ld(G) if G is not None else 0, B, nb, D,
                             M, W, ptr(coef), float(grad_scale), ptr(emb), ldw, emb.stride(0),
-                            ptr(idx_out), ptr(codes), ldc, ptr(batch_idx), ptr(parts),
+                            ptr(idx_out), ptr(codes), ldc, ptr(batch_idx), ptr(parts), zeroed,
                             int(stat_count if stat_count is not None else B), ptr(ws),
                             stream_ptr()), "vq_assign")
     return parts
@@ -116,14 +126,15 @@ def vq_ema_reduce(parts):
 
 
 def vq_ema_finalize(parts, D, W, decay, laplace, grad_scale, epsilon, cs, ema_w, emb, emb_out,
-                    rm_f, rv_f, rm_g, rv_g, bad_flag, stat_count):
+                    rm_f, rv_f, rm_g, rv_g, bad_flag, stat_count, zero_after=False):
     P, nb, M, _ = parts.shape
     ldw = emb.shape[2]
     if not (ema_w.stride() == emb.stride() == emb_out.stride()):
         raise ValueError("ema_w / embedding / output must share one layout")
     if parts.dtype != torch.int64:
         raise ValueError("EMA statistic slabs are int64 fixed point")
-    check(lib().vqgnn_vq_ema_finalize(ptr(parts), P, int(stat_count), nb, M, D, W, ldw,
+    check(lib().vqgnn_vq_ema_finalize(ptr(parts), P, int(bool(zero_after)), int(stat_count), nb,
+                                      M, D, W, ldw,
                                       float(decay),
                                       int(laplace), float(grad_scale), float(epsilon), ptr(cs),
                                       cs.stride(0), ptr(ema_w), ptr(emb), ptr(emb_out),

@@ -58,10 +58,21 @@ class VQBank(nn.Module):
         self.register_buffer("nbt_f", torch.zeros(nb, dtype=torch.long), persistent=False)
         self.register_buffer("nbt_g", torch.zeros(nb, dtype=torch.long), persistent=False)
         self.register_buffer("bad_flag", torch.zeros(1, dtype=torch.int32), persistent=False)
+        # EMA sufficient-statistic slabs (int64 fixed point, include/vqgnn.h
+        # §3), kept zero between calls: the finalize clears what it consumes,
+        # so the assign needs no memset.  dirty[b]: branch b's slab may hold
+        # data (an update interrupted between assign and finalize).
+        zl = lambda W: torch.zeros(1, nb, M, W + 1, dtype=torch.int64)  # noqa: E731
+        self.register_buffer("stats_f", zl(D), persistent=False)
+        self.register_buffer("stats_u", zl(2 * D), persistent=False)
+        self._dirty = {D: [False] * nb, 2 * D: [False] * nb}
         self.bn_inited = [False] * nb
         # multi-GPU: a dist.CodebookSync (all-reduce of sufficient statistics,
         # all-gather of codes); None on one GPU
         self.comm = None
+        # optional list: (start, end) HIP events around every assign launch
+        # (bench.py times vq_assign_kernel alone with it); None = off
+        self.assign_events = None
         self.comm_max_B = None
         # last batched call's logging stash (vq.py:208-214, :276-277)
         self.last_batch = None       # [4, nb*D] mean_f, std_f, mean_g, std_g
@@ -97,6 +108,31 @@ class VQBank(nn.Module):
             VQBank._arange_cache[key] = t
         return t
 
+    def _slab(self, W, b0, nbr):
+        """Zeroed statistic slab [1, nbr, M, W+1] for branches [b0, b0+nbr)."""
+        buf = self.stats_f if W == self.D else self.stats_u
+        view = buf[:, b0:b0 + nbr]
+        dirty = self._dirty[W]
+        if any(dirty[b0:b0 + nbr]):
+            view.zero_()
+        for b in range(b0, b0 + nbr):
+            dirty[b] = True
+        return view
+
+    def _clean(self, W, b0, nbr):
+        for b in range(b0, b0 + nbr):
+            self._dirty[W][b] = False
+
+    def _assign(self, *args, **kw):
+        if self.assign_events is None:
+            return kernels.vq_assign(*args, **kw)
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        ev[0].record()
+        out = kernels.vq_assign(*args, **kw)
+        ev[1].record()
+        self.assign_events.append(ev)
+        return out
+
     def _sel(self, b0, nbr):
         return slice(b0, b0 + nbr)
 
@@ -121,16 +157,17 @@ class VQBank(nn.Module):
             count = B
             coef, _ = kernels.bn_finalize(None, B, F, False, BN_EVAL, 0.1, 1e-5, 0.0, 0.0, 0.0,
                                           self.rm_f[sl], self.rv_f[sl])
+        slab = self._slab(D, b0, nbr) if training else None
         local = None
         if comm is not None and codes is not None:
             local = torch.empty(B, nbr, dtype=torch.int16, device=X.device)
-            stats = kernels.vq_assign(X, None, coef, 1.0, self.emb[sl], D, D, idx_out=idx_out,
-                                      codes=local, batch_idx=self._arange(B, X.device),
-                                      want_stats=training, stat_count=count)
+            stats = self._assign(X, None, coef, 1.0, self.emb[sl], D, D, idx_out=idx_out,
+                                 codes=local, batch_idx=self._arange(B, X.device),
+                                 want_stats=training, stat_count=count, stats_out=slab)
         else:
-            stats = kernels.vq_assign(X, None, coef, 1.0, self.emb[sl], D, D, idx_out=idx_out,
-                                      codes=codes, batch_idx=batch_idx, want_stats=training,
-                                      stat_count=count)
+            stats = self._assign(X, None, coef, 1.0, self.emb[sl], D, D, idx_out=idx_out,
+                                 codes=codes, batch_idx=batch_idx, want_stats=training,
+                                 stat_count=count, stats_out=slab)
         if comm is not None:
             stats = kernels.vq_ema_reduce(stats)
             comm.allreduce_(stats)
@@ -140,7 +177,8 @@ class VQBank(nn.Module):
             kernels.vq_ema_finalize(stats, D, D, self.decay, self.warm_up_flag, 1.0, self.epsilon,
                                     self.cs[sl], self.ema_w[sl], self.emb[sl], self.emb_out[sl],
                                     self.rm_f[sl], self.rv_f[sl], self.rm_g[sl], self.rv_g[sl],
-                                    self.bad_flag, count)
+                                    self.bad_flag, count, zero_after=True)
+            self._clean(D, b0, nbr)
             self._finish()
 
     def update(self, X, G, b0, nbr, training, idx_out=None, codes=None, batch_idx=None):
@@ -174,17 +212,18 @@ class VQBank(nn.Module):
         self.last_batch = batch
         self.last_inputs = (X, G)
         scale = float(self.grad_normalize_scale[0])
+        slab = self._slab(2 * D, b0, nbr) if training else None
         local = None
         if comm is not None and codes is not None:
             local = torch.empty(B, nbr, dtype=torch.int16, device=X.device)
-            stats = kernels.vq_assign(X, G, coef, scale, self.emb[sl], D, 2 * D,
-                                      idx_out=idx_out, codes=local,
-                                      batch_idx=self._arange(B, X.device), want_stats=training,
-                                      stat_count=count)
+            stats = self._assign(X, G, coef, scale, self.emb[sl], D, 2 * D,
+                                 idx_out=idx_out, codes=local,
+                                 batch_idx=self._arange(B, X.device), want_stats=training,
+                                 stat_count=count, stats_out=slab)
         else:
-            stats = kernels.vq_assign(X, G, coef, scale, self.emb[sl], D, 2 * D,
-                                      idx_out=idx_out, codes=codes, batch_idx=batch_idx,
-                                      want_stats=training, stat_count=count)
+            stats = self._assign(X, G, coef, scale, self.emb[sl], D, 2 * D,
+                                 idx_out=idx_out, codes=codes, batch_idx=batch_idx,
+                                 want_stats=training, stat_count=count, stats_out=slab)
         if comm is not None:
             stats = kernels.vq_ema_reduce(stats)
             comm.allreduce_(stats)
@@ -194,7 +233,9 @@ class VQBank(nn.Module):
             kernels.vq_ema_finalize(stats, D, 2 * D, self.decay, self.warm_up_flag, scale,
                                     self.epsilon, self.cs[sl], self.ema_w[sl], self.emb[sl],
                                     self.emb_out[sl], self.rm_f[sl], self.rv_f[sl],
-                                    self.rm_g[sl], self.rv_g[sl], self.bad_flag, count)
+                                    self.rm_g[sl], self.rv_g[sl], self.bad_flag, count,
+                                    zero_after=True)
+            self._clean(2 * D, b0, nbr)
             self._finish()
 
 
