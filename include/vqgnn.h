@@ -190,12 +190,52 @@ int vqgnn_spmm(const int32_t* rowptr, const int32_t* col, const float* val,
 /* 7. CSR transpose (structure + values) for the backward product
  *    dX = A^T dOut (torch_sparse matmul autograd, convs.py:95).  Output CSR of
  *    A^T with rows sorted by column of A; within a row, entries ordered by
- *    row of A (canonical, deterministic).                                     */
+ *    row of A (canonical, deterministic).  t_val and t_perm are optional;
+ *    t_perm[k] = index in the input CSR of transposed entry k (to carry other
+ *    per-edge values, e.g. GAT coefficients, into transposed order).
+ *    vqgnn_csr_expand_rows: rows[e] = row of edge e (COO row indices).       */
 size_t vqgnn_csr_transpose_workspace(int32_t n_rows, int32_t n_cols, int64_t nnz);
 int vqgnn_csr_transpose(const int32_t* rowptr, const int32_t* col, const float* val,
                         int32_t n_rows, int32_t n_cols, int64_t nnz,
                         int32_t* t_rowptr, int32_t* t_col, float* t_val,
-                        void* workspace, vqgnn_stream_t stream);
+                        int32_t* t_perm, void* workspace, vqgnn_stream_t stream);
+int vqgnn_csr_expand_rows(const int32_t* rowptr, int32_t n_rows, int64_t nnz,
+                          int32_t* rows, vqgnn_stream_t stream);
+
+/* ------------------------------------------------------------------------ *
+ * 8. GAT attention aggregation (OurGATConv, convs.py:165-266, vq_softmax
+ *    utils/vq_softmax.py:33-57, normalisation models.py:178-179/:187-189).
+ *    x_in = [X (rows < B) ; X2 (rows >= B) ; ones column if ones != 0].
+ *    gat_alpha: alpha_l/r[i] = x_in[i] . att_l/r (att length F + ones) and
+ *      params[5] = {max_l, max_r, s, ds/dmax_l, ds/dmax_r} with
+ *      s = sqrt(max_l^2+1) * sqrt(max_r^2+1)                  (convs.py:209-211)
+ *    gat_coef: coef[e] = exp(leaky(alpha_l[col]/s + alpha_r[row]/s)) * val[e]
+ *      (no max shift, no softmax normalisation), den[i] = sum_e coef[e] in
+ *      CSR order (the ones column of the aggregation)         (convs.py:249-266)
+ *    The aggregation itself is vqgnn_spmm with val = coef.
+ *    gat_normalize: rows < B: out[i][:F] /= den[i] + eps       (models.py:188)
+ *    gat_edge_grad: backward of the coefficient chain for every edge:
+ *      dcoef = dy[row] . x_in[col][:F] + dden[row];  da = dcoef*coef*leaky'(a);
+ *      dalpha_l[col] += da/s; dalpha_r[row] += da/s; ds_row[row] += -da*a/s
+ *      (atomic adds: the caller zeroes dalpha_l, dalpha_r, ds_row).
+ * ------------------------------------------------------------------------ */
+size_t vqgnn_gat_alpha_workspace(int32_t n);
+int vqgnn_gat_alpha(const float* X, int64_t ldx, const float* X2, int64_t ldx2,
+                    int32_t B, int32_t n, int32_t F, int32_t ones,
+                    const float* att_l, const float* att_r, float* alpha_l, float* alpha_r,
+                    float* params, void* workspace, vqgnn_stream_t stream);
+int vqgnn_gat_coef(const int32_t* rowptr, const int32_t* col, const float* val,
+                   int32_t n_rows, int64_t nnz, const float* alpha_l, const float* alpha_r,
+                   const float* params, float negative_slope, float* coef, float* den,
+                   vqgnn_stream_t stream);
+int vqgnn_gat_normalize(float* out, int64_t ldo, int32_t B, int32_t F, const float* den,
+                        float eps, vqgnn_stream_t stream);
+int vqgnn_gat_edge_grad(const int32_t* rows, const int32_t* col, const float* coef,
+                        int64_t nnz, const float* X, int64_t ldx, const float* X2,
+                        int64_t ldx2, int32_t B, int32_t F, const float* dy, int64_t lddy,
+                        const float* dden, const float* alpha_l, const float* alpha_r,
+                        const float* params, float negative_slope, float* dalpha_l,
+                        float* dalpha_r, float* ds_row, vqgnn_stream_t stream);
 
 #ifdef __cplusplus
 }

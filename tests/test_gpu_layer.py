@@ -143,3 +143,59 @@ def test_opt_in_backward_vq_update_moves_codebooks():
     out.sum().backward()
     assert not torch.equal(model.convs[1]._bank.emb, emb_before)
     assert model.convs[1]._bank.bn_inited[0]
+
+
+def test_layer_gat_forward_backward_vs_oracle():
+    """conv_type='GAT' (models.py:93-97, :178-189): codebook gather, ones
+    column, attention aggregation, normalisation of the batch rows, Linear."""
+    torch.manual_seed(3)
+    g, b = _small_batch("GAT", seed=3)
+    F_in, F_out, M, D = 32, 16, 64, 4
+    layer = _layer(F_in, F_out, M, g.N, "GAT")
+    att_l = layer.conv.att_l.detach().view(-1).clone()
+    att_r = layer.conv.att_r.detach().view(-1).clone()
+    lin_w = layer.gnn_transform.weight.detach().clone()
+    lin_b = layer.gnn_transform.bias.detach().clone()
+    layer = layer.to(DEV).train()
+    x = torch.randn(b.B, F_in)
+    xg = x.clone().to(DEV).requires_grad_(True)
+    out, *_ = layer(xg, graph.batch_to_device(b, DEV), 1.0, False)
+    codes = layer._codes.cpu().numpy()
+    emb_out = layer._bank.emb_out.cpu().numpy()
+    xin = conv_ref.gather_input(x, b.subset, b.B, codes, emb_out, D).numpy()
+    xin1 = np.concatenate([xin, np.ones((b.n, 1), np.float32)], 1)
+    agg, _ = conv_ref.gat_forward(xin1, att_l.numpy(), att_r.numpy(), b.rowptr, b.col, b.val,
+                                  B=b.B, normalize=True)
+    ref = agg[:b.B] @ lin_w.t() + lin_b
+    torch.testing.assert_close(out.detach().cpu(), ref, rtol=1e-4, atol=1e-4)
+    # backward vs fp64 autograd of the same chain
+    R = torch.randn(b.B, F_out)
+    (out * R.to(DEV)).sum().backward()
+    x64 = x.double().requires_grad_(True)
+    agg64 = conv_ref.gat_forward_fp64(x64, torch.from_numpy(xin[b.B:]), att_l.double(),
+                                      att_r.double(), b.rowptr, b.col, b.val, b.B)
+    ((agg64[:b.B] @ lin_w.double().t() + lin_b.double()) * R.double()).sum().backward()
+    np.testing.assert_allclose(xg.grad.cpu().numpy(), x64.grad.numpy(), rtol=2e-3, atol=2e-4)
+    assert layer.conv.att_l.grad is not None and torch.isfinite(layer.conv.att_l.grad).all()
+
+
+def test_model_gat_train_step():
+    torch.manual_seed(4)
+    g, b = _small_batch("GAT", seed=4)
+    model = LowRankGNN(32, 16, 7, 2, 0.0, 64, 4, g.N, no_second_fc=True, skip=True,
+                       grad_scale=[1, 1], warm_up_flag=True, conv_type='GAT').to(DEV)
+    batch_A = graph.batch_to_device(b, DEV)
+    x = torch.randn(b.B, 32, device=DEV)
+    model.train()
+    with torch.no_grad():
+        for layer_idx in range(1, 3):
+            model.init((x, batch_A), layer_idx)
+    y = torch.randint(0, 7, (b.B,), device=DEV)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+    for _ in range(2):
+        opt.zero_grad()
+        out, _, info_b = model((x, batch_A), 1.0)
+        loss = torch.nn.functional.cross_entropy(out, y) + info_b
+        loss.backward()
+        opt.step()
+        assert torch.isfinite(loss)

@@ -109,16 +109,21 @@ def test_two_source_far_apart_inputs():
     rowptr, col, val = _random_csr(n, n, 14, rng)
     x = rng.standard_normal((n, F)).astype(np.float32)
     a = _dev_csr(rowptr, col, val, n, n)
-    xd = torch.from_numpy(x[:B]).to(DEV)
-    gap = torch.empty(5 << 30, dtype=torch.uint8, device=DEV)       # 5 GiB in between
-    x2d = torch.from_numpy(x[B:]).to(DEV)
-    assert abs(x2d.data_ptr() - xd.data_ptr()) > (4 << 30) or gap.numel() == 0
+    # both inputs carved out of one allocation, 5 GiB apart
+    gap = 5 << 30
+    nb2 = (n - B) * F * 4
+    big = torch.empty(gap + nb2, dtype=torch.uint8, device=DEV)
+    xd = big[:B * F * 4].view(torch.float32).view(B, F)
+    x2d = big[gap:gap + nb2].view(torch.float32).view(n - B, F)
+    xd.copy_(torch.from_numpy(x[:B]))
+    x2d.copy_(torch.from_numpy(x[B:]))
+    assert x2d.data_ptr() - xd.data_ptr() >= (4 << 30)
     out = kernels.spmm(a.rowptr, a.col, a.value, n, a.nnz(), xd, F, X2=x2d, B=B)
     ref = conv_ref.spmm_seq(rowptr, col, val, x)
     inside = np.diff(rowptr) <= 128
     assert np.array_equal(out.cpu().numpy()[inside], ref[inside])
     np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=1e-5, atol=1e-5)
-    del gap
+    del big
 
 
 def test_scatter_codes():

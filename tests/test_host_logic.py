@@ -147,3 +147,32 @@ def test_no_cpu_fallback():
     from vq_gnn_amd import kernels
     with pytest.raises(RuntimeError, match="GPU"):
         kernels.bn_stats(torch.zeros(4, 8), None, 8)
+
+
+def test_gat_oracle_known_answer():
+    """3-node KAT for the GAT restatement, computed independently with
+    Python floats from convs.py:189-266 / models.py:187-189."""
+    import math
+    x = np.array([[1.0, 0.0, 1.0], [0.0, 2.0, 1.0], [-1.0, 1.0, 1.0]], dtype=np.float32)
+    att_l = np.array([0.5, -0.25, 0.1], dtype=np.float32)
+    att_r = np.array([-0.2, 0.3, 0.05], dtype=np.float32)
+    # row 0 <- {0, 1}, row 1 <- {2}, row 2 <- {0, 1, 2}
+    rowptr = np.array([0, 2, 3, 6])
+    col = np.array([0, 1, 2, 0, 1, 2])
+    val = np.array([0.5, 2.0, 1.0, 1.0, 0.25, 3.0], dtype=np.float32)
+    out, coef = conv_ref.gat_forward(x, att_l, att_r, rowptr, col, val, B=2, normalize=True)
+    al = [sum(float(x[i, c]) * float(att_l[c]) for c in range(3)) for i in range(3)]
+    ar = [sum(float(x[i, c]) * float(att_r[c]) for c in range(3)) for i in range(3)]
+    s = math.sqrt(max(al) ** 2 + 1) * math.sqrt(max(ar) ** 2 + 1)
+    rows = [0, 0, 1, 2, 2, 2]
+    exp_coef = []
+    for e in range(6):
+        a = al[col[e]] / s + ar[rows[e]] / s
+        a = a if a > 0 else 0.2 * a
+        exp_coef.append(math.exp(a) * float(val[e]))
+    np.testing.assert_allclose(coef.numpy(), exp_coef, rtol=1e-6)
+    ref = np.zeros((3, 3))
+    for e in range(6):
+        ref[rows[e]] += exp_coef[e] * x[col[e]].astype(np.float64)
+    ref[:2, :2] /= ref[:2, 2:] + 1e-16
+    np.testing.assert_allclose(out.numpy(), ref[:, :2], rtol=1e-6, atol=1e-7)

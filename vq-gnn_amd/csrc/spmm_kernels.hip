@@ -517,7 +517,7 @@ __global__ void expand_rows_kernel(const int32_t* __restrict__ rowptr, int n_row
     if (rowptr[mid] <= e) lo = mid; else hi = mid - 1;
   }
   rows[e] = lo;
-  iota[e] = e;
+  if (iota) iota[e] = e;
 }
 
 __global__ void transpose_finish_kernel(const int32_t* __restrict__ sorted_cols,
@@ -525,12 +525,14 @@ __global__ void transpose_finish_kernel(const int32_t* __restrict__ sorted_cols,
                                         const int32_t* __restrict__ rows,
                                         const float* __restrict__ val, int nnz, int n_cols,
                                         int32_t* __restrict__ t_rowptr,
-                                        int32_t* __restrict__ t_col, float* __restrict__ t_val) {
+                                        int32_t* __restrict__ t_col, float* __restrict__ t_val,
+                                        int32_t* __restrict__ t_perm) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t < nnz) {
     const int e = perm[t];
     t_col[t] = rows[e];
     if (t_val) t_val[t] = val[e];
+    if (t_perm) t_perm[t] = e;
   }
   if (t <= n_cols) {  // t_rowptr[c] = first position with sorted_col >= c
     int lo = 0, hi = nnz;
@@ -760,7 +762,7 @@ extern "C" size_t vqgnn_csr_transpose_workspace(int32_t n_rows, int32_t n_cols, 
 extern "C" int vqgnn_csr_transpose(const int32_t* rowptr, const int32_t* col, const float* val,
                                    int32_t n_rows, int32_t n_cols, int64_t nnz,
                                    int32_t* t_rowptr, int32_t* t_col, float* t_val,
-                                   void* workspace, vqgnn_stream_t stream) {
+                                   int32_t* t_perm, void* workspace, vqgnn_stream_t stream) {
   clear_error();
   VQGNN_REQUIRE(rowptr && t_rowptr && n_rows >= 0 && n_cols >= 0, "csr_transpose: bad args");
   VQGNN_REQUIRE(nnz < (int64_t)INT32_MAX, "csr_transpose: nnz >= 2^31");
@@ -793,6 +795,18 @@ extern "C" int vqgnn_csr_transpose(const int32_t* rowptr, const int32_t* col, co
   }
   const int tot = n > n_cols + 1 ? n : n_cols + 1;
   hipLaunchKernelGGL(transpose_finish_kernel, dim3((tot + 255) / 256), dim3(256), 0, s, keys_out,
-                     perm, rows, val, n, n_cols, t_rowptr, t_col, t_val);
+                     perm, rows, val, n, n_cols, t_rowptr, t_col, t_val, t_perm);
   return check_launch("csr_transpose");
+}
+
+extern "C" int vqgnn_csr_expand_rows(const int32_t* rowptr, int32_t n_rows, int64_t nnz,
+                                     int32_t* rows, vqgnn_stream_t stream) {
+  clear_error();
+  VQGNN_REQUIRE(nnz < (int64_t)INT32_MAX && n_rows >= 0, "csr_expand_rows: bad shape");
+  if (nnz == 0) return VQGNN_OK;
+  VQGNN_REQUIRE(rowptr && rows && n_rows > 0, "csr_expand_rows: null pointer");
+  const int n = (int)nnz;
+  hipLaunchKernelGGL(expand_rows_kernel, dim3((n + 255) / 256), dim3(256), 0, as_stream(stream),
+                     rowptr, n_rows, rows, (int32_t*)nullptr, n);
+  return check_launch("csr_expand_rows");
 }

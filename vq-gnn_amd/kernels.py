@@ -187,14 +187,78 @@ def spmm(rowptr, col, val, n_rows, nnz, X, F, X2=None, B=None, out=None):
     return out
 
 
-def csr_transpose(rowptr, col, val, n_rows, n_cols, nnz):
+def csr_transpose(rowptr, col, val, n_rows, n_cols, nnz, want_perm=False):
+    """-> (t_rowptr, t_col, t_val[, t_perm]); t_perm[k] = input edge of entry k."""
     dev = rowptr.device
     t_rowptr = torch.empty(n_cols + 1, dtype=torch.int32, device=dev)
     t_col = torch.empty(max(nnz, 1), dtype=torch.int32, device=dev)
     t_val = torch.empty(max(nnz, 1), dtype=torch.float32, device=dev)
+    t_perm = torch.empty(max(nnz, 1), dtype=torch.int32, device=dev) if want_perm else None
     L = lib()
     ws = workspace(L.vqgnn_csr_transpose_workspace(n_rows, n_cols, nnz), dev)
     check(L.vqgnn_csr_transpose(ptr(rowptr), ptr(col), ptr(val), n_rows, n_cols, nnz,
-                                ptr(t_rowptr), ptr(t_col), ptr(t_val), ptr(ws), stream_ptr()),
-          "csr_transpose")
+                                ptr(t_rowptr), ptr(t_col), ptr(t_val), ptr(t_perm), ptr(ws),
+                                stream_ptr()), "csr_transpose")
+    if want_perm:
+        return t_rowptr, t_col[:nnz], t_val[:nnz], t_perm[:nnz]
     return t_rowptr, t_col[:nnz], t_val[:nnz]
+
+
+def csr_expand_rows(rowptr, n_rows, nnz):
+    """COO row index of every CSR entry (int32 [nnz])."""
+    rows = torch.empty(max(nnz, 1), dtype=torch.int32, device=rowptr.device)
+    check(lib().vqgnn_csr_expand_rows(ptr(rowptr), int(n_rows), int(nnz), ptr(rows),
+                                      stream_ptr()), "csr_expand_rows")
+    return rows[:nnz]
+
+
+# ---- GAT (include/vqgnn.h §8) ----
+
+def gat_alpha(X, att_l, att_r, F, X2=None, B=None, ones=True):
+    """alpha_l, alpha_r [n] and params [5] = (max_l, max_r, s, ds/dmax_l, ds/dmax_r)."""
+    require_gpu(X, "gat_alpha")
+    dev = X.device
+    Bv = int(B) if X2 is not None else X.shape[0]
+    n = Bv + (X2.shape[0] if X2 is not None else 0)
+    al = torch.empty(n, dtype=torch.float32, device=dev)
+    ar = torch.empty(n, dtype=torch.float32, device=dev)
+    params = torch.empty(5, dtype=torch.float32, device=dev)
+    L = lib()
+    ws = workspace(L.vqgnn_gat_alpha_workspace(n), dev)
+    check(L.vqgnn_gat_alpha(ptr(X), _ld(X), ptr(X2), _ld(X2) if X2 is not None else 0, Bv, n,
+                            int(F), int(bool(ones)), ptr(att_l), ptr(att_r), ptr(al), ptr(ar),
+                            ptr(params), ptr(ws), stream_ptr()), "gat_alpha")
+    return al, ar, params
+
+
+def gat_coef(rowptr, col, val, n_rows, nnz, al, ar, params, negative_slope=0.2):
+    """-> (coef [nnz], den [n_rows])."""
+    dev = al.device
+    coef = torch.empty(max(nnz, 1), dtype=torch.float32, device=dev)
+    den = torch.empty(n_rows, dtype=torch.float32, device=dev)
+    check(lib().vqgnn_gat_coef(ptr(rowptr), ptr(col), ptr(val), int(n_rows), int(nnz), ptr(al),
+                               ptr(ar), ptr(params), float(negative_slope), ptr(coef), ptr(den),
+                               stream_ptr()), "gat_coef")
+    return coef[:nnz], den
+
+
+def gat_normalize(out, B, F, den, eps=1e-16):
+    check(lib().vqgnn_gat_normalize(ptr(out), _ld(out), int(B), int(F), ptr(den), float(eps),
+                                    stream_ptr()), "gat_normalize")
+
+
+def gat_edge_grad(rows, col, coef, nnz, X, F, dy, dden, al, ar, params, X2=None, B=None,
+                  negative_slope=0.2):
+    """-> (dalpha_l [n], dalpha_r [n], ds_row [n]) for the coefficient chain."""
+    dev = X.device
+    n = al.shape[0]
+    dal = torch.zeros(n, dtype=torch.float32, device=dev)
+    dar = torch.zeros(n, dtype=torch.float32, device=dev)
+    dsr = torch.zeros(n, dtype=torch.float32, device=dev)
+    Bv = int(B) if X2 is not None else X.shape[0]
+    check(lib().vqgnn_gat_edge_grad(ptr(rows), ptr(col), ptr(coef), int(nnz), ptr(X), _ld(X),
+                                    ptr(X2), _ld(X2) if X2 is not None else 0, Bv, int(F),
+                                    ptr(dy), _ld(dy), ptr(dden), ptr(al), ptr(ar), ptr(params),
+                                    float(negative_slope), ptr(dal), ptr(dar), ptr(dsr),
+                                    stream_ptr()), "gat_edge_grad")
+    return dal, dar, dsr

@@ -16,7 +16,7 @@ import torch
 
 
 class CSR:
-    __slots__ = ("rowptr", "col", "value", "_sizes", "_t", "_host_nnz")
+    __slots__ = ("rowptr", "col", "value", "_sizes", "_t", "_host_nnz", "_rows", "t_perm")
 
     def __init__(self, rowptr: torch.Tensor, col: torch.Tensor, value: torch.Tensor | None,
                  sparse_sizes):
@@ -27,6 +27,8 @@ class CSR:
         self.value = value.to(torch.float32).contiguous()
         self._sizes = (int(sparse_sizes[0]), int(sparse_sizes[1]))
         self._t = None
+        self._rows = None
+        self.t_perm = None
         self._host_nnz = int(self.col.shape[0])
         if self.rowptr.shape[0] != self._sizes[0] + 1:
             raise ValueError("rowptr must have n_rows + 1 entries")
@@ -85,6 +87,8 @@ class CSR:
         out.value = self.value.to(device, non_blocking=non_blocking)
         out._sizes = self._sizes
         out._t = None
+        out._rows = None
+        out.t_perm = None
         out._host_nnz = self._host_nnz
         return out
 
@@ -92,18 +96,30 @@ class CSR:
         return self.to(device if device is not None else "cuda")
 
     def transposed(self):
-        """A^T as CSR, built on the device by vqgnn_csr_transpose; cached."""
+        """A^T as CSR, built on the device by vqgnn_csr_transpose; cached, with
+        the permutation ``t_perm`` (transposed entry -> input entry)."""
         if self._t is None:
             from . import kernels
-            tr, tc, tv = kernels.csr_transpose(self.rowptr, self.col, self.value,
-                                               self._sizes[0], self._sizes[1], self._host_nnz)
+            tr, tc, tv, tp = kernels.csr_transpose(self.rowptr, self.col, self.value,
+                                                   self._sizes[0], self._sizes[1],
+                                                   self._host_nnz, want_perm=True)
             t = CSR.__new__(CSR)
             t.rowptr, t.col, t.value = tr, tc, tv
             t._sizes = (self._sizes[1], self._sizes[0])
             t._t = self
             t._host_nnz = self._host_nnz
+            t._rows = None
+            t.t_perm = None
+            self.t_perm = tp
             self._t = t
         return self._t
+
+    def rows(self):
+        """COO row index of every entry (int32, on the device); cached."""
+        if self._rows is None:
+            from . import kernels
+            self._rows = kernels.csr_expand_rows(self.rowptr, self._sizes[0], self._host_nnz)
+        return self._rows
 
     def __repr__(self):
         return f"CSR(sizes={self._sizes}, nnz={self._host_nnz}, device={self.device})"
