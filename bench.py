@@ -88,6 +88,11 @@ def main():
         tot = comm.global_count(B)
         comm.cache_count(B, tot)
         bank.comm_max_B = comm.global_max(B)
+    gat = None
+    if cfg["conv"] == "GAT":
+        from vq_gnn_amd.convs_gat import OurGATConv
+        torch.manual_seed(4)
+        gat = OurGATConv(F + 1, F + 1, bias=False, add_self_loops=False).to(dev)
     # codebook state = one feature_update warm pass
     bank.feature_update(Xd, 0, nb, True, codes=codes, batch_idx=bidx)
     torch.cuda.synchronize()
@@ -107,7 +112,11 @@ def main():
         x_first, _ = kernels.gather_codewords(subset, B, codes, bank.emb_out, D)
         if record:
             e[2].record()
-        kernels.spmm(adj.rowptr, adj.col, adj.value, n, nnz, Xd, F, X2=x_first, B=B)
+        if gat is not None:     # attention aggregation (alpha, coef, SpMM, normalise)
+            with torch.no_grad():
+                gat.fused_forward(Xd, adj, x_first, B)
+        else:
+            kernels.spmm(adj.rowptr, adj.col, adj.value, n, nnz, Xd, F, X2=x_first, B=B)
         if record:
             e[3].record()
             ev.append(e)
@@ -164,7 +173,9 @@ def main():
                 pmc = pm.get("hbm_bytes_per_launch", {})
         except (OSError, ValueError):
             pmc = {}
-    rl_spmm = dict(kernel="spmm_wave_kernel+spmm_fixup_kernel", bound="hbm",
+    agg_name = ("gat aggregation (alpha+coef+spmm+normalize)" if gat is not None
+                else "spmm_wave_kernel+spmm_fixup_kernel")
+    rl_spmm = dict(kernel=agg_name, bound="hbm",
                    achieved=spmm_bytes / (spmm_ms * 1e-3) / 1e9, peak=8000.0, unit="GB/s",
                    bytes_per_launch=spmm_bytes, ms_per_launch=spmm_ms,
                    traffic=pmc.get("spmm_wave_kernel"))
@@ -180,7 +191,7 @@ def main():
                     kernel=dominant["kernel"])
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and gat is None:
         from oracle.cpu_baseline import layer_step_timer
         threads = min(16, os.cpu_count() or 1)
         t_cpu, nsteps = layer_step_timer(X, G, batch, codes0, M, D, threads,
@@ -197,7 +208,8 @@ def main():
             ms_per_step=ms_step, higher_is_better=True, scaling="weak", vs_baseline=None,
             dtype="f32", data="synthetic (seeded arxiv-shaped graph, random features)",
             config=dict(workload=f"{args.config}: one layer step (VQ {args.semantics} + EMA for "
-                                 f"{nb} branches, codeword gather, SpMM)",
+                                 f"{nb} branches, codeword gather, "
+                                 f"{'GAT attention aggregation' if gat is not None else 'SpMM'})",
                         B=B, B_prime=n - B, nnz=nnz, F=F, M=M, D=D, W=W,
                         parallelism=f"dp{world}"),
             roofline=roofline,
