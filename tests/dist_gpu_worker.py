@@ -1,0 +1,67 @@
+"""Worker for tests/test_gpu_dist.py (launched by torch.distributed.run, 2 ranks
+on one GPU over gloo): each rank runs VQBank.feature_update + update on its
+half of a batch with CodebookSync; rank 0 then replays the union batch in a
+single-process bank.  Results -> <out>/r<rank>.npz."""
+import os
+import sys
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main(out_dir):
+    dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    import vqgnn_pkg
+    vqgnn_pkg.load()
+    from vq_gnn_amd.dist import CodebookSync
+    from vq_gnn_amd.vq import VQBank
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    nb, M, D, N, Bu = 6, 64, 4, 4000, 3000
+    F = nb * D
+    gen = torch.Generator().manual_seed(11)
+    X = torch.randn(Bu, F, generator=gen)
+    G = torch.randn(Bu, F, generator=gen) * 1e-3
+    node = torch.randperm(N, generator=gen)[:Bu]
+    codes0 = torch.randint(0, M, (N, nb), dtype=torch.int16, generator=gen)
+
+    def fresh_bank():
+        torch.manual_seed(0)
+        bank = VQBank(nb, M, D, warm_up_flag=True)
+        for b in range(nb):
+            bank.init_branch(b)
+        return bank.to(dev)
+
+    mine = torch.arange(rank, Bu, world)          # this rank's rows of the union batch
+    bank = fresh_bank()
+    bank.comm = CodebookSync(count_group=dist.new_group(backend="gloo"))
+    codes = codes0.to(dev)
+    Xr, Gr, nr = X[mine].to(dev), G[mine].to(dev), node[mine].to(dev)
+    bank.feature_update(Xr, 0, nb, True, codes=codes, batch_idx=nr)
+    bank.update(Xr, Gr, 0, nb, True, codes=codes, batch_idx=nr)
+    torch.cuda.synchronize()
+    res = {k: getattr(bank, k).cpu().numpy() for k in
+           ("emb", "emb_out", "ema_w", "cs", "rm_f", "rv_f", "rm_g", "rv_g")}
+    res["codes"] = codes.cpu().numpy()
+    if rank == 0:                                  # single-process union batch
+        ref = fresh_bank()
+        rc = codes0.to(dev)
+        Xu, Gu, nu = X.to(dev), G.to(dev), node.to(dev)
+        ref.feature_update(Xu, 0, nb, True, codes=rc, batch_idx=nu)
+        ref.update(Xu, Gu, 0, nb, True, codes=rc, batch_idx=nu)
+        torch.cuda.synchronize()
+        for k in ("emb", "emb_out", "ema_w", "cs", "rm_f", "rv_f", "rm_g", "rv_g"):
+            res["ref_" + k] = getattr(ref, k).cpu().numpy()
+        res["ref_codes"] = rc.cpu().numpy()
+    np.savez(os.path.join(out_dir, f"r{rank}.npz"), **res)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])

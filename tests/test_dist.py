@@ -1,0 +1,65 @@
+"""Multi-process host logic of the data-parallel path (vq-gnn_amd/dist.py) on
+CPU: world_size 2 over gloo, rendezvous on 127.0.0.1."""
+import os
+import socket
+
+import numpy as np
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, out_dir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import vqgnn_pkg
+    vqgnn_pkg.load()
+    from vq_gnn_amd.dist import CodebookSync
+    sync = CodebookSync(count_group=dist.new_group(backend="gloo"))
+    B = [5, 3][rank]
+    res = {}
+    res["count"] = sync.global_count(B)
+    res["max"] = sync.global_max(B)
+    # BN sums (fp64) and EMA statistic (int64) all-reduce
+    sums = torch.arange(8, dtype=torch.float64).view(4, 2) * (rank + 1)
+    sync.allreduce_(sums)
+    res["sums"] = sums.numpy()
+    st = torch.full((1, 2, 3, 5), rank + 1, dtype=torch.int64)
+    st[0, 1, 2, 4] = (1 << 40) * (rank + 1)           # large fixed-point values stay exact
+    sync.allreduce_(st)
+    res["stats"] = st.numpy()
+    # codes: rank r owns nodes {r, r+2, ...}
+    idx = torch.arange(rank, 2 * B, 2, dtype=torch.int64)[:B]
+    loc = (idx[:, None] * 10 + torch.arange(3)[None]).to(torch.int16)
+    all_idx, all_loc = sync.gather_codes(idx, loc)
+    res["all_idx"] = all_idx.numpy()
+    res["all_loc"] = all_loc.numpy()
+    np.savez(os.path.join(out_dir, f"r{rank}.npz"), **res)
+    dist.destroy_process_group()
+
+
+def test_codebook_sync_gloo_world2(tmp_path):
+    port = _free_port()
+    mp.spawn(_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    r = [np.load(tmp_path / f"r{k}.npz") for k in range(2)]
+    for k in range(2):
+        assert int(r[k]["count"]) == 8 and int(r[k]["max"]) == 5
+        np.testing.assert_array_equal(r[k]["sums"], np.arange(8).reshape(4, 2) * 3.0)
+        st = r[k]["stats"]
+        assert st[0, 0, 0, 0] == 3 and st[0, 1, 2, 4] == 3 * (1 << 40)
+        # padded union of (batch_idx, codes), rank-major
+        idx, loc = r[k]["all_idx"], r[k]["all_loc"]
+        assert idx.shape == (10,) and loc.shape == (10, 3)
+        np.testing.assert_array_equal(idx[:5], [0, 2, 4, 6, 8])
+        np.testing.assert_array_equal(idx[5:], [1, 3, 5, -1, -1])
+        valid = idx >= 0
+        np.testing.assert_array_equal(loc[valid], idx[valid, None] * 10 + np.arange(3))
+    # every rank sees the same gathered codes (replicas stay identical)
+    np.testing.assert_array_equal(r[0]["all_loc"], r[1]["all_loc"])
