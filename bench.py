@@ -37,6 +37,9 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
+    # rehearsal of the N>1 path on one GPU: --backend gloo with
+    # VQGNN_BENCH_ONE_DEVICE=1 puts every rank on cuda:0
+    p.add_argument("--backend", default="nccl", choices=["nccl", "gloo"])
     return p.parse_args()
 
 
@@ -54,11 +57,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("VQGNN_BENCH_ONE_DEVICE") == "1":
+        local_rank = 0
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     comm = None
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
         from vq_gnn_amd.dist import CodebookSync
         comm = CodebookSync(count_group=dist.new_group(backend="gloo"))
 
@@ -117,6 +125,7 @@ def main():
                 gat.fused_forward(Xd, adj, x_first, B)
         else:
             kernels.spmm(adj.rowptr, adj.col, adj.value, n, nnz, Xd, F, X2=x_first, B=B)
+        bank.sync_codes()   # multi-GPU: other ranks' codes, exchanged behind gather + SpMM
         if record:
             e[3].record()
             ev.append(e)

@@ -44,6 +44,7 @@ def main(out_dir):
     Xr, Gr, nr = X[mine].to(dev), G[mine].to(dev), node[mine].to(dev)
     bank.feature_update(Xr, 0, nb, True, codes=codes, batch_idx=nr)
     bank.update(Xr, Gr, 0, nb, True, codes=codes, batch_idx=nr)
+    bank.sync_codes()
     torch.cuda.synchronize()
     res = {k: getattr(bank, k).cpu().numpy() for k in
            ("emb", "emb_out", "ema_w", "cs", "rm_f", "rv_f", "rm_g", "rv_g")}

@@ -38,9 +38,15 @@ def _worker(rank, world, port, out_dir):
     # codes: rank r owns nodes {r, r+2, ...}
     idx = torch.arange(rank, 2 * B, 2, dtype=torch.int64)[:B]
     loc = (idx[:, None] * 10 + torch.arange(3)[None]).to(torch.int16)
-    all_idx, all_loc = sync.gather_codes(idx, loc)
+    _, all_idx, all_loc = sync.gather_codes(idx, loc, M=64)
     res["all_idx"] = all_idx.numpy()
     res["all_loc"] = all_loc.numpy()
+    # int16 wire format (M > 256) and the async form
+    pend, ai2, al2 = sync.gather_codes(idx, loc * 7, M=4096, async_op=True)
+    for w in pend:
+        w.wait()
+    res["all_loc16"] = al2.numpy()
+    res["all_idx16"] = ai2.numpy()
     np.savez(os.path.join(out_dir, f"r{rank}.npz"), **res)
     dist.destroy_process_group()
 
@@ -61,5 +67,9 @@ def test_codebook_sync_gloo_world2(tmp_path):
         np.testing.assert_array_equal(idx[5:], [1, 3, 5, -1, -1])
         valid = idx >= 0
         np.testing.assert_array_equal(loc[valid], idx[valid, None] * 10 + np.arange(3))
+        assert loc.dtype == np.uint8 and r[k]["all_loc16"].dtype == np.int16
+        l16 = r[k]["all_loc16"]
+        np.testing.assert_array_equal(l16[valid], (idx[valid, None] * 10 + np.arange(3)) * 7)
+        np.testing.assert_array_equal(r[k]["all_idx16"], idx)
     # every rank sees the same gathered codes (replicas stay identical)
     np.testing.assert_array_equal(r[0]["all_loc"], r[1]["all_loc"])

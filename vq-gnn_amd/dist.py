@@ -51,31 +51,48 @@ class CodebookSync:
         """Fixed batches (bench): remember the global count for this local B."""
         self._count_cache[B] = total
 
+    @staticmethod
+    def _wire_dtype(M):
+        return torch.uint8 if M <= 256 else torch.int16
+
     def gather_codes(self, batch_idx: torch.Tensor, local: torch.Tensor,
-                     max_B: int | None = None):
+                     max_B: int | None = None, M: int = 32767, async_op: bool = False):
         """All ranks' (batch_idx, local codes), padded to max_B rows per rank
-        (padding: batch_idx = -1).  -> (idx [world*max_B] int64,
-        codes [world*max_B, nb] int16), on local's device."""
+        (padding: batch_idx = -1).  Wire format: node ids int32, codes uint8
+        when M <= 256 (else int16), both as bytes (RCCL has no 16-bit ints).
+        -> (pending, idx [world*max_B] int32, codes [world*max_B, nb] wire
+        dtype); ``pending`` is a list of async works (empty if not async_op)."""
         B, nb = local.shape
         if max_B is None:
             max_B = self.global_max(B)
         dev = local.device
-        pad_idx = torch.full((max_B,), -1, dtype=torch.int64, device=dev)
+        wd = self._wire_dtype(M)
+        pad_idx = torch.full((max_B,), -1, dtype=torch.int32, device=dev)
         pad_idx[:B] = batch_idx
-        pad_loc = torch.zeros(max_B, nb, dtype=torch.int16, device=dev)
+        pad_loc = torch.zeros(max_B, nb, dtype=wd, device=dev)
         pad_loc[:B] = local
-        all_idx = torch.empty(self.world, max_B, dtype=torch.int64, device=dev)
-        all_loc = torch.empty(self.world, max_B, nb, dtype=torch.int16, device=dev)
-        dist.all_gather(list(all_idx.unbind(0)), pad_idx, group=self.group)
-        dist.all_gather(list(all_loc.view(torch.uint8).unbind(0)),
-                        pad_loc.view(torch.uint8), group=self.group)
-        return all_idx.view(-1), all_loc.view(-1, nb)
+        all_idx = torch.empty(self.world, max_B, dtype=torch.int32, device=dev)
+        all_loc = torch.empty(self.world, max_B, nb, dtype=wd, device=dev)
+        w1 = dist.all_gather(list(all_idx.unbind(0)), pad_idx, group=self.group,
+                             async_op=async_op)
+        w2 = dist.all_gather(list(all_loc.view(torch.uint8).unbind(0)),
+                             pad_loc.view(torch.uint8), group=self.group, async_op=async_op)
+        pending = [w for w in (w1, w2) if w is not None] if async_op else []
+        return pending, all_idx.view(-1), all_loc.view(-1, nb)
 
     def allgather_codes_(self, batch_idx: torch.Tensor, local: torch.Tensor,
-                         codes: torch.Tensor, max_B: int | None = None) -> None:
+                         codes: torch.Tensor, max_B: int | None = None, M: int = 32767) -> None:
         """Scatter every rank's (batch_idx, local codes) into ``codes`` (HIP)."""
-        all_idx, all_loc = self.gather_codes(batch_idx, local, max_B)
-        kernels.scatter_codes(all_idx, all_loc, codes)
+        _, all_idx, all_loc = self.gather_codes(batch_idx, local, max_B, M)
+        kernels.scatter_codes(all_idx.to(torch.int64), all_loc.to(torch.int16), codes)
+
+    def start_codes_exchange(self, batch_idx, local, codes, max_B=None, M=32767):
+        """Asynchronous allgather_codes_: returns a PendingCodes whose wait()
+        scatters the gathered codes (call it before ``codes`` is next read
+        for nodes of other ranks' batches)."""
+        pending, all_idx, all_loc = self.gather_codes(batch_idx, local, max_B, M, async_op=True)
+        return PendingCodes(pending, all_idx, all_loc, codes)
+
 
     def global_max(self, B: int) -> int:
         t = torch.tensor([B], dtype=torch.int64)
@@ -86,6 +103,17 @@ class CodebookSync:
         dist.all_reduce(dev, op=dist.ReduceOp.MAX, group=self.group)
         return int(dev.item())
 
+
+class PendingCodes:
+    def __init__(self, works, all_idx, all_loc, codes):
+        self.works, self.all_idx, self.all_loc, self.codes = works, all_idx, all_loc, codes
+
+    def wait(self):
+        for w in self.works:
+            w.wait()
+        kernels.scatter_codes(self.all_idx.to(torch.int64), self.all_loc.to(torch.int16),
+                              self.codes)
+        self.works = []
 
 def _device_of(group):
     backend = dist.get_backend(group)

@@ -222,6 +222,9 @@ class LowRankGNNLayer(torch.nn.Module):
             x_output = self.conv.fused_forward(x, adj, x_first, B, hook)
         else:
             x_output = self.conv(GatheredInput(x, x_first), adj, _hook=hook)
+        # multi-GPU: the other ranks' new codes were exchanged behind the
+        # gather + aggregation; land them before anything reads c_indices again
+        self._bank.sync_codes()
 
         for _ in branch_idx:
             errors.append(0)

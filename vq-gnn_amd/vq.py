@@ -74,6 +74,9 @@ class VQBank(nn.Module):
         # (bench.py times vq_assign_kernel alone with it); None = off
         self.assign_events = None
         self.comm_max_B = None
+        # multi-GPU: codes of the other ranks' batches arrive asynchronously
+        # (dist.PendingCodes); sync_codes() lands them
+        self._pending_codes = None
         # last batched call's logging stash (vq.py:208-214, :276-277)
         self.last_batch = None       # [4, nb*D] mean_f, std_f, mean_g, std_g
         self.last_inputs = None      # (X, G) of the last update()
@@ -108,6 +111,20 @@ class VQBank(nn.Module):
             VQBank._arange_cache[key] = t
         return t
 
+    def sync_codes(self):
+        """Land the other ranks' codes of the last update (multi-GPU); a no-op
+        on one GPU.  Called before the next VQ call and by the layer after its
+        aggregation, so the exchange overlaps the gather + SpMM."""
+        p, self._pending_codes = self._pending_codes, None
+        if p is not None:
+            p.wait()
+
+    def _exchange_codes(self, batch_idx, local, codes):
+        """Own codes now (local scatter), everyone's asynchronously."""
+        kernels.scatter_codes(batch_idx, local, codes)
+        self._pending_codes = self.comm.start_codes_exchange(batch_idx, local, codes,
+                                                             self.comm_max_B, self.M)
+
     def _slab(self, W, b0, nbr):
         """Zeroed statistic slab [1, nbr, M, W+1] for branches [b0, b0+nbr)."""
         buf = self.stats_f if W == self.D else self.stats_u
@@ -138,6 +155,7 @@ class VQBank(nn.Module):
 
     def feature_update(self, X, b0, nbr, training, idx_out=None, codes=None, batch_idx=None):
         """vq.py:160-202 for branches [b0, b0+nbr): X is [B, nbr*D] (a row-major view)."""
+        self.sync_codes()
         D, F = self.D, nbr * self.D
         sl = self._sel(b0, nbr)
         B = X.shape[0]
@@ -172,7 +190,7 @@ class VQBank(nn.Module):
             stats = kernels.vq_ema_reduce(stats)
             comm.allreduce_(stats)
             if local is not None:
-                comm.allgather_codes_(batch_idx, local, codes, self.comm_max_B)
+                self._exchange_codes(batch_idx, local, codes)
         if training:
             kernels.vq_ema_finalize(stats, D, D, self.decay, self.warm_up_flag, 1.0, self.epsilon,
                                     self.cs[sl], self.ema_w[sl], self.emb[sl], self.emb_out[sl],
@@ -183,6 +201,7 @@ class VQBank(nn.Module):
 
     def update(self, X, G, b0, nbr, training, idx_out=None, codes=None, batch_idx=None):
         """vq.py:204-279 for branches [b0, b0+nbr): X, G are [B, nbr*D] views."""
+        self.sync_codes()
         D, F = self.D, nbr * self.D
         sl = self._sel(b0, nbr)
         B = X.shape[0]
@@ -228,7 +247,7 @@ class VQBank(nn.Module):
             stats = kernels.vq_ema_reduce(stats)
             comm.allreduce_(stats)
             if local is not None:
-                comm.allgather_codes_(batch_idx, local, codes, self.comm_max_B)
+                self._exchange_codes(batch_idx, local, codes)
         if training:
             kernels.vq_ema_finalize(stats, D, 2 * D, self.decay, self.warm_up_flag, scale,
                                     self.epsilon, self.cs[sl], self.ema_w[sl], self.emb[sl],
