@@ -74,12 +74,17 @@ int vqgnn_bn_stats(const float* X, int64_t ldx, const float* G, int64_t ldg,
  *          3 = eval  + init_from_batch (vq.py:216-221, then as 0)
  *    count = rows over all ranks.  coef[4][F]: alpha_f, beta_f, alpha_g, beta_g.
  *    batch_out[4][F] (optional, may be NULL): mean_f, std_f, mean_g, std_g with
- *    std = sqrt(unbiased var + eps_std) (vq.py:208-211 logging stash).         */
+ *    std = sqrt(unbiased var + eps_std) (vq.py:208-211 logging stash).
+ *    nbt_f / nbt_g (optional, [F / nbt_d] int64): BatchNorm1d's
+ *    num_batches_tracked of each branch (nbt_d columns per branch) += 1 —
+ *    pass them in training modes only.                                        */
 int vqgnn_bn_finalize(const double* sums, int64_t count, int32_t F, int32_t with_grad,
                       int32_t mode, float momentum_f, float eps_f,
                       float momentum_g, float eps_g, float eps_std,
                       float* rm_f, float* rv_f, float* rm_g, float* rv_g,
-                      float* coef, float* batch_out, vqgnn_stream_t stream);
+                      float* coef, float* batch_out,
+                      int64_t* nbt_f, int64_t* nbt_g, int32_t nbt_d,
+                      vqgnn_stream_t stream);
 
 /* ------------------------------------------------------------------------ *
  * 3. Product-quantised nearest-codeword assignment for nb branches at once,

@@ -32,7 +32,8 @@ SIGNATURES = {
                                       _c_void_p, _c_void_p, _c_void_p]),
     "vqgnn_bn_finalize": (ctypes.c_int, [_c_void_p, _i64, _i32, _i32, _i32, _f32, _f32, _f32,
                                          _f32, _f32, _c_void_p, _c_void_p, _c_void_p,
-                                         _c_void_p, _c_void_p, _c_void_p, _c_void_p]),
+                                         _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
+                                         _i32, _c_void_p]),
     "vqgnn_vq_stat_shifts": (None, [_i64, _f32, _c_void_p, _c_void_p]),
     "vqgnn_vq_ema_parts": (_i32, [_i32, _i32, _i32, _i32]),
     "vqgnn_vq_assign_workspace": (_size, [_i32, _i32, _i32, _i32]),

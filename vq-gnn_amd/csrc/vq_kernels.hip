@@ -221,9 +221,14 @@ __global__ void bn_finalize_kernel(const double* __restrict__ sums, int64_t n, i
                                    int mode, float mom_f, float eps_f, float mom_g, float eps_g,
                                    float eps_std, float* rm_f, float* rv_f, float* rm_g,
                                    float* rv_g, float* __restrict__ coef,
-                                   float* __restrict__ batch_out) {
+                                   float* __restrict__ batch_out, long long* __restrict__ nbt_f,
+                                   long long* __restrict__ nbt_g, int D) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= F) return;
+  if (D > 0 && c % D == 0) {   // BatchNorm1d.num_batches_tracked += 1 (train)
+    if (nbt_f) nbt_f[c / D] += 1;
+    if (nbt_g && with_grad) nbt_g[c / D] += 1;
+  }
   bn_column(sums[c], sums[F + c], n, mode, mom_f, eps_f, eps_std, rm_f + c, rv_f + c,
             coef + c, coef + F + c, batch_out ? batch_out + c : nullptr,
             batch_out ? batch_out + F + c : nullptr);
@@ -545,15 +550,30 @@ vq_assign_kernel(const float* __restrict__ X, int64_t ldx,
   // independent and those lanes write nothing.
   constexpr int RPW = 16 * NG;                 // rows per wave per iteration
   constexpr int RPI = WV * RPW;                // rows per workgroup iteration
+  // X / G as buffer resources: 32-bit row offsets (the host checks that
+  // B*ld*4 < 2^32), no 64-bit address arithmetic per load
+  constexpr bool kBuf = WM != 0 && KC >= 2;   // k-slot -> X or G is compile-time
+  const __amdgpu_buffer_rsrc_t rsx = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)X, 0, (int)(uint32_t)min((int64_t)B * ldx * 4, (int64_t)0xFFFFFFFF), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsg = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(Gr ? Gr : X), 0,
+      (int)(uint32_t)min((int64_t)B * (Gr ? ldg : ldx) * 4, (int64_t)0xFFFFFFFF), 0x00020000);
   auto load_rows = [&](int it, float (&raw)[NG][KC]) {
     const int row0 = part_begin + it * RPI + wave * RPW;
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
-      const int64_t row = min(row0 + g * 16 + j, part_end - 1);
+      const int rowi = min(row0 + g * 16 + j, part_end - 1);
 #pragma unroll
       for (int kc = 0; kc < KC; ++kc) {
         float v = 0.f;
-        if (kval[kc]) v = isg[kc] ? Gr[row * ldg + colx[kc]] : X[row * ldx + colx[kc]];
+        if constexpr (kBuf) {
+          const bool gk = isg[kc];
+          const uint32_t off = ((uint32_t)rowi * (uint32_t)(gk ? ldg : ldx) + (uint32_t)colx[kc]) * 4u;
+          v = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(gk ? rsg : rsx, off, 0, 0));
+        } else {
+          const int64_t row = rowi;
+          if (kval[kc]) v = isg[kc] ? Gr[row * ldg + colx[kc]] : X[row * ldx + colx[kc]];
+        }
         raw[g][kc] = v;
       }
     }
@@ -694,14 +714,13 @@ vq_assign_kernel(const float* __restrict__ X, int64_t ldx,
 #pragma unroll
           for (int k = 0; k < K4; ++k) e[k] = (WM != 0 || k < W) ? er[k] : 0.f;
         }
-        float se_c = 0.f, dot = 0.f;
+        float dot = 0.f;
 #pragma unroll
         for (int k = 0; k < K4; ++k) {
-          if (WM != 0 || k < W) {
-            se_c = (k == 0) ? __fmul_rn(e[k], e[k]) : __fadd_rn(se_c, __fmul_rn(e[k], e[k]));
-            dot = (k == 0) ? __fmul_rn(e[k], xr[k]) : fmaf(e[k], xr[k], dot);
-          }
+          if (WM != 0 || k < W) dot = (k == 0) ? __fmul_rn(e[k], xr[k]) : fmaf(e[k], xr[k], dot);
         }
+        // |e|^2 as staged (same operations; +inf past the codebook end)
+        const float se_c = se[min(key + q, chunk - 1)];
         const float dist = fmaf(-2.f, dot, __fadd_rn(sx[g], cv ? se_c : INFINITY));
         int r = (dist == rmin) ? q : 4;
         r = min(r, __shfl_xor(r, 16));
@@ -953,6 +972,7 @@ extern "C" int vqgnn_bn_finalize(const double* sums, int64_t count, int32_t F, i
                                  int32_t mode, float momentum_f, float eps_f, float momentum_g,
                                  float eps_g, float eps_std, float* rm_f, float* rv_f,
                                  float* rm_g, float* rv_g, float* coef, float* batch_out,
+                                 int64_t* nbt_f, int64_t* nbt_g, int32_t nbt_d,
                                  vqgnn_stream_t stream) {
   clear_error();
   VQGNN_REQUIRE(F > 0 && coef && rm_f && rv_f, "bn_finalize: bad arguments");
@@ -961,7 +981,9 @@ extern "C" int vqgnn_bn_finalize(const double* sums, int64_t count, int32_t F, i
   VQGNN_REQUIRE(!with_grad || (rm_g && rv_g), "bn_finalize: grad running stats required");
   hipLaunchKernelGGL(bn_finalize_kernel, dim3((F + 255) / 256), dim3(256), 0, as_stream(stream),
                      sums, count, F, with_grad, mode, momentum_f, eps_f, momentum_g, eps_g,
-                     eps_std, rm_f, rv_f, rm_g, rv_g, coef, batch_out);
+                     eps_std, rm_f, rv_f, rm_g, rv_g, coef, batch_out,
+                     reinterpret_cast<long long*>(nbt_f), reinterpret_cast<long long*>(nbt_g),
+                     nbt_d);
   return check_launch("bn_finalize");
 }
 
@@ -1055,6 +1077,9 @@ extern "C" int vqgnn_vq_assign(const float* X, int64_t ldx, const float* G, int6
   VQGNN_REQUIRE(!ema_parts || workspace, "vq_assign: workspace required for EMA statistics");
   VQGNN_REQUIRE(M <= 32767 || !codes, "vq_assign: int16 codes need M <= 32767");
   VQGNN_REQUIRE(!ema_parts || stat_count >= B, "vq_assign: stat_count < B");
+  VQGNN_REQUIRE((int64_t)B * ldx * 4 < ((int64_t)1 << 32) &&
+                    (!G || (int64_t)B * ldg * 4 < ((int64_t)1 << 32)),
+                "vq_assign: B*ldx (and B*ldg) must span < 4 GiB");
   hipStream_t s = as_stream(stream);
   unsigned long long* parts = reinterpret_cast<unsigned long long*>(ema_parts);
   const int kc = W <= 4 ? 1 : (W <= 8 ? 2 : 4);

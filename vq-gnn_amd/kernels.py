@@ -38,8 +38,10 @@ def bn_stats(X: torch.Tensor, G: torch.Tensor | None, F: int) -> torch.Tensor:
 
 
 def bn_finalize(sums, count, F, with_grad, mode, mom_f, eps_f, mom_g, eps_g, eps_std,
-                rm_f, rv_f, rm_g=None, rv_g=None, want_batch=False):
-    """-> (coef [4, F], batch_out [4, F] or None); updates running stats in place."""
+                rm_f, rv_f, rm_g=None, rv_g=None, want_batch=False, nbt_f=None, nbt_g=None,
+                D=0):
+    """-> (coef [4, F], batch_out [4, F] or None); updates running stats in place
+    and, when given, num_batches_tracked (nbt_f / nbt_g [F // D] int64) += 1."""
     dev = rm_f.device
     coef = torch.empty(4, F, dtype=torch.float32, device=dev)
     if not with_grad:
@@ -48,7 +50,8 @@ def bn_finalize(sums, count, F, with_grad, mode, mom_f, eps_f, mom_g, eps_g, eps
     check(lib().vqgnn_bn_finalize(ptr(sums), int(count), F, int(with_grad), int(mode),
                                   float(mom_f), float(eps_f), float(mom_g), float(eps_g),
                                   float(eps_std), ptr(rm_f), ptr(rv_f), ptr(rm_g), ptr(rv_g),
-                                  ptr(coef), ptr(batch), stream_ptr()), "bn_finalize")
+                                  ptr(coef), ptr(batch), ptr(nbt_f), ptr(nbt_g), int(D),
+                                  stream_ptr()), "bn_finalize")
     return coef, batch
 
 

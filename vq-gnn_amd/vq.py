@@ -169,8 +169,8 @@ class VQBank(nn.Module):
                 comm.allreduce_(sums)
                 count = comm.global_count(B)
             coef, _ = kernels.bn_finalize(sums, count, F, False, BN_TRAIN, 0.1, 1e-5, 0.0, 0.0,
-                                          0.0, self.rm_f[sl], self.rv_f[sl])
-            self.nbt_f[sl] += 1
+                                          0.0, self.rm_f[sl], self.rv_f[sl], nbt_f=self.nbt_f[sl],
+                                          D=D)
         else:
             count = B
             coef, _ = kernels.bn_finalize(None, B, F, False, BN_EVAL, 0.1, 1e-5, 0.0, 0.0, 0.0,
@@ -222,12 +222,11 @@ class VQBank(nn.Module):
         coef, batch = kernels.bn_finalize(sums, count, F, True, mode, 0.1, 1e-5, self.momentum,
                                           self.epsilon, self.epsilon, self.rm_f[sl],
                                           self.rv_f[sl], self.rm_g[sl], self.rv_g[sl],
-                                          want_batch=True)
+                                          want_batch=True,
+                                          nbt_f=self.nbt_f[sl] if training else None,
+                                          nbt_g=self.nbt_g[sl] if training else None, D=D)
         for b in range(b0, b0 + nbr):
             self.bn_inited[b] = True
-        if training:
-            self.nbt_f[sl] += 1
-            self.nbt_g[sl] += 1
         self.last_batch = batch
         self.last_inputs = (X, G)
         scale = float(self.grad_normalize_scale[0])
