@@ -190,7 +190,15 @@ size_t vqgnn_spmm_workspace(int32_t n_rows, int64_t nnz, int32_t F);
 int vqgnn_spmm(const int32_t* rowptr, const int32_t* col, const float* val,
                int32_t n_rows, int32_t n_cols, int64_t nnz, int32_t B,
                const float* X, int64_t ldx, const float* X2, int64_t ldx2,
-               int32_t F, float* out, int64_t ldo, void* workspace, vqgnn_stream_t stream);
+               int32_t F, float* out, int64_t ldo, const int32_t* plan,
+               void* workspace, vqgnn_stream_t stream);
+/* 6b. Optional SpMM plan of a CSR (computed once per batch adjacency and F,
+ *     like the transpose): the first row of every edge chunk, so the kernel's
+ *     waves skip the row search.  plan: vqgnn_spmm_plan_size(nnz, F) int32;
+ *     pass it to vqgnn_spmm (NULL = search in-kernel).                       */
+int64_t vqgnn_spmm_plan_size(int64_t nnz, int32_t F);
+int vqgnn_spmm_plan(const int32_t* rowptr, int32_t n_rows, int64_t nnz, int32_t F,
+                    int32_t* plan, vqgnn_stream_t stream);
 
 /* 7. CSR transpose (structure + values) for the backward product
  *    dX = A^T dOut (torch_sparse matmul autograd, convs.py:95).  Output CSR of

@@ -13,7 +13,7 @@ while read -r line; do
     -- python scripts/pmc_target.py $TARGET > $OUT/p$i.log 2>&1
   rc=$?; echo "pass $i ($line) rc=$rc"
   if [ $rc -ne 0 ]; then tail -5 $OUT/p$i.log; exit $rc; fi
-done <<'LIST'
+done <<< "${PMC_LIST:-$(cat <<'LIST'
 SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU
 SQ_INSTS_MFMA SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_VALU_MFMA_COEXEC_CYCLES SQ_LDS_IDX_ACTIVE
 TCC_HIT TCC_MISS GRBM_GUI_ACTIVE
@@ -21,3 +21,4 @@ FETCH_SIZE
 WRITE_SIZE
 TCC_EA0_RDREQ TCC_EA0_RDREQ_DRAM TCC_EA0_WRREQ
 LIST
+)}"

@@ -72,14 +72,25 @@ def bench_spmm():
     by = 4 * (b.n + 1) + 8 * b.nnz + 8 * b.n * F
     deg = np.diff(b.rowptr)
     print(f"batch B={b.B} n={b.n} nnz={b.nnz} maxdeg={deg.max()} rows>128: {(deg > 128).sum()}")
+    pl = adj.plan(F) if os.environ.get("MB_PLAN", "1") == "1" else None
     t = timeit(lambda: kernels.spmm(adj.rowptr, adj.col, adj.value, b.n, b.nnz, X, F, X2=xt,
-                                    B=b.B))
+                                    B=b.B, plan=pl))
     print(f"spmm two-source     {t:8.1f} us  {by / t / 1e3:7.1f} GB/s alg  "
           f"{b.nnz * 512 / t / 1e6:6.2f} TB/s gathered")
-    t = timeit(lambda: kernels.spmm(adj.rowptr, adj.col, adj.value, b.n, b.nnz, Xn, F))
+    t = timeit(lambda: kernels.spmm(adj.rowptr, adj.col, adj.value, b.n, b.nnz, Xn, F, plan=pl))
     print(f"spmm dense n rows   {t:8.1f} us  {b.nnz * 512 / t / 1e6:6.2f} TB/s gathered")
     t = timeit(lambda: kernels.gather_codewords(subset, b.B, codes, emb_out, D))
     print(f"gather_codewords    {t:8.1f} us  {(b.n - b.B) * F * 4 / t / 1e3:7.1f} GB/s written")
+    # bound probes: same CSR shape, columns rewritten
+    rows = torch.repeat_interleave(torch.arange(b.n, device=dev),
+                                   torch.from_numpy(deg).to(dev))
+    for name, colv in (("hot set (1024 rows)", (torch.arange(b.nnz, device=dev) % 1024)),
+                       ("col = row (stream)", rows),
+                       ("col = row+k (local)", (rows + torch.arange(b.nnz, device=dev) % 16)
+                        .clamp(max=b.n - 1))):
+        c32 = colv.to(torch.int32).contiguous()
+        t = timeit(lambda: kernels.spmm(adj.rowptr, c32, adj.value, b.n, b.nnz, Xn, F, plan=pl))
+        print(f"probe {name:22s} {t:8.1f} us  {b.nnz * 512 / t / 1e6:6.2f} TB/s gathered")
 
 
 if __name__ == "__main__":

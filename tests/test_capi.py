@@ -54,7 +54,7 @@ def test_invalid_arguments_rejected_without_device():
     assert rc == 1
     assert b"null" in h.vqgnn_last_error() or b"W" in h.vqgnn_last_error()
     # dummy non-null addresses: validation rejects F before any pointer is used
-    rc = h.vqgnn_spmm(16, None, None, 4, 4, 0, 0, None, 4, None, 0, 6, 16, 4, None, None)
+    rc = h.vqgnn_spmm(16, None, None, 4, 4, 0, 0, None, 4, None, 0, 6, 16, 4, None, None, None)
     assert rc == 1 and b"multiple of 4" in h.vqgnn_last_error()
-    rc = h.vqgnn_spmm(None, None, None, 4, 4, 0, 0, None, 4, None, 0, 8, None, 8, None, None)
+    rc = h.vqgnn_spmm(None, None, None, 4, 4, 0, 0, None, 4, None, 0, 8, None, 8, None, None, None)
     assert rc == 1 and b"null" in h.vqgnn_last_error()

@@ -58,7 +58,8 @@ class GatherSpMMFunction(torch.autograd.Function):
         n = adj.size(0)
         xc = x if (x.stride(1) == 1 and x.stride(0) % 4 == 0 and
                    x.data_ptr() % 16 == 0) else x.contiguous()
-        out = kernels.spmm(adj.rowptr, adj.col, adj.value, n, adj.nnz(), xc, F, X2=x_first, B=B)
+        out = kernels.spmm(adj.rowptr, adj.col, adj.value, n, adj.nnz(), xc, F, X2=x_first, B=B,
+                           plan=adj.plan(F))
         ctx.adj, ctx.B, ctx.hook = adj, B, hook
         return out
 
@@ -74,7 +75,7 @@ class GatherSpMMFunction(torch.autograd.Function):
             F = dout.shape[1]
             # rows [0, B) of A^T = columns [0, B) of A; the merge kernel bounds
             # the walk with the full nnz, so no host read of t_rowptr[B] is needed
-            dx = kernels.spmm(at.rowptr, at.col, at.value, B, at.nnz(), dout, F)
+            dx = kernels.spmm(at.rowptr, at.col, at.value, B, at.nnz(), dout, F, plan=at.plan(F))
         return dx, None, None, None, None
 
 
@@ -88,7 +89,8 @@ class SpMMFunction(torch.autograd.Function):
         xc = x.contiguous()
         if pad:
             xc = torch.nn.functional.pad(xc, (0, pad))
-        out = kernels.spmm(adj.rowptr, adj.col, adj.value, adj.size(0), adj.nnz(), xc, F + pad)
+        out = kernels.spmm(adj.rowptr, adj.col, adj.value, adj.size(0), adj.nnz(), xc, F + pad,
+                           plan=adj.plan(F + pad))
         ctx.adj, ctx.pad, ctx.F = adj, pad, F
         return out[:, :F] if pad else out
 
@@ -98,7 +100,8 @@ class SpMMFunction(torch.autograd.Function):
         d = dout.contiguous()
         if ctx.pad:
             d = torch.nn.functional.pad(d, (0, ctx.pad))
-        dx = kernels.spmm(at.rowptr, at.col, at.value, at.size(0), at.nnz(), d, ctx.F + ctx.pad)
+        dx = kernels.spmm(at.rowptr, at.col, at.value, at.size(0), at.nnz(), d, ctx.F + ctx.pad,
+                          plan=at.plan(ctx.F + ctx.pad))
         return (dx[:, :ctx.F] if ctx.pad else dx), None
 
 

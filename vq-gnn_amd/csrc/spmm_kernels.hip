@@ -65,6 +65,9 @@ struct SpmmArgs {
   uint32_t offx, ldxb;    // X row j at offx + j*ldxb
   uint32_t offx2, ldx2b;  // X2 row j-B at offx2 + (j-B)*ldx2b
   int kpw;                // wave kernel: consecutive chunks per wave
+  const int* chunk_row;   // [nchunks] first row starting at or after chunk*S (or null)
+  int dbg;                // experiments: 1 = no gathers, 2 = no output stores, 4 = stamps
+  unsigned long long* stamps;  // dbg & 4: [waves][8] s_memtime stamps
 };
 
 template <int NCH>
@@ -229,6 +232,12 @@ spmm_merge_kernel(SpmmArgs a) {
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
 
+__device__ __forceinline__ unsigned long long stamp() {
+  unsigned long long t;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
+  return t;
+}
+
 
 template <int V>
 __device__ __forceinline__ void buf_load(__amdgpu_buffer_rsrc_t rs, uint32_t vo, uint32_t so,
@@ -294,6 +303,21 @@ __device__ __forceinline__ void window_stage(const SpmmArgs& a, EdgeWindow<FAR>&
   }
 }
 
+// lane l holds rowptr[base + l]: row bounds by v_readlane, no scalar-load
+// round trip at every row boundary (rows average ~16 edges)
+struct RowWindow {
+  int base;
+  int rp;
+};
+
+__device__ __forceinline__ int row_at(const SpmmArgs& a, RowWindow& rw, int idx, int lane) {
+  if (idx < rw.base || idx >= rw.base + 64) {
+    rw.base = idx;
+    rw.rp = a.rowptr[min(idx + lane, a.n_rows)];
+  }
+  return __builtin_amdgcn_readlane(rw.rp, uni(idx - rw.base));
+}
+
 // row k of the window, this lane's V columns
 template <int V, bool FAR>
 __device__ __forceinline__ void window_load(__amdgpu_buffer_rsrc_t rs, const EdgeWindow<FAR>& win,
@@ -351,45 +375,221 @@ __device__ __forceinline__ void wave_segment(const SpmmArgs& a, __amdgpu_buffer_
   }
 }
 
+// ---------------------------------------------------------------------------
+// Paired variant for F = 128: the row's edges are taken two at a time, one
+// dwordx4 wave-instruction loading edge e into lanes 0-31 and edge e+1 into
+// lanes 32-63 (the texture addresser costs the same per wave-instruction, so
+// this halves its work per edge: probe scripts/probes/gather_shape.hip, 1.75x
+// the rows/s of one 512-B row per instruction).  Each half multiplies by its
+// own weight; v_permlane32_swap moves the upper half's product to lanes 0-31,
+// which add p_e then p_e+1 — the sequential CSR order of spmm_sum, bit-exact.
+// acc (4 floats) is meaningful in lanes 0-31 only.
+// ---------------------------------------------------------------------------
+struct U32x2 {
+  unsigned a, b;
+};
+
+__device__ __forceinline__ float upper_to_lower(float p) {
+  // lanes 0-31 <- lanes 32-63 of p (second result of the swap; element
+  // access by struct bit_cast: vector subscripts miscompile here)
+  const U32x2 r = __builtin_bit_cast(
+      U32x2, __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, p),
+                                              __builtin_bit_cast(unsigned, p), false, false));
+  return __builtin_bit_cast(float, r.b);
+}
+
+template <bool FAR>
+__device__ __forceinline__ void pair_load(__amdgpu_buffer_rsrc_t rs, const EdgeWindow<FAR>& win,
+                                          int ka, int kb, bool upper, uint32_t lo16,
+                                          float (&v)[4]) {
+  if constexpr (FAR) {
+    const uint32_t la = __builtin_amdgcn_readlane(win.off, ka);
+    const uint32_t ha = __builtin_amdgcn_readlane(win.hi, ka);
+    const uint32_t lb = __builtin_amdgcn_readlane(win.off, kb);
+    const uint32_t hb = __builtin_amdgcn_readlane(win.hi, kb);
+    const uint64_t p = upper ? (((uint64_t)hb << 32) | lb) : (((uint64_t)ha << 32) | la);
+    const float4 t = *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(p) + lo16);
+    v[0] = t.x;
+    v[1] = t.y;
+    v[2] = t.z;
+    v[3] = t.w;
+  } else {
+    const uint32_t sa = __builtin_amdgcn_readlane(win.off, ka);
+    const uint32_t sb = __builtin_amdgcn_readlane(win.off, kb);
+    const float4 t = __builtin_bit_cast(
+        float4, __builtin_amdgcn_raw_buffer_load_b128(rs, (upper ? sb : sa) + lo16, 0, 0));
+    v[0] = t.x;
+    v[1] = t.y;
+    v[2] = t.z;
+    v[3] = t.w;
+  }
+}
+
+template <bool FAR>
+__device__ __forceinline__ void single_load(__amdgpu_buffer_rsrc_t rs, const EdgeWindow<FAR>& win,
+                                            int k, uint32_t lo16, float (&v)[4]) {
+  if constexpr (FAR) {
+    const uint32_t l = __builtin_amdgcn_readlane(win.off, k);
+    const uint32_t h = __builtin_amdgcn_readlane(win.hi, k);
+    const float4 t = *reinterpret_cast<const float4*>(
+        reinterpret_cast<const char*>((((uint64_t)h << 32) | l)) + lo16);
+    v[0] = t.x;
+    v[1] = t.y;
+    v[2] = t.z;
+    v[3] = t.w;
+  } else {
+    const float4 t = __builtin_bit_cast(
+        float4, __builtin_amdgcn_raw_buffer_load_b128(rs, lo16, __builtin_amdgcn_readlane(win.off, k),
+                                                      0));
+    v[0] = t.x;
+    v[1] = t.y;
+    v[2] = t.z;
+    v[3] = t.w;
+  }
+}
+
+template <int UP, bool FAR>
+__device__ __forceinline__ void wave_segment_pair(const SpmmArgs& a, __amdgpu_buffer_rsrc_t rs,
+                                                  EdgeWindow<FAR>& win, int eb, int ee, int lane,
+                                                  float (&acc)[4]) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) acc[k] = 0.f;
+  const bool upper = lane >= 32;
+  const uint32_t lo16 = (uint32_t)(lane & 31) * 16;
+  const int up4 = upper ? 4 : 0;
+  int e = eb;
+  while (e < ee) {
+    if (e < win.wb || e >= win.wb + 64) window_stage(a, win, e, lane);
+    const int lim = min(ee, win.wb + 64);
+    for (; e + 2 * UP <= lim; e += 2 * UP) {
+      const int k0 = uni(e - win.wb);
+      // lane reads window lane k0 + 2u + upper: one address per group, the
+      // pair index in ds_bpermute's immediate offset
+      const int addr = k0 * 4 + up4;
+      float v[UP][4];
+      float ww[UP];
+#pragma unroll
+      for (int u = 0; u < UP; ++u) {
+        int off, wbits;
+        if constexpr (FAR) {
+          const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(addr + 8 * u, (int)win.off);
+          const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(addr + 8 * u, (int)win.hi);
+          const float4 t = *reinterpret_cast<const float4*>(
+              reinterpret_cast<const char*>((((uint64_t)hi << 32) | lo)) + lo16);
+          v[u][0] = t.x;
+          v[u][1] = t.y;
+          v[u][2] = t.z;
+          v[u][3] = t.w;
+          off = 0;
+        } else {
+          off = __builtin_amdgcn_ds_bpermute(addr + 8 * u, (int)win.off);
+          const float4 t = (a.dbg & 1) ? make_float4(1.f, 1.f, 1.f, (float)off) : __builtin_bit_cast(
+              float4, __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)off + lo16, 0, 0));
+          v[u][0] = t.x;
+          v[u][1] = t.y;
+          v[u][2] = t.z;
+          v[u][3] = t.w;
+        }
+        wbits = __builtin_amdgcn_ds_bpermute(addr + 8 * u, __builtin_bit_cast(int, win.w));
+        ww[u] = __builtin_bit_cast(float, wbits);
+      }
+#pragma unroll
+      for (int u = 0; u < UP; ++u) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float p = __fmul_rn(ww[u], v[u][k]);
+          acc[k] = __fadd_rn(__fadd_rn(acc[k], p), upper_to_lower(p));
+        }
+      }
+    }
+    for (; e + 2 <= lim; e += 2) {
+      const int ka = uni(e - win.wb), kb = ka + 1;
+      const float wa = __builtin_bit_cast(
+          float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, win.w), ka));
+      const float wb = __builtin_bit_cast(
+          float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, win.w), kb));
+      float v[4];
+      pair_load<FAR>(rs, win, ka, kb, upper, lo16, v);
+      const float w = upper ? wb : wa;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float p = __fmul_rn(w, v[k]);
+        acc[k] = __fadd_rn(__fadd_rn(acc[k], p), upper_to_lower(p));
+      }
+    }
+    if (e < lim) {   // odd last edge of the row (or window): lanes 0-31 only
+      const int k = uni(e - win.wb);
+      const float w = __builtin_bit_cast(
+          float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, win.w), k));
+      if (!upper) {
+        float v[4];
+        single_load<FAR>(rs, win, k, lo16, v);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[c] = __fadd_rn(acc[c], __fmul_rn(w, v[c]));
+      }
+      ++e;
+    }
+  }
+}
+
+// chunk_row[c] = first row whose start is >= c*S: one thread per chunk, the
+// searches in parallel instead of as a dependent chain at every wave's head
+__global__ void spmm_chunk_rows_kernel(const int32_t* __restrict__ rowptr, int n_rows, int S,
+                                       int nchunks, int* __restrict__ chunk_row) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < nchunks) chunk_row[c] = lower_bound_i32(rowptr, n_rows, c * S);
+}
+
 // One chunk (rows owned by chunk, carries) starting at row i; returns the
-// first row of the next chunk.
-template <int V, int U, bool FAR>
+// first row of the next chunk.  PAIR: F = 128 in the paired form (acc = 4
+// floats in lanes 0-31; V must be 4).
+template <int V, int U, bool FAR, bool PAIR>
+__device__ __forceinline__ void segment(const SpmmArgs& a, __amdgpu_buffer_rsrc_t rs,
+                                        EdgeWindow<FAR>& win, int eb, int ee, int lane,
+                                        float (&acc)[V]) {
+  if constexpr (PAIR) wave_segment_pair<U / 2, FAR>(a, rs, win, eb, ee, lane, acc);
+  else wave_segment<V, U, FAR>(a, rs, win, eb, ee, lane, acc);
+}
+
+template <int V, int U, bool FAR, bool PAIR>
 __device__ __forceinline__ int wave_chunk(const SpmmArgs& a, __amdgpu_buffer_rsrc_t rs,
-                                          EdgeWindow<FAR>& win, int chunk, int i, int lane) {
+                                          EdgeWindow<FAR>& win, RowWindow& rw, int chunk, int i,
+                                          int lane) {
   const int e0 = chunk * a.S;
   const int e1 = min(e0 + a.S, a.nnz);
   const bool last = e1 == a.nnz;
   const int F = a.F4 * 4;
   const int ldo = (int)(a.ldo4 * 4);
+  const bool st = (!PAIR || lane < 32) && !(a.dbg & 2);    // lanes that own output columns
   int crow = -1;
   float acc[V];
   if (i > 0) {
-    const int ri = uni(a.rowptr[i]);
+    const int ri = row_at(a, rw, i, lane);
     if (ri > e0) {  // row i-1 started before this chunk
-      const int rs0 = uni(a.rowptr[i - 1]);
+      const int rs0 = row_at(a, rw, i - 1, lane);
       if (ri - rs0 > a.L) {
         const int re = min(ri, e1);
-        wave_segment<V, U, FAR>(a, rs, win, e0, re, lane, acc);
-        vstore<V>(a.carry + (int64_t)chunk * 2 * F + lane * V, acc);
+        segment<V, U, FAR, PAIR>(a, rs, win, e0, re, lane, acc);
+        if (st) vstore<V>(a.carry + (int64_t)chunk * 2 * F + lane * V, acc);
         crow = i - 1;
       }
     }
   }
   int next = -1;
-  int rb = (i < a.n_rows) ? uni(a.rowptr[i]) : 0;
+  int rb = (i < a.n_rows) ? row_at(a, rw, i, lane) : 0;
   for (; i < a.n_rows; ++i) {
     if (!(rb < e1 || last)) break;
-    const int re_full = uni(a.rowptr[i + 1]);
+    const int re_full = row_at(a, rw, i + 1, lane);
     if (re_full - rb <= a.L) {
-      wave_segment<V, U, FAR>(a, rs, win, rb, re_full, lane, acc);
-      vstore<V>(a.out + (int64_t)i * ldo + lane * V, acc);
+      segment<V, U, FAR, PAIR>(a, rs, win, rb, re_full, lane, acc);
+      if (st) vstore<V>(a.out + (int64_t)i * ldo + lane * V, acc);
     } else {
       const int re = min(re_full, e1);
-      wave_segment<V, U, FAR>(a, rs, win, rb, re, lane, acc);
+      segment<V, U, FAR, PAIR>(a, rs, win, rb, re, lane, acc);
       if (re_full <= e1) {
-        vstore<V>(a.out + (int64_t)i * ldo + lane * V, acc);
+        if (st) vstore<V>(a.out + (int64_t)i * ldo + lane * V, acc);
       } else {
-        vstore<V>(a.carry + ((int64_t)chunk * 2 + 1) * F + lane * V, acc);
+        if (st) vstore<V>(a.carry + ((int64_t)chunk * 2 + 1) * F + lane * V, acc);
         next = i + 1;   // the row continues into the next chunk
         break;
       }
@@ -402,11 +602,13 @@ __device__ __forceinline__ int wave_chunk(const SpmmArgs& a, __amdgpu_buffer_rsr
 
 // Each wave walks K consecutive chunks (its edge window and row cursor carry
 // over; only the first chunk needs the row search).
-template <int V, int U, bool FAR>
+template <int V, int U, bool FAR, bool PAIR>
 __global__ void __launch_bounds__(kSpmmThreads)
 spmm_wave_kernel(SpmmArgs a) {
   const int lane = threadIdx.x & 63;
   const int wave = uni(threadIdx.x >> 6);
+  const bool stp = (a.dbg & 4) != 0;
+  unsigned long long t0 = stp ? stamp() : 0ull;
   const int K = a.kpw;
   const int nsuper = (a.nchunks + K - 1) / K;
   int split = nsuper;
@@ -417,9 +619,26 @@ spmm_wave_kernel(SpmmArgs a) {
       __builtin_amdgcn_make_buffer_rsrc((void*)a.ubase, 0, a.span, 0x00020000);
   EdgeWindow<FAR> win;
   win.wb = INT32_MIN / 2;
+  RowWindow rw;
+  rw.base = INT32_MIN / 2;
   const int c0 = sc * K, c1 = min(a.nchunks, c0 + K);
-  int i = uni(lower_bound_i32(a.rowptr, a.n_rows, c0 * a.S));
-  for (int c = c0; c < c1; ++c) i = uni(wave_chunk<V, U, FAR>(a, rs, win, c, i, lane));
+  // a plan built over more rows than n_rows (the backward's row-restricted
+  // transpose) clamps to the restricted search's answer (rowptr is monotone)
+  int i = uni(a.chunk_row ? min(a.chunk_row[c0], a.n_rows)
+                          : lower_bound_i32(a.rowptr, a.n_rows, c0 * a.S));
+  unsigned long long t1 = stp ? stamp() : 0ull;
+  for (int c = c0; c < c1; ++c)
+    i = uni(wave_chunk<V, U, FAR, PAIR>(a, rs, win, rw, c, i, lane));
+  if (stp) {
+    const unsigned long long t2 = stamp();
+    if (lane == 0) {
+      unsigned long long* o = a.stamps + (int64_t)sc * 4;
+      o[0] = t0;
+      o[1] = t1;
+      o[2] = t2;
+      o[3] = (unsigned long long)(c1 - c0);
+    }
+  }
 }
 
 // For every row that spans chunks, the chunk where it ends adds the partials:
@@ -544,6 +763,10 @@ __global__ void transpose_finish_kernel(const int32_t* __restrict__ sorted_cols,
   }
 }
 
+static unsigned long long* g_stamps = nullptr;   // debug only (VQGNN_SPMM_DEBUG & 4)
+static size_t g_stamp_cap = 0;
+static int64_t g_stamp_n = 0;
+
 static int env_int(const char* name, int dflt) {
   const char* v = getenv(name);
   return v && *v ? atoi(v) : dflt;
@@ -568,7 +791,7 @@ extern "C" size_t vqgnn_spmm_workspace(int32_t n_rows, int64_t nnz, int32_t F) {
   const int S = spmm_chunk_edges((F + 3) / 4);
   const int64_t nchunks = (nnz + S - 1) / S;
   return align_up((size_t)nchunks * 2 * F * sizeof(float), 256) +
-         align_up((size_t)nchunks * sizeof(int), 256);
+         2 * align_up((size_t)nchunks * sizeof(int), 256);
 }
 
 template <int G, int NCH, bool TWO>
@@ -581,15 +804,22 @@ static void launch_spmm(const SpmmArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(spmm_fixup_kernel, dim3((a.nchunks + 255) / 256), dim3(256), 0, s, a);
 }
 
-template <int V, int U, bool FAR>
+template <int V, int U, bool FAR, bool PAIR = false>
 static void launch_spmm_wave(SpmmArgs& a, hipStream_t s) {
   constexpr int WPB = kSpmmThreads / 64;
   static const int kpw = env_int("VQGNN_SPMM_K", 1);
   a.kpw = kpw < 1 ? 1 : kpw;
   const int nsuper = (a.nchunks + a.kpw - 1) / a.kpw;
+  static const int plan = env_int("VQGNN_SPMM_PLAN", 1);
+  if (!a.chunk_row && plan) {
+    int* cr = a.carry_row + align_up((size_t)a.nchunks * sizeof(int), 256) / sizeof(int);
+    hipLaunchKernelGGL(spmm_chunk_rows_kernel, dim3((a.nchunks + 255) / 256), dim3(256), 0, s,
+                       a.rowptr, a.n_rows, a.S, a.nchunks, cr);
+    a.chunk_row = cr;
+  }
   const int per_xcd = (nsuper + kNumXcd - 1) / kNumXcd + 1;
   const int grid = kNumXcd * ((per_xcd + WPB - 1) / WPB);
-  hipLaunchKernelGGL((spmm_wave_kernel<V, U, FAR>), dim3(grid), dim3(kSpmmThreads), 0, s, a);
+  hipLaunchKernelGGL((spmm_wave_kernel<V, U, FAR, PAIR>), dim3(grid), dim3(kSpmmThreads), 0, s, a);
   hipLaunchKernelGGL(spmm_fixup_kernel, dim3((a.nchunks + 255) / 256), dim3(256), 0, s, a);
 }
 
@@ -635,7 +865,15 @@ static int dispatch_spmm(SpmmArgs& a, int64_t rows_x, int64_t rows_x2, hipStream
       a.ubase = nullptr;
       a.span = 0;
     }
-    if (F == 128) {
+    static const int pair = env_int("VQGNN_SPMM_PAIR", 0);
+    static const int pu = env_int("VQGNN_SPMM_U", 8);
+    if (F == 128 && pair && pu == 16) {
+      if (near) launch_spmm_wave<4, 16, false, true>(a, s);
+      else launch_spmm_wave<4, 16, true, true>(a, s);
+    } else if (F == 128 && pair) {
+      if (near) launch_spmm_wave<4, 8, false, true>(a, s);
+      else launch_spmm_wave<4, 8, true, true>(a, s);
+    } else if (F == 128) {
       if (near) launch_spmm_wave<2, 8, false>(a, s); else launch_spmm_wave<2, 8, true>(a, s);
     } else if (F == 256) {
       if (near) launch_spmm_wave<4, 4, false>(a, s); else launch_spmm_wave<4, 4, true>(a, s);
@@ -659,11 +897,31 @@ static int dispatch_spmm(SpmmArgs& a, int64_t rows_x, int64_t rows_x2, hipStream
   return check_launch("spmm");
 }
 
+extern "C" int64_t vqgnn_spmm_plan_size(int64_t nnz, int32_t F) {
+  if (nnz <= 0 || F <= 0) return 0;
+  const int S = spmm_chunk_edges((F + 3) / 4);
+  return (nnz + S - 1) / S;
+}
+
+extern "C" int vqgnn_spmm_plan(const int32_t* rowptr, int32_t n_rows, int64_t nnz, int32_t F,
+                               int32_t* plan, vqgnn_stream_t stream) {
+  clear_error();
+  VQGNN_REQUIRE(n_rows >= 0 && nnz >= 0 && nnz < (int64_t)INT32_MAX && F > 0,
+                "spmm_plan: bad shape");
+  const int64_t nchunks = vqgnn_spmm_plan_size(nnz, F);
+  if (nchunks == 0) return VQGNN_OK;
+  VQGNN_REQUIRE(rowptr && plan, "spmm_plan: null pointer");
+  const int S = spmm_chunk_edges((F + 3) / 4);
+  hipLaunchKernelGGL(spmm_chunk_rows_kernel, dim3((nchunks + 255) / 256), dim3(256), 0,
+                     as_stream(stream), rowptr, n_rows, S, (int)nchunks, plan);
+  return check_launch("spmm_plan");
+}
+
 extern "C" int vqgnn_spmm(const int32_t* rowptr, const int32_t* col, const float* val,
                           int32_t n_rows, int32_t n_cols, int64_t nnz, int32_t B,
                           const float* X, int64_t ldx,
                           const float* X2, int64_t ldx2, int32_t F, float* out, int64_t ldo,
-                          void* workspace, vqgnn_stream_t stream) {
+                          const int32_t* plan, void* workspace, vqgnn_stream_t stream) {
   clear_error();
   VQGNN_REQUIRE(rowptr && out && n_rows >= 0, "spmm: null pointer");
   VQGNN_REQUIRE(F > 0 && F % 4 == 0, "spmm: F=%d must be a positive multiple of 4", F);
@@ -705,6 +963,20 @@ extern "C" int vqgnn_spmm(const int32_t* rowptr, const int32_t* col, const float
   a.carry = reinterpret_cast<float*>(workspace);
   a.carry_row = reinterpret_cast<int*>(reinterpret_cast<char*>(workspace) +
                                        align_up((size_t)a.nchunks * 2 * F * sizeof(float), 256));
+  a.kpw = 1;
+  a.chunk_row = plan;
+  a.dbg = env_int("VQGNN_SPMM_DEBUG", 0);
+  a.stamps = nullptr;
+  if (a.dbg & 4) {
+    const size_t need = (size_t)a.nchunks * 4 * sizeof(unsigned long long);
+    if (need > g_stamp_cap) {
+      if (g_stamps) (void)hipFree(g_stamps);
+      (void)hipMalloc(&g_stamps, need);
+      g_stamp_cap = need;
+    }
+    g_stamp_n = (int64_t)a.nchunks * 4;
+    a.stamps = g_stamps;
+  }
   a.ubase = nullptr;
   a.span = a.offx = a.ldxb = a.offx2 = a.ldx2b = 0;
   return X2 ? dispatch_spmm<true>(a, B, (int64_t)n_cols - B, s)
@@ -750,6 +1022,16 @@ static size_t sort_temp_bytes(int64_t nnz, int n_cols) {
   (void)rocprim::radix_sort_pairs((void*)nullptr, bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr,
                             (const int32_t*)nullptr, (int32_t*)nullptr, (size_t)nnz, 0, bits);
   return bytes;
+}
+
+// debug: copy the stamp buffer of the last spmm launch (dbg & 4) to host;
+// returns the number of entries ([chunk-groups][t0, t1, t2, nchunks])
+extern "C" int64_t vqgnn_debug_spmm_stamps(unsigned long long* host, int64_t n) {
+  if (!g_stamps || n <= 0) return g_stamp_n;
+  const int64_t m = n < g_stamp_n ? n : g_stamp_n;
+  (void)hipDeviceSynchronize();
+  (void)hipMemcpy(host, g_stamps, (size_t)m * sizeof(unsigned long long), hipMemcpyDeviceToHost);
+  return m;
 }
 
 extern "C" size_t vqgnn_csr_transpose_workspace(int32_t n_rows, int32_t n_cols, int64_t nnz) {

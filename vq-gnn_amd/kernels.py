@@ -170,7 +170,17 @@ def scatter_codes(batch_idx: torch.Tensor, local: torch.Tensor, codes: torch.Ten
                                     codes.stride(0), stream_ptr()), "scatter_codes")
 
 
-def spmm(rowptr, col, val, n_rows, nnz, X, F, X2=None, B=None, out=None):
+def spmm_plan(rowptr, n_rows, nnz, F):
+    """Chunk plan of a CSR for vqgnn_spmm (include/vqgnn.h §6b)."""
+    L = lib()
+    m = L.vqgnn_spmm_plan_size(int(nnz), int(F))
+    plan = torch.empty(max(m, 1), dtype=torch.int32, device=rowptr.device)
+    check(L.vqgnn_spmm_plan(ptr(rowptr), int(n_rows), int(nnz), int(F), ptr(plan),
+                            stream_ptr()), "spmm_plan")
+    return plan
+
+
+def spmm(rowptr, col, val, n_rows, nnz, X, F, X2=None, B=None, out=None, plan=None):
     """out[i] = sum_e val[e] * xin[col[e]]; xin = X rows (< B), X2 rows (>= B).
     Every column index must be < the rows of xin (X rows, or B + X2 rows)."""
     require_gpu(X, "spmm")
@@ -185,8 +195,8 @@ def spmm(rowptr, col, val, n_rows, nnz, X, F, X2=None, B=None, out=None):
         raise ValueError(f"spmm: X has {X.shape[0]} rows < B={Bv}")
     check(L.vqgnn_spmm(ptr(rowptr), ptr(col), ptr(val), int(n_rows), int(n_cols), int(nnz), Bv,
                        ptr(X), _ld(X),
-                       ptr(X2), _ld(X2) if X2 is not None else 0, F, ptr(out), _ld(out), ptr(ws),
-                       stream_ptr()), "spmm")
+                       ptr(X2), _ld(X2) if X2 is not None else 0, F, ptr(out), _ld(out),
+                       ptr(plan), ptr(ws), stream_ptr()), "spmm")
     return out
 
 

@@ -16,7 +16,8 @@ import torch
 
 
 class CSR:
-    __slots__ = ("rowptr", "col", "value", "_sizes", "_t", "_host_nnz", "_rows", "t_perm")
+    __slots__ = ("rowptr", "col", "value", "_sizes", "_t", "_host_nnz", "_rows", "t_perm",
+                 "_plans")
 
     def __init__(self, rowptr: torch.Tensor, col: torch.Tensor, value: torch.Tensor | None,
                  sparse_sizes):
@@ -29,6 +30,7 @@ class CSR:
         self._t = None
         self._rows = None
         self.t_perm = None
+        self._plans = {}
         self._host_nnz = int(self.col.shape[0])
         if self.rowptr.shape[0] != self._sizes[0] + 1:
             raise ValueError("rowptr must have n_rows + 1 entries")
@@ -89,6 +91,7 @@ class CSR:
         out._t = None
         out._rows = None
         out.t_perm = None
+        out._plans = {}
         out._host_nnz = self._host_nnz
         return out
 
@@ -110,9 +113,19 @@ class CSR:
             t._host_nnz = self._host_nnz
             t._rows = None
             t.t_perm = None
+            t._plans = {}
             self.t_perm = tp
             self._t = t
         return self._t
+
+    def plan(self, F):
+        """SpMM chunk plan for feature width F (include/vqgnn.h §6b); cached."""
+        p = self._plans.get(F)
+        if p is None:
+            from . import kernels
+            p = kernels.spmm_plan(self.rowptr, self._sizes[0], self._host_nnz, F)
+            self._plans[F] = p
+        return p
 
     def rows(self):
         """COO row index of every entry (int32, on the device); cached."""
