@@ -40,6 +40,9 @@ def parse():
     # rehearsal of the N>1 path on one GPU: --backend gloo with
     # VQGNN_BENCH_ONE_DEVICE=1 puts every rank on cuda:0
     p.add_argument("--backend", default="nccl", choices=["nccl", "gloo"])
+    # kernel events inside the timed region (the roofline kernel's launches);
+    # off only to measure what they cost
+    p.add_argument("--no-kernel-events", action="store_true")
     return p.parse_args()
 
 
@@ -143,15 +146,29 @@ def main():
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
-    bank.assign_events = []          # HIP events around each vq_assign_kernel launch
+    # timed region: only the roofline kernel's launches are bracketed by HIP
+    # events (on the stream they are launched on); the per-phase breakdown
+    # is a separate pass below, so its events do not sit in the timed steps
+    if not args.no_kernel_events:
+        bank.assign_events = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step(True)
+        step(False)
     torch.cuda.synchronize()
     barrier()
     t1 = time.perf_counter()
     torch.cuda.synchronize()
-    assign_ev, bank.assign_events = bank.assign_events, None
+    assign_ev, bank.assign_events = bank.assign_events or [], None
+    # per-phase breakdown (untimed for value): update | gather | aggregation
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize()
+    if not assign_ev:           # --no-kernel-events: assign timed in the breakdown pass
+        bank.assign_events = []
+        for _ in range(args.steps):
+            step(False)
+        torch.cuda.synchronize()
+        assign_ev, bank.assign_events = bank.assign_events, None
     bank.check_bad_init()
 
     dt = t1 - t0
