@@ -262,6 +262,9 @@ __global__ void bn_finalize_kernel(const double* __restrict__ sums, int64_t n, i
 // ---------------------------------------------------------------------------
 constexpr int kAssignThreads = 1024;       // non-fused EMA kernel block
 constexpr size_t kLdsBudget = 160 * 1024;
+// codewords of LDS slack after each staged chunk: the sweep prefetches one
+// tile pair ahead without a bound check (staged as e = 0, |e|^2 = +inf)
+constexpr int kSweepSlack = 32;
 
 struct AssignGeom {
   int parts;          // row parts per branch (= EMA partial slabs)
@@ -275,7 +278,9 @@ struct AssignGeom {
 
 template <int KC>
 __host__ __device__ constexpr int q_pad_bytes() {
-  return KC == 1 ? 64 : (KC == 2 ? 128 : 0);
+  // >= kSweepSlack codewords of each plane; mod 256 B (one pass over the 64
+  // banks) the planes keep the bank offsets 16 (KC=1) / 32 (KC=2) / 0 (KC=4)
+  return KC == 1 ? 320 : (KC == 2 ? 384 : 512);
 }
 
 template <int KC>
@@ -283,9 +288,10 @@ __host__ __device__ inline int q_stride_floats(int chunk) {
   return chunk * KC + q_pad_bytes<KC>() / 4;
 }
 
+// codebook planes + |e|^2, each with kSweepSlack codewords of slack
 static size_t cb_lds_bytes(int kc, int chunk) {
-  const int pad = kc == 1 ? 64 : (kc == 2 ? 128 : 0);
-  return (size_t)4 * (chunk * kc * 4 + pad) + (size_t)chunk * 4;
+  const int pad = kc == 1 ? q_pad_bytes<1>() : (kc == 2 ? q_pad_bytes<2>() : q_pad_bytes<4>());
+  return (size_t)4 * (chunk * kc * 4 + pad) + (size_t)(chunk + kSweepSlack) * 4;
 }
 
 // EMA sufficient statistics are int64 fixed point.  Every normalised value
@@ -447,6 +453,12 @@ __device__ __forceinline__ float vmin(float a, float b) {
   return r;
 }
 
+__device__ __forceinline__ float vmin3(float a, float b, float c) {
+  float r;
+  asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
 template <int NG>
 __device__ __forceinline__ int pickn(const int (&a)[NG], int i) {
   int v = a[0];
@@ -455,12 +467,13 @@ __device__ __forceinline__ int pickn(const int (&a)[NG], int i) {
   return v;
 }
 
-// stage codebook rows [mc0, mc0+chunk) of E into LDS (cb [4][qs], se [chunk])
+// stage codebook rows [mc0, mc0+chunk) of E into LDS (cb [4][qs], se [chunk]),
+// and the slack after them as empty codewords (e = 0, |e|^2 = +inf)
 template <int KC, int NT>
 __device__ __forceinline__ void stage_chunk(const float* __restrict__ E, int ldw, int W,
                                             int mc0, int mcount, int chunk, int qs,
                                             float* cb, float* se, int tid) {
-  for (int m = tid; m < chunk; m += NT) {
+  for (int m = tid; m < chunk + kSweepSlack; m += NT) {
     float e[4 * KC];
     const bool mv = m < mcount;
 #pragma unroll
@@ -506,7 +519,7 @@ vq_assign_kernel(const float* __restrict__ X, int64_t ldx,
   float* se = smem + 4 * qs;              // [chunk]
   // [M][W+1] int64 fixed-point accumulators (FUSED), 8-byte aligned
   unsigned long long* acc =
-      reinterpret_cast<unsigned long long*>(se + ((chunk + 1) & ~1));
+      reinterpret_cast<unsigned long long*>(se + chunk + kSweepSlack);
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int q = lane >> 4, j = lane & 15;
@@ -637,7 +650,6 @@ vq_assign_kernel(const float* __restrict__ X, int64_t ldx,
         stage_chunk<KC, NT>(E, ldw, W, mc0, mcount, chunk, qs, cb, se, tid);
         __syncthreads();
       }
-      const float* cbq = cb + q * qs;
       // Sweep: per lane and row group only the running minimum distance and
       // the tile that first reached it (strict <: earliest tile wins ties).
       // Which codeword of the tile it was is resolved after the sweep by an
@@ -645,21 +657,20 @@ vq_assign_kernel(const float* __restrict__ X, int64_t ldx,
       // which keeps v_cmp/v_cndmask (4-cycle issue) out of the per-element
       // path: 3 v_min + 1 v_cmp + 1 v_min + 1 v_cndmask per 4 distances.
       float cbest[NG];
-      int ctile[NG];
+      // the tile that first reached cbest, recorded as the LDS offset register
+      // the sweep read it through (no v_mov of a tile index): the codebook-
+      // plane offset for the even tile of a pair, the |e|^2 offset for the
+      // odd one; the two ranges are disjoint, decoded after the sweep
+      const uint32_t a0 = (uint32_t)(q * qs + j * KC) * 4u;      // plane q, codeword j
+      const uint32_t s0 = (uint32_t)(4 * qs + 4 * q) * 4u;       // |e|^2 of codewords 4q..4q+3
+      uint32_t cmark[NG];
 #pragma unroll
       for (int g = 0; g < NG; ++g) {
         cbest[g] = INFINITY;
-        ctile[g] = 0;
+        cmark[g] = a0;                                            // tile 0
       }
-      // operands of the next tile are read while this tile computes
-      Frag<KC> a_nx = lds_frag<KC>(cbq + j * KC);
-      float4 s_nx = *reinterpret_cast<const float4*>(se + 4 * q);
-      for (int m0 = 0; m0 < mcount; m0 += 16) {
-        const Frag<KC> a = a_nx;
-        const float4 s4 = s_nx;
-        const int mn = min(m0 + 16, chunk - 16);   // in-bounds (staged up to chunk)
-        a_nx = lds_frag<KC>(cbq + (mn + j) * KC);
-        s_nx = *reinterpret_cast<const float4*>(se + mn + 4 * q);
+      const char* lds = reinterpret_cast<const char*>(smem);
+      auto tile = [&](const Frag<KC>& a, const float4& s4, uint32_t mark) {
         floatx4 d[NG];
 #pragma unroll
         for (int g = 0; g < NG; ++g) {
@@ -674,11 +685,41 @@ vq_assign_kernel(const float* __restrict__ X, int64_t ldx,
           float dist[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) dist[r] = fmaf(-2.f, d[g][r], __fadd_rn(sx[g], sev[r]));
-          const float m = vmin(vmin(dist[0], dist[1]), vmin(dist[2], dist[3]));
-          ctile[g] = (m < cbest[g]) ? m0 : ctile[g];
-          cbest[g] = vmin(cbest[g], m);
+          // n = min(cbest, tile min); n < cbest <=> the tile min < cbest
+          // (strict: the earliest tile wins ties)
+          const float n = vmin3(cbest[g], vmin3(dist[0], dist[1], dist[2]), dist[3]);
+          cmark[g] = (n < cbest[g]) ? mark : cmark[g];
+          cbest[g] = n;
         }
+      };
+      // Sweep over tile pairs: per lane and row group only the running minimum
+      // and the tile that first reached it.  Which codeword of the tile it was
+      // is resolved after the sweep by an exact recompute (the f32 MFMA is
+      // bit-for-bit a k-ordered fma chain), which keeps v_cmp/v_cndmask
+      // (4-cycle issue) out of the per-element path.  Operands of the next
+      // pair are read while this pair computes (past the last tile: slack).
+      uint32_t ao = a0, so = s0;
+      Frag<KC> a_n0 = lds_frag<KC>(reinterpret_cast<const float*>(lds + ao));
+      Frag<KC> a_n1 = lds_frag<KC>(reinterpret_cast<const float*>(lds + ao + 16 * KC * 4));
+      float4 s_n0 = *reinterpret_cast<const float4*>(lds + so);
+      float4 s_n1 = *reinterpret_cast<const float4*>(lds + so + 64);
+      for (int m0 = 0; m0 < mcount; m0 += 32) {
+        const Frag<KC> a_0 = a_n0, a_1 = a_n1;
+        const float4 s_0 = s_n0, s_1 = s_n1;
+        a_n0 = lds_frag<KC>(reinterpret_cast<const float*>(lds + ao + 32 * KC * 4));
+        a_n1 = lds_frag<KC>(reinterpret_cast<const float*>(lds + ao + 48 * KC * 4));
+        s_n0 = *reinterpret_cast<const float4*>(lds + so + 128);
+        s_n1 = *reinterpret_cast<const float4*>(lds + so + 192);
+        tile(a_0, s_0, ao);
+        tile(a_1, s_1, so);          // past mcount: empty codewords, never < cbest
+        ao += 32 * KC * 4;
+        so += 128;
       }
+      int ctile[NG];
+#pragma unroll
+      for (int g = 0; g < NG; ++g)
+        ctile[g] = cmark[g] >= (uint32_t)(4 * qs * 4) ? (int)((cmark[g] - s0) >> 2) + 16
+                                                      : (int)((cmark[g] - a0) / (KC * 4));
       // Resolve, spread over the 4 q-lanes of a row: the row minimum, the
       // first (tile, q-lane) that reached it (index order = (tile, q, r)),
       // then lane q recomputes candidate r = q of that lane's codewords with
