@@ -58,6 +58,30 @@ def test_spmm_hub_rows_span_chunks():
     assert np.max(np.abs(out.cpu().numpy() - ref) / scale) < 1e-5
 
 
+@pytest.mark.parametrize("F", [16, 64, 128, 256, 604])
+def test_spmm_many_adjacent_long_rows(F):
+    """Runs of rows longer than L = 256 edges: several rows end inside one
+    wave's 64 chunks, so the fixup sums up to 64/F4 rows at a time."""
+    rng = np.random.default_rng(F + 7)
+    n_rows, n_cols = 400, 900
+    deg = rng.integers(0, 30, size=n_rows)
+    deg[100:160] = rng.integers(257, 700, size=60)
+    deg[300:303] = 900
+    rowptr = np.zeros(n_rows + 1, np.int64)
+    rowptr[1:] = np.cumsum(deg)
+    col = np.concatenate([np.sort(rng.choice(n_cols, size=d, replace=False)) for d in deg])
+    val = rng.standard_normal(col.shape[0]).astype(np.float32)
+    x = rng.standard_normal((n_cols, F)).astype(np.float32)
+    a = _dev_csr(rowptr, col, val, n_rows, n_cols)
+    xd = torch.from_numpy(x).to(DEV)
+    out = kernels.spmm(a.rowptr, a.col, a.value, n_rows, a.nnz(), xd, F)
+    ref = conv_ref.spmm_fp64(rowptr, col, val, x)
+    scale = conv_ref.spmm_fp64(rowptr, col, np.abs(val), np.abs(x)) + 1e-6
+    assert np.max(np.abs(out.cpu().numpy() - ref) / scale) < 1e-5
+    again = kernels.spmm(a.rowptr, a.col, a.value, n_rows, a.nnz(), xd, F)
+    assert torch.equal(out, again)      # fixed chunk order: deterministic
+
+
 def test_spmm_empty_and_degenerate():
     x = torch.randn(10, 8, device=DEV)
     a = _dev_csr([0, 0, 0, 0], [], [], 3, 10)

@@ -646,6 +646,10 @@ spmm_wave_kernel(SpmmArgs a) {
 // One wave scans 64 chunks and serves the few that end a spanning row.
 __global__ void __launch_bounds__(256)
 spmm_fixup_kernel(SpmmArgs a) {
+  // rows longer than L: out[row] = carry1[gs] + carry0[gs+1] + ... + carry0[ch]
+  // (chunk order).  A wave finds the rows that end in its 64 chunks, then
+  // sums R of them at once (R = 64 / the column group, 2 at F = 128), with the
+  // carry loads of up to 8 chunks in flight ahead of the in-order adds.
   const int lane = threadIdx.x & 63;
   const int chunk = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 64 + lane;
   bool need = false;
@@ -659,23 +663,44 @@ spmm_fixup_kernel(SpmmArgs a) {
   }
   unsigned long long mask = __ballot(need);
   const int F4 = a.F4;
+  int cw = 1;                                  // lanes per row: pow2 >= F4, <= 64
+  while (cw < F4 && cw < 64) cw <<= 1;
+  const int R = 64 / cw;
+  const int h = lane / cw, c0 = lane % cw;
   const float4* carry4 = reinterpret_cast<const float4*>(a.carry);
   float4* out4 = reinterpret_cast<float4*>(a.out);
+  auto add4 = [](float4 s, float4 t) {
+    s.x = __fadd_rn(s.x, t.x);
+    s.y = __fadd_rn(s.y, t.y);
+    s.z = __fadd_rn(s.z, t.z);
+    s.w = __fadd_rn(s.w, t.w);
+    return s;
+  };
   while (mask) {
-    const int src = __ffsll((long long)mask) - 1;
-    mask &= mask - 1;
-    const int ch = __shfl(chunk, src);
-    const int row = __shfl(r, src);
+    // the h-th of the next R set bits
+    unsigned long long m = mask;
+    int src = -1;
+    for (int i = 0; i < R && m; ++i) {
+      const int b = __ffsll((long long)m) - 1;
+      m &= m - 1;
+      if (i == h) src = b;
+    }
+    mask = m;
+    const int ch = __shfl(chunk, src < 0 ? 0 : src);
+    const int row = __shfl(r, src < 0 ? 0 : src);
+    if (src < 0) continue;
     const int gs = a.rowptr[row] / a.S;
-    for (int cc = lane; cc < F4; cc += 64) {
+    for (int cc = c0; cc < F4; cc += cw) {
       float4 s = carry4[((int64_t)gs * 2 + 1) * F4 + cc];
-      for (int g = gs + 1; g <= ch; ++g) {
-        const float4 t = carry4[(int64_t)g * 2 * F4 + cc];
-        s.x = __fadd_rn(s.x, t.x);
-        s.y = __fadd_rn(s.y, t.y);
-        s.z = __fadd_rn(s.z, t.z);
-        s.w = __fadd_rn(s.w, t.w);
+      int g = gs + 1;
+      for (; g + 8 <= ch + 1; g += 8) {
+        float4 t[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) t[u] = carry4[(int64_t)(g + u) * 2 * F4 + cc];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s = add4(s, t[u]);
       }
+      for (; g <= ch; ++g) s = add4(s, carry4[(int64_t)g * 2 * F4 + cc]);
       out4[(int64_t)row * a.ldo4 + cc] = s;
     }
   }
