@@ -250,6 +250,57 @@ int vqgnn_gat_edge_grad(const int32_t* rows, const int32_t* col, const float* co
                         const float* params, float negative_slope, float* dalpha_l,
                         float* dalpha_r, float* ds_row, vqgnn_stream_t stream);
 
+/* ------------------------------------------------------------------------ *
+ * 9. Mini-batch construction on the device.
+ *    Replaces OurDataLoader._k_hop_subgraph (dataloader.py:98-148; num_hops,
+ *    relabel_nodes=True, train_flag) and the SparseTensor build of
+ *    prepare_batch_input (utils/misc.py:73).
+ *    Full graph (data.adj_t, the normalised adjacency): rowptr int64 [N+1],
+ *    col int32 [nnz_g < 2^31], val fp32.  node_idx int64 [B] (batch nodes).
+ *
+ *    vqgnn_khop_subset: node_map [N] (local id or -1), subset [capacity N]
+ *      = [node_idx ; B' in ascending global id] (dataloader.py:121-126),
+ *      out_rowptr [capacity N+1] of the rows emitted, and
+ *      sizes [4] on the device = {n, nnz, rows emitted, status}; status =
+ *      VQGNN_KHOP_OUT_OF_RANGE if a node id is outside [0, N).  A node
+ *      repeated in node_idx behaves as in the reference: every copy stays in
+ *      subset[:B], the last copy is its local id (node_idx[subset] = arange,
+ *      :144), the rows of earlier copies are empty.
+ *      order VQGNN_KHOP_ORDER_CSR: rows = subset order (every local row).
+ *      order VQGNN_KHOP_ORDER_REF: rows = the reference's edge_index row order
+ *      (ascending global id; eval: the batch nodes only), written to rows
+ *      [capacity N].
+ *      Kept entries: train -> both ends in subset (:132-133); eval -> rows
+ *      of batch nodes (:136-138).
+ *    vqgnn_khop_edges: after the caller read sizes (n, nnz, rows emitted):
+ *      ORDER_CSR: out_col / out_val sorted by local column in every row -> the
+ *      batch CSR the layer consumes (local row r = subset[r]);
+ *      ORDER_REF: entries in edge_index[:, edge_mask] order (global row, then
+ *      global column), out_row = local row (edge_index[0]).
+ *      rows = subset (ORDER_CSR) or the rows array of vqgnn_khop_subset.
+ *    vqgnn_coo_to_csr: SparseTensor(row=, col=, value=, sparse_sizes) ->
+ *      CSR sorted by (row, col), stable for repeated (row, col) pairs; status
+ *      (device int64) = VQGNN_KHOP_OUT_OF_RANGE if an index is outside.
+ * ------------------------------------------------------------------------ */
+enum vqgnn_khop_order { VQGNN_KHOP_ORDER_CSR = 0, VQGNN_KHOP_ORDER_REF = 1 };
+enum vqgnn_khop_status { VQGNN_KHOP_OUT_OF_RANGE = 2 };
+size_t vqgnn_khop_workspace(int64_t N);
+int vqgnn_khop_subset(const int64_t* rowptr, const int32_t* col, int64_t N,
+                      const int64_t* node_idx, int32_t B, int32_t num_hops, int32_t train_flag,
+                      int32_t order, int32_t* node_map, int64_t* subset, int64_t* rows,
+                      int32_t* out_rowptr, int64_t* sizes, void* workspace,
+                      vqgnn_stream_t stream);
+size_t vqgnn_khop_edges_workspace(int64_t nrows, int64_t nnz);
+int vqgnn_khop_edges(const int64_t* rowptr, const int32_t* col, const float* val, int64_t N,
+                     const int32_t* node_map, const int64_t* rows, int64_t nrows, int64_t n,
+                     int32_t B, int32_t train_flag, int32_t order, const int32_t* out_rowptr,
+                     int64_t nnz, int32_t* out_col, float* out_val, int32_t* out_row,
+                     void* workspace, vqgnn_stream_t stream);
+size_t vqgnn_coo_to_csr_workspace(int64_t nnz, int64_t n_rows, int64_t n_cols);
+int vqgnn_coo_to_csr(const int64_t* row, const int64_t* col, const float* val, int64_t nnz,
+                     int64_t n_rows, int64_t n_cols, int32_t* out_rowptr, int32_t* out_col,
+                     float* out_val, int64_t* status, void* workspace, vqgnn_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,120 @@
+"""CPU checks of the batch-construction oracle (oracle/subgraph_ref.py, the
+restatement of vq_gnn_v2/dataloader.py:98-148 + utils/misc.py:73): a
+hand-computed known answer, a pure-Python loop restatement on random graphs
+(train / eval, 1 and 2 hops), and agreement with the numpy batch builder the
+bench uses (vq_gnn_amd/graph.py)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import subgraph_ref
+from vq_gnn_amd import graph
+
+
+def _csr(n, edges):
+    """Symmetric CSR with sorted columns from undirected (u, v) pairs."""
+    adj = {u: set() for u in range(n)}
+    for u, v in edges:
+        adj[u].add(v)
+        adj[v].add(u)
+    rowptr = [0]
+    col = []
+    for u in range(n):
+        col += sorted(adj[u])
+        rowptr.append(len(col))
+    val = np.arange(1, len(col) + 1, dtype=np.float32) / 8   # distinct, exact weights
+    return np.array(rowptr), np.array(col), val
+
+
+def _loop(rowptr, col, val, N, node_idx, hops, train_flag):
+    """Breadth-first loop restatement: nodes within `hops` of the batch."""
+    node_idx = [int(v) for v in node_idx]
+    seen = set(node_idx)
+    frontier = list(node_idx)
+    for _ in range(hops):
+        nxt = []
+        for u in frontier:
+            for e in range(rowptr[u], rowptr[u + 1]):
+                nxt.append(int(col[e]))
+        seen |= set(nxt)
+        frontier = nxt
+    batch = set(node_idx)
+    subset = node_idx + sorted(seen - batch)
+    pos = {v: i for i, v in enumerate(subset)}
+    rows, cols, ws = [], [], []
+    for u in range(N):
+        for e in range(rowptr[u], rowptr[u + 1]):
+            v = int(col[e])
+            ok = (u in pos and v in pos) if train_flag else (u in batch)
+            if ok:
+                rows.append(pos[u])
+                cols.append(pos[v])
+                ws.append(val[e])
+    return np.array(subset), np.array([rows, cols]).reshape(2, -1), np.array(ws, np.float32)
+
+
+def test_k_hop_known_answer():
+    # 0-1, 1-2, 2-3, 3-4, 5-6, 0-5 ; batch = [3, 1]
+    rowptr, col, val = _csr(7, [(0, 1), (1, 2), (2, 3), (3, 4), (5, 6), (0, 5)])
+    subset, ei, w = subgraph_ref.k_hop_subgraph(rowptr, col, val, 7, [3, 1])
+    # neighbours of {3, 1}: {2, 4} and {0, 2} -> B' = [0, 2, 4] ascending
+    assert subset.tolist() == [3, 1, 0, 2, 4]
+    # train: edges with both ends in {0,1,2,3,4}, global row order, relabelled
+    # rows 0:(1) 1:(0,2) 2:(1,3) 3:(2,4) 4:(3)  -> local ids via [3,1,0,2,4]
+    assert ei.tolist() == [[2, 1, 1, 3, 3, 0, 0, 4],
+                           [1, 2, 3, 1, 0, 3, 4, 0]]
+    # weights follow the kept global entries: entries 0 (0->1), 2 (1->0), 3 (1->2) ...
+    kept = [0, 2, 3, 4, 5, 6, 7, 8]     # global CSR positions of the kept entries
+    assert np.array_equal(w.numpy(), val[kept])
+    # eval: rows of batch nodes only
+    _, ei_e, _ = subgraph_ref.k_hop_subgraph(rowptr, col, val, 7, [3, 1], train_flag=False)
+    assert ei_e.tolist() == [[1, 1, 0, 0], [2, 3, 3, 4]]
+
+
+@pytest.mark.parametrize("seed,hops,train", [(0, 1, True), (1, 1, False), (2, 2, True),
+                                             (3, 2, False), (4, 3, True)])
+def test_k_hop_oracle_vs_loop(seed, hops, train):
+    rng = np.random.default_rng(seed)
+    N = 60
+    edges = {(int(a), int(b)) for a, b in rng.integers(0, N, size=(90, 2)) if a != b}
+    rowptr, col, val = _csr(N, sorted(edges))
+    node_idx = rng.permutation(N)[:12]                 # unsorted batch
+    s, ei, w = subgraph_ref.k_hop_subgraph(rowptr, col, val, N, node_idx, hops, train)
+    s2, ei2, w2 = _loop(rowptr, col, val, N, node_idx, hops, train)
+    assert np.array_equal(s.numpy(), s2)
+    assert np.array_equal(ei.numpy(), ei2)
+    assert np.array_equal(w.numpy(), w2)
+
+
+@pytest.mark.parametrize("train", [True, False])
+def test_oracle_csr_matches_batch_builder(train):
+    g = graph.synthetic_graph(3000, 6, 9000, seed=1)
+    rp, cl, vl = graph.norm_adj(g, "GCN")
+    node_idx = graph.cluster_batch(g, [4, 1, 3])
+    b = graph.k_hop_batch(rp, cl, vl, g.N, node_idx, train)
+    subset, ei, w = subgraph_ref.k_hop_subgraph(rp, cl, vl, g.N, node_idx, 1, train)
+    rowptr, col, val = subgraph_ref.sparse_tensor_csr(ei[0], ei[1], w, subset.numel(),
+                                                      subset.numel())
+    assert np.array_equal(subset.numpy(), b.subset)
+    assert np.array_equal(rowptr.numpy(), b.rowptr)
+    assert np.array_equal(col.numpy(), b.col)
+    assert np.array_equal(val.numpy(), b.val)
+
+
+def test_oracle_edge_cases():
+    rowptr, col, val = _csr(5, [(0, 1), (1, 2)])
+    # empty batch
+    s, ei, w = subgraph_ref.k_hop_subgraph(rowptr, col, val, 5, torch.zeros(0, dtype=torch.int64))
+    assert s.numel() == 0 and ei.shape == (2, 0) and w.numel() == 0
+    # isolated batch node
+    s, ei, _ = subgraph_ref.k_hop_subgraph(rowptr, col, val, 5, [4])
+    assert s.tolist() == [4] and ei.shape == (2, 0)
+    # repeated batch node: the assert at dataloader.py:128 holds (subset keeps
+    # both copies); the relabelling's last write wins (:144)
+    s, ei, _ = subgraph_ref.k_hop_subgraph(rowptr, col, val, 5, [1, 1])
+    assert s.tolist() == [1, 1, 0, 2]
+    assert ei.tolist() == [[2, 1, 1, 3], [1, 2, 3, 1]]
+    # SparseTensor ordering keeps repeated (row, col) entries in input order
+    rp, c, v = subgraph_ref.sparse_tensor_csr([1, 0, 1, 1], [2, 3, 0, 2], [1., 2., 3., 4.], 3, 4)
+    assert rp.tolist() == [0, 1, 4, 4] and c.tolist() == [3, 0, 2, 2]
+    assert v.tolist() == [2., 3., 1., 4.]

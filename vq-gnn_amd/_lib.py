@@ -76,6 +76,19 @@ SIGNATURES = {
                                            _c_void_p, _i64, _i32, _i32, _c_void_p, _i64,
                                            _c_void_p, _c_void_p, _c_void_p, _c_void_p, _f32,
                                            _c_void_p, _c_void_p, _c_void_p, _c_void_p]),
+    # §9 mini-batch construction
+    "vqgnn_khop_workspace": (_size, [_i64]),
+    "vqgnn_khop_subset": (ctypes.c_int, [_c_void_p, _c_void_p, _i64, _c_void_p, _i32, _i32, _i32,
+                                         _i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
+                                         _c_void_p, _c_void_p, _c_void_p]),
+    "vqgnn_khop_edges_workspace": (_size, [_i64, _i64]),
+    "vqgnn_khop_edges": (ctypes.c_int, [_c_void_p, _c_void_p, _c_void_p, _i64, _c_void_p,
+                                        _c_void_p, _i64, _i64, _i32, _i32, _i32, _c_void_p, _i64,
+                                        _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p]),
+    "vqgnn_coo_to_csr_workspace": (_size, [_i64, _i64, _i64]),
+    "vqgnn_coo_to_csr": (ctypes.c_int, [_c_void_p, _c_void_p, _c_void_p, _i64, _i64, _i64,
+                                        _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
+                                        _c_void_p]),
 }
 
 _lock = threading.Lock()

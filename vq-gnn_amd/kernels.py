@@ -275,3 +275,83 @@ def gat_edge_grad(rows, col, coef, nnz, X, F, dy, dden, al, ar, params, X2=None,
                                     float(negative_slope), ptr(dal), ptr(dar), ptr(dsr),
                                     stream_ptr()), "gat_edge_grad")
     return dal, dar, dsr
+
+
+# ---- mini-batch construction (include/vqgnn.h §9) ----
+
+KHOP_ORDER_CSR, KHOP_ORDER_REF = 0, 1
+KHOP_OUT_OF_RANGE = 2
+
+
+def _khop_status(status: int) -> None:
+    if status & KHOP_OUT_OF_RANGE:
+        # node_mask[subsets[-1]] = True (dataloader.py:115) raises IndexError
+        raise IndexError("k_hop_subgraph: node index out of range")
+
+
+def khop_subgraph(rowptr, col, val, N, node_idx, num_hops=1, train_flag=True,
+                  order=KHOP_ORDER_CSR):
+    """_k_hop_subgraph (dataloader.py:98-148) of node_idx on the full graph
+    (rowptr int64 [N+1], col int32, val fp32, all on the device).
+
+    Returns dict(subset int64 [n], node_map int32 [N], rowptr int32 [rows+1],
+    col int32 [nnz], val fp32 [nnz], row int32 [nnz] (ORDER_REF only), n, nnz,
+    rows).  One device->host read of the sizes (the outputs are data-sized)."""
+    require_gpu(rowptr, "khop_subgraph")
+    dev = rowptr.device
+    node_idx = node_idx.to(device=dev, dtype=torch.int64).contiguous()
+    B = int(node_idx.numel())
+    N = int(N)
+    L = lib()
+    node_map = torch.empty(max(N, 1), dtype=torch.int32, device=dev)
+    subset = torch.empty(max(N, 1), dtype=torch.int64, device=dev)
+    rows = torch.empty(max(N, 1), dtype=torch.int64, device=dev) if order == KHOP_ORDER_REF \
+        else None
+    out_rowptr = torch.empty(N + 1, dtype=torch.int32, device=dev)
+    sizes = torch.zeros(4, dtype=torch.int64, device=dev)
+    ws = workspace(L.vqgnn_khop_workspace(N), dev)
+    check(L.vqgnn_khop_subset(ptr(rowptr), ptr(col), N, ptr(node_idx), B, int(num_hops),
+                              int(bool(train_flag)), int(order), ptr(node_map), ptr(subset),
+                              ptr(rows), ptr(out_rowptr), ptr(sizes), ptr(ws), stream_ptr()),
+          "khop_subset")
+    n, nnz, nrows, status = (int(v) for v in sizes.cpu())
+    _khop_status(status)
+    out_col = torch.empty(max(nnz, 1), dtype=torch.int32, device=dev)
+    out_val = torch.empty(max(nnz, 1), dtype=torch.float32, device=dev)
+    out_row = torch.empty(max(nnz, 1), dtype=torch.int32, device=dev) \
+        if order == KHOP_ORDER_REF else None
+    emit = rows if order == KHOP_ORDER_REF else subset
+    ws2 = workspace(L.vqgnn_khop_edges_workspace(nrows, nnz), dev)
+    check(L.vqgnn_khop_edges(ptr(rowptr), ptr(col), ptr(val), N, ptr(node_map), ptr(emit), nrows,
+                             n, B, int(bool(train_flag)), int(order), ptr(out_rowptr), nnz,
+                             ptr(out_col), ptr(out_val), ptr(out_row), ptr(ws2), stream_ptr()),
+          "khop_edges")
+    return dict(subset=subset[:n], node_map=node_map[:N], rowptr=out_rowptr[:nrows + 1],
+                col=out_col[:nnz], val=out_val[:nnz],
+                row=out_row[:nnz] if out_row is not None else None,
+                rows=rows[:nrows] if rows is not None else None, n=n, nnz=nnz)
+
+
+def coo_to_csr(row, col, val, n_rows, n_cols):
+    """SparseTensor(row=, col=, value=, sparse_sizes=(n_rows, n_cols)) ->
+    (rowptr int32, col int32, val fp32) sorted by (row, col), stable."""
+    require_gpu(row, "coo_to_csr")
+    dev = row.device
+    row = row.to(torch.int64).contiguous()
+    col = col.to(device=dev, dtype=torch.int64).contiguous()
+    nnz = int(row.numel())
+    if val is None:
+        val = torch.ones(nnz, dtype=torch.float32, device=dev)
+    val = val.to(device=dev, dtype=torch.float32).contiguous()
+    L = lib()
+    out_rowptr = torch.empty(int(n_rows) + 1, dtype=torch.int32, device=dev)
+    out_col = torch.empty(max(nnz, 1), dtype=torch.int32, device=dev)
+    out_val = torch.empty(max(nnz, 1), dtype=torch.float32, device=dev)
+    status = torch.zeros(1, dtype=torch.int64, device=dev)
+    ws = workspace(L.vqgnn_coo_to_csr_workspace(nnz, int(n_rows), int(n_cols)), dev)
+    check(L.vqgnn_coo_to_csr(ptr(row), ptr(col), ptr(val), nnz, int(n_rows), int(n_cols),
+                             ptr(out_rowptr), ptr(out_col), ptr(out_val), ptr(status), ptr(ws),
+                             stream_ptr()), "coo_to_csr")
+    if int(status.item()) & KHOP_OUT_OF_RANGE:
+        raise IndexError("coo_to_csr: index out of range")
+    return out_rowptr, out_col[:nnz], out_val[:nnz]
