@@ -86,6 +86,18 @@ int vqgnn_bn_finalize(const double* sums, int64_t count, int32_t F, int32_t with
                       int64_t* nbt_f, int64_t* nbt_g, int32_t nbt_d,
                       vqgnn_stream_t stream);
 
+/* 2b. Single-process shortcut: vqgnn_bn_stats + vqgnn_bn_finalize in two
+ *     kernels (the reduce and the finalize fused: one wave per data column,
+ *     same summation order, same bits).  mode must be a batch-statistics mode
+ *     (1..3); count = B.  sums (optional) receives the fp64 sums.  Multi-GPU
+ *     callers all-reduce the sums between the two calls instead. */
+int vqgnn_bn_stats_finalize(const float* X, int64_t ldx, const float* G, int64_t ldg,
+                            int32_t B, int32_t F, int32_t with_grad, double* sums, int32_t mode,
+                            float momentum_f, float eps_f, float momentum_g, float eps_g,
+                            float eps_std, float* rm_f, float* rv_f, float* rm_g, float* rv_g,
+                            float* coef, float* batch_out, int64_t* nbt_f, int64_t* nbt_g,
+                            int32_t nbt_d, void* workspace, vqgnn_stream_t stream);
+
 /* ------------------------------------------------------------------------ *
  * 3. Product-quantised nearest-codeword assignment for nb branches at once,
  *    plus (ema_parts != NULL) the EMA sufficient statistics.

@@ -190,3 +190,22 @@ def test_bad_init_raises_on_gpu():
     bank = _bank_from_pre(meta, rec["pre"], False)
     with pytest.raises(ValueError, match="Bad Init!"):
         bank.feature_update(rec["X"].to(DEV), 0, 1, True)
+
+
+def test_update_eval_mode_stashes_batch_stats():
+    """vq.py:208-211: update() records the batch mean / std in every mode,
+    including eval after the running statistics were initialised."""
+    torch.manual_seed(3)
+    m = VectorQuantizerEMA(64, 4, grad_normalize_scale=[1, 1], warm_up_flag=True).to(DEV)
+    m.train()
+    m.update(torch.randn(400, 4, device=DEV), torch.randn(400, 4, device=DEV) * 1e-3)
+    m.eval()
+    X = torch.randn(300, 4, device=DEV) * 2 + 1
+    G = torch.randn(300, 4, device=DEV) * 1e-3
+    rm = m.batch_norm_feat.running_mean.clone()
+    m.update(X, G)
+    inputs = torch.cat([X, G], 1)
+    torch.testing.assert_close(m.mean, inputs.mean(0, keepdim=True), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(m.std, torch.sqrt(inputs.var(0, keepdim=True) + 1e-24),
+                               rtol=1e-5, atol=1e-7)
+    assert torch.equal(m.batch_norm_feat.running_mean, rm)      # eval: running stats untouched

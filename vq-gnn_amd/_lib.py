@@ -76,6 +76,11 @@ SIGNATURES = {
                                            _c_void_p, _i64, _i32, _i32, _c_void_p, _i64,
                                            _c_void_p, _c_void_p, _c_void_p, _c_void_p, _f32,
                                            _c_void_p, _c_void_p, _c_void_p, _c_void_p]),
+    "vqgnn_bn_stats_finalize": (ctypes.c_int, [_c_void_p, _i64, _c_void_p, _i64, _i32, _i32, _i32,
+                                               _c_void_p, _i32, _f32, _f32, _f32, _f32, _f32,
+                                               _c_void_p, _c_void_p, _c_void_p, _c_void_p,
+                                               _c_void_p, _c_void_p, _c_void_p, _c_void_p,
+                                               _i32, _c_void_p, _c_void_p]),
     # §9 mini-batch construction
     "vqgnn_khop_workspace": (_size, [_i64]),
     "vqgnn_khop_subset": (ctypes.c_int, [_c_void_p, _c_void_p, _i64, _c_void_p, _i32, _i32, _i32,

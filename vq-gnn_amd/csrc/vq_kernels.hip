@@ -181,7 +181,10 @@ bn_stats_reduce_kernel(const double* __restrict__ part, int chunks, int F, int C
 //    running_var uses the unbiased variance.  Eval: invstd = 1/sqrtf(rv+eps)
 //    in float (opmath).  beta = -(mean*alpha) in float.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void bn_column(double s, double s2, int64_t n, int mode,
+// have: the batch sums are available (always in the training modes; in eval
+// mode for update(), whose batch mean / std stash runs in every mode,
+// vq.py:208-211)
+__device__ __forceinline__ void bn_column(double s, double s2, bool have, int64_t n, int mode,
                                           float momentum, float eps, float eps_std,
                                           float* rm, float* rv, float* alpha, float* beta,
                                           float* mean_out, float* std_out) {
@@ -189,7 +192,7 @@ __device__ __forceinline__ void bn_column(double s, double s2, int64_t n, int mo
   const bool init = mode >= 2;
   const double nd = (double)n;
   double mean = 0.0, var_b = 0.0, var_u = 0.0;
-  if (train || init) {
+  if (have) {
     mean = s / nd;
     double m2 = s2 - s * mean;            // sum (x - mean)^2
     if (m2 < 0.0) m2 = 0.0;
@@ -229,15 +232,57 @@ __global__ void bn_finalize_kernel(const double* __restrict__ sums, int64_t n, i
     if (nbt_f) nbt_f[c / D] += 1;
     if (nbt_g && with_grad) nbt_g[c / D] += 1;
   }
-  bn_column(sums[c], sums[F + c], n, mode, mom_f, eps_f, eps_std, rm_f + c, rv_f + c,
-            coef + c, coef + F + c, batch_out ? batch_out + c : nullptr,
+  const bool have = sums != nullptr;
+  bn_column(have ? sums[c] : 0.0, have ? sums[F + c] : 0.0, have, n, mode, mom_f, eps_f, eps_std,
+            rm_f + c, rv_f + c, coef + c, coef + F + c, batch_out ? batch_out + c : nullptr,
             batch_out ? batch_out + F + c : nullptr);
   if (with_grad) {
-    bn_column(sums[2 * F + c], sums[3 * F + c], n, mode, mom_g, eps_g, eps_std, rm_g + c,
+    bn_column(have ? sums[2 * F + c] : 0.0, have ? sums[3 * F + c] : 0.0, have, n, mode, mom_g,
+              eps_g, eps_std, rm_g + c,
               rv_g + c, coef + 2 * F + c, coef + 3 * F + c,
               batch_out ? batch_out + 2 * F + c : nullptr,
               batch_out ? batch_out + 3 * F + c : nullptr);
   }
+}
+
+// Single-process fusion of bn_stats_reduce + bn_finalize: one wave per data
+// column c in [0, C) folds its sum and sum of squares in the reduce kernel's
+// order (lane-strided chunks, then the butterfly: the same bits), then lane 0
+// runs the column's BatchNorm update.  No all-reduce can sit between the two
+// here, so multi-GPU callers keep vqgnn_bn_stats + vqgnn_bn_finalize.
+__global__ void __launch_bounds__(kReduceWaves * 64)
+bn_reduce_finalize_kernel(const double* __restrict__ part, int chunks, int F, int C,
+                          double* __restrict__ sums, int64_t n, int mode, float mom_f,
+                          float eps_f, float mom_g, float eps_g, float eps_std, float* rm_f,
+                          float* rv_f, float* rm_g, float* rv_g, float* __restrict__ coef,
+                          float* __restrict__ batch_out, long long* __restrict__ nbt_f,
+                          long long* __restrict__ nbt_g, int D) {
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * kReduceWaves + (threadIdx.x >> 6);   // data column in [0, C)
+  if (c >= C) return;
+  double a = 0.0, q = 0.0;
+  for (int p = lane; p < chunks; p += 64) a += part[(int64_t)p * 2 * C + c];
+  for (int p = lane; p < chunks; p += 64) q += part[(int64_t)p * 2 * C + C + c];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    a += __shfl_xor(a, off);
+    q += __shfl_xor(q, off);
+  }
+  if (lane != 0) return;
+  const bool g = c >= F;
+  const int k = g ? c - F : c;
+  if (sums) {
+    sums[(g ? 2 * F : 0) + k] = a;
+    sums[(g ? 3 * F : F) + k] = q;
+  }
+  if (D > 0 && k % D == 0) {   // BatchNorm1d.num_batches_tracked += 1 (train)
+    long long* nbt = g ? nbt_g : nbt_f;
+    if (nbt) nbt[k / D] += 1;
+  }
+  const int o = g ? 2 * F : 0;
+  bn_column(a, q, true, n, mode, g ? mom_g : mom_f, g ? eps_g : eps_f, eps_std,
+            (g ? rm_g : rm_f) + k, (g ? rv_g : rv_f) + k, coef + o + k, coef + o + F + k,
+            batch_out ? batch_out + o + k : nullptr, batch_out ? batch_out + o + F + k : nullptr);
 }
 
 // ---------------------------------------------------------------------------
@@ -1026,6 +1071,41 @@ extern "C" int vqgnn_bn_finalize(const double* sums, int64_t count, int32_t F, i
                      reinterpret_cast<long long*>(nbt_f), reinterpret_cast<long long*>(nbt_g),
                      nbt_d);
   return check_launch("bn_finalize");
+}
+
+extern "C" int vqgnn_bn_stats_finalize(const float* X, int64_t ldx, const float* G, int64_t ldg,
+                                       int32_t B, int32_t F, int32_t with_grad, double* sums,
+                                       int32_t mode, float momentum_f, float eps_f,
+                                       float momentum_g, float eps_g, float eps_std, float* rm_f,
+                                       float* rv_f, float* rm_g, float* rv_g, float* coef,
+                                       float* batch_out, int64_t* nbt_f, int64_t* nbt_g,
+                                       int32_t nbt_d, void* workspace, vqgnn_stream_t stream) {
+  clear_error();
+  VQGNN_REQUIRE(X && coef && rm_f && rv_f && workspace, "bn_stats_finalize: null pointer");
+  VQGNN_REQUIRE(B > 0 && F > 0 && ldx >= F, "bn_stats_finalize: bad shape B=%d F=%d", B, F);
+  VQGNN_REQUIRE(mode >= 1 && mode <= 3, "bn_stats_finalize: mode must use batch statistics");
+  VQGNN_REQUIRE(!with_grad || (G && ldg >= F && rm_g && rv_g), "bn_stats_finalize: grads required");
+  const bool vec = F % 4 == 0 && ldx % 4 == 0 && ((uintptr_t)X & 15) == 0 &&
+                   (!with_grad || (ldg % 4 == 0 && ((uintptr_t)G & 15) == 0));
+  const int C = with_grad ? 2 * F : F;
+  const int C4 = (C + 3) / 4;
+  const int chunks = stats_chunks(B, C4);
+  const int rpc = (B + chunks - 1) / chunks;
+  double* part = reinterpret_cast<double*>(workspace);
+  hipStream_t s = as_stream(stream);
+  if (vec) {
+    hipLaunchKernelGGL(bn_stats_partial_kernel, dim3(chunks), dim3(kStatsThreads), 0, s, X, ldx,
+                       G, ldg, B, F / 4, C4, rpc, part);
+  } else {
+    hipLaunchKernelGGL(bn_stats_partial_scalar_kernel, dim3(chunks), dim3(kStatsThreads), 0, s,
+                       X, ldx, G, ldg, B, F, C, rpc, part);
+  }
+  hipLaunchKernelGGL(bn_reduce_finalize_kernel, dim3((C + kReduceWaves - 1) / kReduceWaves),
+                     dim3(kReduceWaves * 64), 0, s, part, chunks, F, C, sums, (int64_t)B, mode,
+                     momentum_f, eps_f, momentum_g, eps_g, eps_std, rm_f, rv_f, rm_g, rv_g, coef,
+                     batch_out, reinterpret_cast<long long*>(nbt_f),
+                     reinterpret_cast<long long*>(nbt_g), nbt_d);
+  return check_launch("bn_stats_finalize");
 }
 
 extern "C" int32_t vqgnn_vq_ema_parts(int32_t B, int32_t nb, int32_t M, int32_t W) {

@@ -55,6 +55,31 @@ def bn_finalize(sums, count, F, with_grad, mode, mom_f, eps_f, mom_g, eps_g, eps
     return coef, batch
 
 
+def bn_stats_finalize(X, G, F, mode, mom_f, eps_f, mom_g, eps_g, eps_std, rm_f, rv_f,
+                      rm_g=None, rv_g=None, want_batch=False, nbt_f=None, nbt_g=None, D=0,
+                      want_sums=False):
+    """bn_stats + bn_finalize for a single process (count = B): the reduce and
+    the finalize run as one kernel.  -> (coef, batch_out or None, sums or None)."""
+    require_gpu(X, "bn_stats_finalize")
+    B = X.shape[0]
+    dev = X.device
+    with_grad = G is not None
+    L = lib()
+    ws = workspace(L.vqgnn_bn_stats_workspace(B, F), dev)
+    coef = torch.empty(4, F, dtype=torch.float32, device=dev)
+    if not with_grad:
+        coef[2:].zero_()
+    batch = torch.empty(4, F, dtype=torch.float32, device=dev) if want_batch else None
+    sums = torch.zeros(4, F, dtype=torch.float64, device=dev) if want_sums else None
+    check(L.vqgnn_bn_stats_finalize(ptr(X), _ld(X), ptr(G), _ld(G) if with_grad else 0, B, F,
+                                    int(with_grad), ptr(sums), int(mode), float(mom_f),
+                                    float(eps_f), float(mom_g), float(eps_g), float(eps_std),
+                                    ptr(rm_f), ptr(rv_f), ptr(rm_g), ptr(rv_g), ptr(coef),
+                                    ptr(batch), ptr(nbt_f), ptr(nbt_g), int(D), ptr(ws),
+                                    stream_ptr()), "bn_stats_finalize")
+    return coef, batch, sums
+
+
 def stat_shifts(stat_count: int, grad_scale: float) -> tuple[int, int]:
     """Fixed-point scale of the EMA statistic slabs (include/vqgnn.h §3)."""
     import ctypes

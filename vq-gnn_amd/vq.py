@@ -162,12 +162,15 @@ class VQBank(nn.Module):
         if training and B <= 1:
             raise ValueError("Expected more than 1 value per channel when training")
         comm = self.comm if training else None
-        if training:
-            sums = kernels.bn_stats(X, None, F)
+        if training and comm is None:      # one process: reduce + finalize fused
             count = B
-            if comm is not None:
-                comm.allreduce_(sums)
-                count = comm.global_count(B)
+            coef, _, _ = kernels.bn_stats_finalize(X, None, F, BN_TRAIN, 0.1, 1e-5, 0.0, 0.0,
+                                                   0.0, self.rm_f[sl], self.rv_f[sl],
+                                                   nbt_f=self.nbt_f[sl], D=D)
+        elif training:
+            sums = kernels.bn_stats(X, None, F)
+            comm.allreduce_(sums)
+            count = comm.global_count(B)
             coef, _ = kernels.bn_finalize(sums, count, F, False, BN_TRAIN, 0.1, 1e-5, 0.0, 0.0,
                                           0.0, self.rm_f[sl], self.rv_f[sl], nbt_f=self.nbt_f[sl],
                                           D=D)
@@ -212,19 +215,21 @@ class VQBank(nn.Module):
         if training and B <= 1:
             raise ValueError("Expected more than 1 value per channel when training")
         comm = self.comm if training else None
-        sums = kernels.bn_stats(X, G, F)
         count = B
-        if comm is not None:
-            comm.allreduce_(sums)
-            count = comm.global_count(B)
         mode = (BN_TRAIN_INIT if init else BN_TRAIN) if training else \
             (BN_EVAL_INIT if init else BN_EVAL)
-        coef, batch = kernels.bn_finalize(sums, count, F, True, mode, 0.1, 1e-5, self.momentum,
-                                          self.epsilon, self.epsilon, self.rm_f[sl],
-                                          self.rv_f[sl], self.rm_g[sl], self.rv_g[sl],
-                                          want_batch=True,
-                                          nbt_f=self.nbt_f[sl] if training else None,
-                                          nbt_g=self.nbt_g[sl] if training else None, D=D)
+        bn_args = (mode, 0.1, 1e-5, self.momentum, self.epsilon, self.epsilon, self.rm_f[sl],
+                   self.rv_f[sl], self.rm_g[sl], self.rv_g[sl])
+        bn_kw = dict(want_batch=True, nbt_f=self.nbt_f[sl] if training else None,
+                     nbt_g=self.nbt_g[sl] if training else None, D=D)
+        if comm is None and mode != BN_EVAL:   # one process: reduce + finalize fused
+            coef, batch, _ = kernels.bn_stats_finalize(X, G, F, *bn_args, **bn_kw)
+        else:
+            sums = kernels.bn_stats(X, G, F)
+            if comm is not None:
+                comm.allreduce_(sums)
+                count = comm.global_count(B)
+            coef, batch = kernels.bn_finalize(sums, count, F, True, *bn_args, **bn_kw)
         for b in range(b0, b0 + nbr):
             self.bn_inited[b] = True
         self.last_batch = batch
