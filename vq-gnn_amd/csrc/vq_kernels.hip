@@ -245,42 +245,65 @@ __global__ void bn_finalize_kernel(const double* __restrict__ sums, int64_t n, i
   }
 }
 
-// Single-process fusion of bn_stats_reduce + bn_finalize: one wave per data
-// column c in [0, C) folds its sum and sum of squares in the reduce kernel's
-// order (lane-strided chunks, then the butterfly: the same bits), then lane 0
-// runs the column's BatchNorm update.  No all-reduce can sit between the two
+// Single-process fusion of bn_stats_reduce + bn_finalize.  Block = 32 data
+// columns; lane l of every wave reads value column (l / 32 ? sum of squares :
+// sum) of data column 32*block + l % 32, so a half-wave reads 256 contiguous
+// bytes of a chunk row; wave w sums its slice of the chunks in order, the 16
+// slices are folded in order in LDS (deterministic), then one thread per data
+// column runs its BatchNorm update.  No all-reduce can sit between the two
 // here, so multi-GPU callers keep vqgnn_bn_stats + vqgnn_bn_finalize.
-__global__ void __launch_bounds__(kReduceWaves * 64)
+constexpr int kRfThreads = 1024;
+constexpr int kRfWaves = kRfThreads / 64;
+__global__ void __launch_bounds__(kRfThreads)
 bn_reduce_finalize_kernel(const double* __restrict__ part, int chunks, int F, int C,
                           double* __restrict__ sums, int64_t n, int mode, float mom_f,
                           float eps_f, float mom_g, float eps_g, float eps_std, float* rm_f,
                           float* rv_f, float* rm_g, float* rv_g, float* __restrict__ coef,
                           float* __restrict__ batch_out, long long* __restrict__ nbt_f,
                           long long* __restrict__ nbt_g, int D) {
-  const int lane = threadIdx.x & 63;
-  const int c = blockIdx.x * kReduceWaves + (threadIdx.x >> 6);   // data column in [0, C)
-  if (c >= C) return;
-  double a = 0.0, q = 0.0;
-  for (int p = lane; p < chunks; p += 64) a += part[(int64_t)p * 2 * C + c];
-  for (int p = lane; p < chunks; p += 64) q += part[(int64_t)p * 2 * C + C + c];
+  __shared__ double red[kRfWaves][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = blockIdx.x * 32 + (lane & 31);            // data column
+  const int h = lane >> 5;                                // 0: sum, 1: sum of squares
+  const int per = (chunks + kRfWaves - 1) / kRfWaves;
+  const int p0 = wave * per, p1 = min(chunks, p0 + per);
+  double a = 0.0;
+  if (c < C) {
+    // all of a slice's loads in flight before the in-order adds (the
+    // partials come from every XCD: each round trip is an L2 miss)
+    const double* col = part + (int64_t)h * C + c;
+    for (int p = p0; p < p1; p += 32) {
+      double t[32];
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    a += __shfl_xor(a, off);
-    q += __shfl_xor(q, off);
+      for (int u = 0; u < 32; ++u) t[u] = p + u < p1 ? col[(int64_t)(p + u) * 2 * C] : 0.0;
+#pragma unroll
+      for (int u = 0; u < 32; ++u)
+        if (p + u < p1) a += t[u];
+    }
   }
-  if (lane != 0) return;
+  red[wave][lane] = a;
+  __syncthreads();
+  if (threadIdx.x >= 32) return;
+  const int t = threadIdx.x;
+  if (c >= C) return;
+  double sm = red[0][t], sq = red[0][32 + t];
+#pragma unroll
+  for (int w = 1; w < kRfWaves; ++w) {
+    sm += red[w][t];
+    sq += red[w][32 + t];
+  }
   const bool g = c >= F;
   const int k = g ? c - F : c;
   if (sums) {
-    sums[(g ? 2 * F : 0) + k] = a;
-    sums[(g ? 3 * F : F) + k] = q;
+    sums[(g ? 2 * F : 0) + k] = sm;
+    sums[(g ? 3 * F : F) + k] = sq;
   }
   if (D > 0 && k % D == 0) {   // BatchNorm1d.num_batches_tracked += 1 (train)
     long long* nbt = g ? nbt_g : nbt_f;
     if (nbt) nbt[k / D] += 1;
   }
   const int o = g ? 2 * F : 0;
-  bn_column(a, q, true, n, mode, g ? mom_g : mom_f, g ? eps_g : eps_f, eps_std,
+  bn_column(sm, sq, true, n, mode, g ? mom_g : mom_f, g ? eps_g : eps_f, eps_std,
             (g ? rm_g : rm_f) + k, (g ? rv_g : rv_f) + k, coef + o + k, coef + o + F + k,
             batch_out ? batch_out + o + k : nullptr, batch_out ? batch_out + o + F + k : nullptr);
 }
@@ -916,8 +939,11 @@ __global__ void vq_ema_reduce_kernel(const long long* __restrict__ parts, int np
 // ---------------------------------------------------------------------------
 // 4. EMA finalize: one workgroup per branch.        vq.py:177-200, :242-277
 // ---------------------------------------------------------------------------
-constexpr int kFinThreads = 256;
+constexpr int kFinThreads = 1024;
+constexpr int kFinWaves = kFinThreads / 64;
 
+// One workgroup per branch; cs lives in LDS (dynamic, M floats) between the
+// phases, so the only global traffic is the slab, the state and the outputs.
 __global__ void __launch_bounds__(kFinThreads)
 vq_ema_finalize_kernel(long long* __restrict__ stats, int nparts, int64_t part_stride,
                        int zero_after, int shift_f, int shift_g, int M, int D, int W, int ldw,
@@ -928,10 +954,12 @@ vq_ema_finalize_kernel(long long* __restrict__ stats, int nparts, int64_t part_s
                        const float* __restrict__ rm_f, const float* __restrict__ rv_f,
                        const float* __restrict__ rm_g, const float* __restrict__ rv_g,
                        int* __restrict__ bad_init) {
-  __shared__ float red[kFinThreads];
+  extern __shared__ float cs_s[];            // [M]
+  __shared__ float wred[kFinWaves];
   __shared__ int bad;
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
   long long* st = stats + (int64_t)b * M * (W + 1);
   // statistic = integer sum of the per-part fixed-point slabs, decoded once:
   // round(exact sum * 2^-shift) to fp32 (count column: shift 0).  Every entry
@@ -955,29 +983,33 @@ vq_ema_finalize_kernel(long long* __restrict__ stats, int nparts, int64_t part_s
 
   // cs = cs*decay + (1-decay)*counts  (vq.py:177-178; fp32 tensor ops)
   for (int m = tid; m < M; m += kFinThreads)
-    cs[m] = __fadd_rn(__fmul_rn(cs[m], decay), __fmul_rn(one_m_decay, stat((int64_t)m * (W + 1), 0)));
+    cs_s[m] = __fadd_rn(__fmul_rn(cs[m], decay), __fmul_rn(one_m_decay, stat((int64_t)m * (W + 1), 0)));
   __syncthreads();
 
   if (laplace) {  // vq.py:182-186
     // n = torch.sum(cs): per-thread sequential partials over a strided slice,
-    // then a fixed tree — deterministic (ATen's CPU cascade order differs by ulps)
-    float s = 0.f;
-    for (int m = tid; m < M; m += kFinThreads) s = __fadd_rn(s, cs[m]);
-    red[tid] = s;
+    // a fixed butterfly per wave, then the waves in order — deterministic
+    // (ATen's CPU cascade order differs by ulps)
+    float sum = 0.f;
+    for (int m = tid; m < M; m += kFinThreads) sum = __fadd_rn(sum, cs_s[m]);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) sum = __fadd_rn(sum, __shfl_xor(sum, off));
+    if (lane == 0) wred[wave] = sum;
     __syncthreads();
-    for (int w = kFinThreads / 2; w > 0; w >>= 1) {
-      if (tid < w) red[tid] = __fadd_rn(red[tid], red[tid + w]);
-      __syncthreads();
-    }
-    const float n = red[0];
+    float n = wred[0];
+#pragma unroll
+    for (int w = 1; w < kFinWaves; ++w) n = __fadd_rn(n, wred[w]);
     const float den = __fadd_rn(n, (float)((double)M * 1e-5));  // n + M*1e-5 (python float -> f32)
     for (int m = tid; m < M; m += kFinThreads)
-      cs[m] = __fmul_rn(__fdiv_rn(__fadd_rn(cs[m], 1e-5f), den), n);
+      cs_s[m] = __fmul_rn(__fdiv_rn(__fadd_rn(cs_s[m], 1e-5f), den), n);
     __syncthreads();
   }
 
-  for (int m = tid; m < M; m += kFinThreads)
-    if (cs[m] == 0.f) bad = 1;  // vq.py:188 count_nonzero(cs) != M
+  for (int m = tid; m < M; m += kFinThreads) {
+    const float c = cs_s[m];
+    cs[m] = c;
+    if (c == 0.f) bad = 1;  // vq.py:188 count_nonzero(cs) != M
+  }
   __syncthreads();
   if (bad) {  // reference raises before touching ema_w / embedding
     if (tid == 0) atomicOr(bad_init, 1);
@@ -996,7 +1028,7 @@ vq_ema_finalize_kernel(long long* __restrict__ stats, int nparts, int64_t part_s
     const float dw = stat((int64_t)m * (W + 1) + 1 + k, k < D ? shift_f : shift_g);
     const float w = __fadd_rn(__fmul_rn(ew[o], decay), __fmul_rn(one_m_decay, dw));
     ew[o] = w;
-    const float ev = __fdiv_rn(w, cs[m]);
+    const float ev = __fdiv_rn(w, cs_s[m]);
     e[o] = ev;
     float out;
     if (k < D) {  // vq.py:198-200 / :267-272 feature half: emb*sqrt(rv+1e-5)+rm
@@ -1100,8 +1132,7 @@ extern "C" int vqgnn_bn_stats_finalize(const float* X, int64_t ldx, const float*
     hipLaunchKernelGGL(bn_stats_partial_scalar_kernel, dim3(chunks), dim3(kStatsThreads), 0, s,
                        X, ldx, G, ldg, B, F, C, rpc, part);
   }
-  hipLaunchKernelGGL(bn_reduce_finalize_kernel, dim3((C + kReduceWaves - 1) / kReduceWaves),
-                     dim3(kReduceWaves * 64), 0, s, part, chunks, F, C, sums, (int64_t)B, mode,
+  hipLaunchKernelGGL(bn_reduce_finalize_kernel, dim3((C + 31) / 32), dim3(kRfThreads), 0, s, part, chunks, F, C, sums, (int64_t)B, mode,
                      momentum_f, eps_f, momentum_g, eps_g, eps_std, rm_f, rv_f, rm_g, rv_g, coef,
                      batch_out, reinterpret_cast<long long*>(nbt_f),
                      reinterpret_cast<long long*>(nbt_g), nbt_d);
@@ -1250,8 +1281,17 @@ extern "C" int vqgnn_vq_ema_finalize(int64_t* ema_parts, int32_t nparts, int32_t
   VQGNN_REQUIRE(W == D || (W == 2 * D && rm_g && rv_g), "ema_finalize: W must be D or 2D");
   VQGNN_REQUIRE(nb > 0 && M > 0 && ldw >= W && nparts > 0, "ema_finalize: bad shape");
   VQGNN_REQUIRE(stat_count > 0, "ema_finalize: stat_count must be > 0");
+  VQGNN_REQUIRE((size_t)M * 4 <= 136 * 1024, "ema_finalize: M=%d too large for the LDS", M);
   const StatShift sh = stat_shift(stat_count, grad_scale);
-  hipLaunchKernelGGL(vq_ema_finalize_kernel, dim3(nb), dim3(kFinThreads), 0, as_stream(stream),
+  const size_t lds = (size_t)M * sizeof(float);
+  if (lds > 48 * 1024) {
+    static std::once_flag once;
+    std::call_once(once, [] {
+      (void)hipFuncSetAttribute((const void*)vq_ema_finalize_kernel,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 136 * 1024);
+    });
+  }
+  hipLaunchKernelGGL(vq_ema_finalize_kernel, dim3(nb), dim3(kFinThreads), lds, as_stream(stream),
                      reinterpret_cast<long long*>(ema_parts), nparts,
                      (int64_t)nb * M * (W + 1), zero_after, sh.f, sh.g, M, D, W, ldw, decay,
                      laplace,
