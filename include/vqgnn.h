@@ -313,6 +313,46 @@ int vqgnn_coo_to_csr(const int64_t* row, const int64_t* col, const float* val, i
                      int64_t n_rows, int64_t n_cols, int32_t* out_rowptr, int32_t* out_col,
                      float* out_val, int64_t* status, void* workspace, vqgnn_stream_t stream);
 
+/* ------------------------------------------------------------------------ *
+ * 10. Full-graph preprocessing.  Graph CSR as in §9:
+ *     rowptr int64 [N+1], col int32 (sorted within rows), val fp32 or NULL
+ *     (no values: every entry 1).
+ *   vqgnn_norm_adj: norm_adj (utils/misc.py:14-34).  GCN / GAT: set_diag()
+ *     (the diagonal replaced by, or inserted as, 1), deg = sequential row
+ *     sum, GCN: v = (deg^-1/2[row] * v) * deg^-1/2[col] (ATen pow(-0.5) =
+ *     1/sqrt), SAGE / GAT: v = deg^-1[row] * v; inf -> 0.  Output capacity
+ *     nnz + N (GCN, GAT) or nnz (SAGE); out_rowptr[N] = the output nnz.
+ *   vqgnn_to_symmetric: SparseTensor.to_symmetric() (misc.py:190, :211): A
+ *     and A^T merged, repeated (row, col) summed (val NULL: pattern, 1).
+ *     Capacity 2*nnz; out_nnz (device int64) = the output nnz.
+ *   vqgnn_csr_permute: SparseTensor.permute(perm) (misc.py:113-130): new node
+ *     i = old node perm[i]; rows sorted by the new columns.  status (device
+ *     int64) = 1 if perm holds an index outside [0, N).
+ *   vqgnn_partition: the METIS substitute for metis() (misc.py:93-111; METIS
+ *     is absent): connected components by min-label propagation, a BFS from
+ *     each component's smallest node, nodes ordered by (component, level,
+ *     id) -> perm [N]; ptr [num_parts+1] = equal contiguous bands.  Host-
+ *     synchronous (one readback per propagation / BFS step); iterations
+ *     (host, may be NULL) = the number of steps.
+ * ------------------------------------------------------------------------ */
+enum vqgnn_conv_type { VQGNN_CONV_GCN = 0, VQGNN_CONV_SAGE = 1, VQGNN_CONV_GAT = 2 };
+size_t vqgnn_norm_adj_workspace(int64_t N);
+int vqgnn_norm_adj(const int64_t* rowptr, const int32_t* col, const float* val, int64_t N,
+                   int32_t conv_type, int64_t* out_rowptr, int32_t* out_col, float* out_val,
+                   void* workspace, vqgnn_stream_t stream);
+size_t vqgnn_to_symmetric_workspace(int64_t N, int64_t nnz);
+int vqgnn_to_symmetric(const int64_t* rowptr, const int32_t* col, const float* val, int64_t N,
+                       int64_t nnz, int64_t* out_rowptr, int32_t* out_col, float* out_val,
+                       int64_t* out_nnz, void* workspace, vqgnn_stream_t stream);
+size_t vqgnn_csr_permute_workspace(int64_t N, int64_t nnz);
+int vqgnn_csr_permute(const int64_t* rowptr, const int32_t* col, const float* val, int64_t N,
+                      int64_t nnz, const int64_t* perm, int64_t* out_rowptr, int32_t* out_col,
+                      float* out_val, int64_t* status, void* workspace, vqgnn_stream_t stream);
+size_t vqgnn_partition_workspace(int64_t N);
+int vqgnn_partition(const int64_t* rowptr, const int32_t* col, int64_t N, int32_t num_parts,
+                    int64_t* perm, int64_t* ptr, int32_t* iterations, void* workspace,
+                    vqgnn_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -90,6 +90,20 @@ SIGNATURES = {
     "vqgnn_khop_edges": (ctypes.c_int, [_c_void_p, _c_void_p, _c_void_p, _i64, _c_void_p,
                                         _c_void_p, _i64, _i64, _i32, _i32, _i32, _c_void_p, _i64,
                                         _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p]),
+    # §10 full-graph preprocessing
+    "vqgnn_norm_adj_workspace": (_size, [_i64]),
+    "vqgnn_norm_adj": (ctypes.c_int, [_c_void_p, _c_void_p, _c_void_p, _i64, _i32, _c_void_p,
+                                      _c_void_p, _c_void_p, _c_void_p, _c_void_p]),
+    "vqgnn_to_symmetric_workspace": (_size, [_i64, _i64]),
+    "vqgnn_to_symmetric": (ctypes.c_int, [_c_void_p, _c_void_p, _c_void_p, _i64, _i64, _c_void_p,
+                                          _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p]),
+    "vqgnn_csr_permute_workspace": (_size, [_i64, _i64]),
+    "vqgnn_csr_permute": (ctypes.c_int, [_c_void_p, _c_void_p, _c_void_p, _i64, _i64, _c_void_p,
+                                         _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
+                                         _c_void_p]),
+    "vqgnn_partition_workspace": (_size, [_i64]),
+    "vqgnn_partition": (ctypes.c_int, [_c_void_p, _c_void_p, _i64, _i32, _c_void_p, _c_void_p,
+                                       _c_void_p, _c_void_p, _c_void_p]),
     "vqgnn_coo_to_csr_workspace": (_size, [_i64, _i64, _i64]),
     "vqgnn_coo_to_csr": (ctypes.c_int, [_c_void_p, _c_void_p, _c_void_p, _i64, _i64, _i64,
                                         _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,

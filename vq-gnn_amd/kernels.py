@@ -380,3 +380,84 @@ def coo_to_csr(row, col, val, n_rows, n_cols):
     if int(status.item()) & KHOP_OUT_OF_RANGE:
         raise IndexError("coo_to_csr: index out of range")
     return out_rowptr, out_col[:nnz], out_val[:nnz]
+
+
+# ---- full-graph preprocessing (include/vqgnn.h §10) ----
+
+CONV_TYPES = {"GCN": 0, "SAGE": 1, "GAT": 2}
+
+
+def norm_adj(rowptr, col, val, N, conv_type):
+    """-> (rowptr int64 [N+1], col int32, val fp32) of the normalised graph."""
+    require_gpu(rowptr, "norm_adj")
+    if conv_type not in CONV_TYPES:
+        raise ValueError('GNN conv type not supported')           # misc.py:34
+    dev = rowptr.device
+    nnz = int(col.numel())
+    cap = nnz + (N if conv_type != "SAGE" else 0)
+    out_rowptr = torch.empty(N + 1, dtype=torch.int64, device=dev)
+    out_col = torch.empty(max(cap, 1), dtype=torch.int32, device=dev)
+    out_val = torch.empty(max(cap, 1), dtype=torch.float32, device=dev)
+    L = lib()
+    ws = workspace(L.vqgnn_norm_adj_workspace(N), dev)
+    check(L.vqgnn_norm_adj(ptr(rowptr), ptr(col), ptr(val), int(N), CONV_TYPES[conv_type],
+                           ptr(out_rowptr), ptr(out_col), ptr(out_val), ptr(ws), stream_ptr()),
+          "norm_adj")
+    n = int(out_rowptr[N].item()) if N else 0
+    return out_rowptr, out_col[:n], out_val[:n]
+
+
+def to_symmetric(rowptr, col, val, N):
+    """SparseTensor.to_symmetric(): A and A^T merged, repeats summed (val None:
+    pattern with unit values).  -> (rowptr int64, col int32, val fp32)."""
+    require_gpu(rowptr, "to_symmetric")
+    dev = rowptr.device
+    nnz = int(col.numel())
+    out_rowptr = torch.empty(N + 1, dtype=torch.int64, device=dev)
+    out_col = torch.empty(max(2 * nnz, 1), dtype=torch.int32, device=dev)
+    out_val = torch.empty(max(2 * nnz, 1), dtype=torch.float32, device=dev)
+    out_nnz = torch.zeros(1, dtype=torch.int64, device=dev)
+    L = lib()
+    ws = workspace(L.vqgnn_to_symmetric_workspace(N, nnz), dev)
+    check(L.vqgnn_to_symmetric(ptr(rowptr), ptr(col), ptr(val), int(N), nnz, ptr(out_rowptr),
+                               ptr(out_col), ptr(out_val), ptr(out_nnz), ptr(ws), stream_ptr()),
+          "to_symmetric")
+    n = int(out_nnz.item())
+    return out_rowptr, out_col[:n], out_val[:n]
+
+
+def csr_permute(rowptr, col, val, N, perm):
+    """SparseTensor.permute(perm): node i of the result = node perm[i]."""
+    require_gpu(rowptr, "csr_permute")
+    dev = rowptr.device
+    nnz = int(col.numel())
+    perm = perm.to(device=dev, dtype=torch.int64).contiguous()
+    if perm.numel() != N:
+        raise ValueError("perm must have N entries")
+    out_rowptr = torch.empty(N + 1, dtype=torch.int64, device=dev)
+    out_col = torch.empty(max(nnz, 1), dtype=torch.int32, device=dev)
+    out_val = torch.empty(max(nnz, 1), dtype=torch.float32, device=dev)
+    status = torch.zeros(1, dtype=torch.int64, device=dev)
+    L = lib()
+    ws = workspace(L.vqgnn_csr_permute_workspace(N, nnz), dev)
+    check(L.vqgnn_csr_permute(ptr(rowptr), ptr(col), ptr(val), int(N), nnz, ptr(perm),
+                              ptr(out_rowptr), ptr(out_col), ptr(out_val), ptr(status), ptr(ws),
+                              stream_ptr()), "csr_permute")
+    if int(status.item()):
+        raise IndexError("permute: index out of range")
+    return out_rowptr, out_col[:nnz], out_val[:nnz]
+
+
+def partition(rowptr, col, N, num_parts):
+    """METIS substitute: -> (perm int64 [N], ptr int64 [num_parts+1], steps)."""
+    require_gpu(rowptr, "partition")
+    import ctypes
+    dev = rowptr.device
+    perm = torch.empty(max(N, 1), dtype=torch.int64, device=dev)
+    ptr_ = torch.empty(num_parts + 1, dtype=torch.int64, device=dev)
+    steps = ctypes.c_int32(0)
+    L = lib()
+    ws = workspace(L.vqgnn_partition_workspace(N), dev)
+    check(L.vqgnn_partition(ptr(rowptr), ptr(col), int(N), int(num_parts), ptr(perm), ptr(ptr_),
+                            ctypes.addressof(steps), ptr(ws), stream_ptr()), "partition")
+    return perm[:N], ptr_, int(steps.value)

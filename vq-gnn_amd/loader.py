@@ -35,6 +35,7 @@ class DeviceGraph:
         self.rowptr = torch.as_tensor(rowptr).to(device=dev, dtype=torch.int64).contiguous()
         self.col = torch.as_tensor(col).to(device=dev, dtype=torch.int32).contiguous()
         n_e = int(self.col.numel())
+        self.has_value = value is not None       # torch_sparse adj_t without values
         if value is None:
             value = torch.ones(n_e, dtype=torch.float32)
         self.value = torch.as_tensor(value).to(device=dev, dtype=torch.float32).contiguous()
@@ -57,6 +58,16 @@ class DeviceGraph:
     @property
     def device(self):
         return self.rowptr.device
+
+    # torch_sparse-like surface (data.adj_t)
+    def csr(self):
+        return self.rowptr, self.col, self.value
+
+    def sparse_sizes(self):
+        return (self.N, self.N)
+
+    def nnz(self):
+        return int(self.col.numel())
 
     def _run(self, node_idx, num_hops, train_flag, order):
         if isinstance(node_idx, (int, list, tuple)):          # dataloader.py:108-109
