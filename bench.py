@@ -43,6 +43,10 @@ def parse():
     # kernel events inside the timed region (the roofline kernel's launches);
     # off only to measure what they cost
     p.add_argument("--no-kernel-events", action="store_true")
+    # aggregation source for the out-of-batch rows: "codes" = code records +
+    # LDS-staged codebooks (x_first_order never materialised) where the
+    # codebook fits in LDS; "rows" = gathered x_first_order rows
+    p.add_argument("--spmm-source", default="auto", choices=["auto", "codes", "rows"])
     return p.parse_args()
 
 
@@ -107,6 +111,9 @@ def main():
     # per-batch adjacency preparation (like the reference's SparseTensor build
     # in the data loader): the SpMM chunk plan, computed once per batch
     spmm_plan = adj.plan(F)
+    fused = gat is None and args.spmm_source != "rows" and kernels.spmm_codes_supported(F, nb, M, D)
+    if args.spmm_source == "codes" and not fused:
+        raise SystemExit(f"--spmm-source codes: F={F} M={M} does not fit the LDS codebook path")
     # codebook state = one feature_update warm pass
     bank.feature_update(Xd, 0, nb, True, codes=codes, batch_idx=bidx)
     torch.cuda.synchronize()
@@ -123,10 +130,17 @@ def main():
             bank.feature_update(Xd, 0, nb, True, codes=codes, batch_idx=bidx)
         if record:
             e[1].record()
-        x_first, _ = kernels.gather_codewords(subset, B, codes, bank.emb_out, D)
+        if fused:               # out-of-batch code records (x_first_order stays virtual)
+            _, lcodes = kernels.gather_codewords(subset, B, codes, bank.emb_out, D,
+                                                 want_x=False, want_codes=True)
+        else:
+            x_first, _ = kernels.gather_codewords(subset, B, codes, bank.emb_out, D)
         if record:
             e[2].record()
-        if gat is not None:     # attention aggregation (alpha, coef, SpMM, normalise)
+        if fused:
+            kernels.spmm_codes(adj.rowptr, adj.col, adj.value, n, nnz, Xd, F, lcodes,
+                               bank.emb_out, D, B, plan=spmm_plan)
+        elif gat is not None:     # attention aggregation (alpha, coef, SpMM, normalise)
             with torch.no_grad():
                 gat.fused_forward(Xd, adj, x_first, B)
         else:
@@ -193,7 +207,13 @@ def main():
     #  vq_assign_kernel: 2*B*M*W flops per branch (the distance contraction);
     #  SpMM (spmm_wave_kernel + spmm_fixup_kernel): rowptr + (col, val) + every
     #  input row once (x and x_first_order) + the output rows.
-    spmm_bytes = 4 * (n + 1) + 8 * nnz + 4 * n * F + 4 * n * F
+    #  fused (spmm_codes_kernel): X rows once, the B' code records and the
+    #  codebooks' feature halves instead of x_first_order.
+    if fused:
+        spmm_bytes = 4 * (n + 1) + 8 * nnz + 4 * B * F + 2 * (n - B) * nb + 4 * nb * M * D \
+            + 4 * n * F
+    else:
+        spmm_bytes = 4 * (n + 1) + 8 * nnz + 4 * n * F + 4 * n * F
     vq_flops = 2.0 * B * M * W * nb
     pmc = {}
     if os.path.exists(args.pmc_json):
@@ -204,11 +224,12 @@ def main():
         except (OSError, ValueError):
             pmc = {}
     agg_name = ("gat aggregation (alpha+coef+spmm+normalize)" if gat is not None
+                else "spmm_codes_kernel+spmm_fixup_kernel" if fused
                 else "spmm_wave_kernel+spmm_fixup_kernel")
     rl_spmm = dict(kernel=agg_name, bound="hbm",
                    achieved=spmm_bytes / (spmm_ms * 1e-3) / 1e9, peak=8000.0, unit="GB/s",
                    bytes_per_launch=spmm_bytes, ms_per_launch=spmm_ms,
-                   traffic=pmc.get("spmm_wave_kernel"))
+                   traffic=pmc.get("spmm_codes_kernel" if fused else "spmm_wave_kernel"))
     rl_spmm["frac"] = rl_spmm["achieved"] / rl_spmm["peak"]
     rl_vq = dict(kernel="vq_assign_kernel", bound="mfma",
                  achieved=vq_flops / (assign_ms * 1e-3) / 1e12, peak=157.3, unit="TFLOP/s",
@@ -238,7 +259,8 @@ def main():
             ms_per_step=ms_step, higher_is_better=True, scaling="weak", vs_baseline=None,
             dtype="f32", data="synthetic (seeded arxiv-shaped graph, random features)",
             config=dict(workload=f"{args.config}: one layer step (VQ {args.semantics} + EMA for "
-                                 f"{nb} branches, codeword gather, "
+                                 f"{nb} branches, "
+                                 f"{'out-of-batch code gather' if fused else 'codeword gather'}, "
                                  f"{'GAT attention aggregation' if gat is not None else 'SpMM'})",
                         B=B, B_prime=n - B, nnz=nnz, F=F, M=M, D=D, W=W,
                         parallelism=f"dp{world}"),

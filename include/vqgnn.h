@@ -212,6 +212,25 @@ int64_t vqgnn_spmm_plan_size(int64_t nnz, int32_t F);
 int vqgnn_spmm_plan(const int32_t* rowptr, int32_t n_rows, int64_t nnz, int32_t F,
                     int32_t* plan, vqgnn_stream_t stream);
 
+/* 6c. Code-source SpMM: vqgnn_spmm with xin[j] = X[j] for j < B and, for
+ *     j >= B, xin[j][b*D + k] = emb[b*emb_bstride + code*ldw + col_offset + k]
+ *     with code = lcodes[(j - B)*ldlc + b] — x_first_order (models.py:168-174)
+ *     is never materialised: the codebooks' feature halves are staged in LDS
+ *     and an out-of-batch edge reads its 2*nb-byte code record instead of a
+ *     4*F-byte row.  Same summation order and bits as vqgnn_spmm.
+ *     Applies when vqgnn_spmm_codes_supported(F, nb, M, D) (F in {64, 128,
+ *     256}, nb*D == F, nb*M*D <= 32768 floats); else VQGNN_ERR_UNSUPPORTED.
+ *     lcodes: vqgnn_gather_codewords(..., xt = NULL, lcodes); workspace and
+ *     plan as vqgnn_spmm.                                                    */
+int vqgnn_spmm_codes_supported(int32_t F, int32_t nb, int32_t M, int32_t D);
+int vqgnn_spmm_codes(const int32_t* rowptr, const int32_t* col, const float* val,
+                     int32_t n_rows, int32_t n_cols, int64_t nnz, int32_t B,
+                     const float* X, int64_t ldx, const int16_t* lcodes, int64_t ldlc,
+                     int32_t nb, const float* emb, int32_t M, int32_t D, int32_t ldw,
+                     int64_t emb_bstride, int32_t col_offset, int32_t F, float* out,
+                     int64_t ldo, const int32_t* plan, void* workspace,
+                     vqgnn_stream_t stream);
+
 /* 7. CSR transpose (structure + values) for the backward product
  *    dX = A^T dOut (torch_sparse matmul autograd, convs.py:95).  Output CSR of
  *    A^T with rows sorted by column of A; within a row, entries ordered by

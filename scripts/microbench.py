@@ -93,10 +93,49 @@ def bench_spmm():
         print(f"probe {name:22s} {t:8.1f} us  {b.nnz * 512 / t / 1e6:6.2f} TB/s gathered")
 
 
+def bench_codes():
+    """Code-source SpMM against the two-source SpMM, plus structure probes:
+    all-X (B = n) isolates the persistent/occupancy structure, all-codes
+    (B = 0) the LDS codeword path."""
+    cfg = CONFIGS["arxiv_gcn"]
+    g, _, b = make_batch(cfg)
+    bidx, subset, adj = batch_to_device(b, dev)
+    F, D, M = 128, 4, 256
+    nb = F // D
+    X = torch.randn(b.B, F, device=dev)
+    Xn = torch.randn(b.n, F, device=dev)
+    emb_out = torch.randn(nb, M, 2 * D, device=dev)
+    codes = torch.randint(0, M, (g.N, nb), dtype=torch.int16, device=dev)
+    xt, lc = kernels.gather_codewords(subset, b.B, codes, emb_out, D, want_codes=True)
+    lc_all = torch.randint(0, M, (b.n, nb), dtype=torch.int16, device=dev)
+    pl = adj.plan(F)
+    res = {}
+    res["rows two-source"] = timeit(lambda: kernels.spmm(adj.rowptr, adj.col, adj.value, b.n,
+                                                         b.nnz, X, F, X2=xt, B=b.B, plan=pl))
+    res["rows all-X"] = timeit(lambda: kernels.spmm(adj.rowptr, adj.col, adj.value, b.n, b.nnz,
+                                                    Xn, F, plan=pl))
+    res["codes fused"] = timeit(lambda: kernels.spmm_codes(adj.rowptr, adj.col, adj.value, b.n,
+                                                           b.nnz, X, F, lc, emb_out, D, b.B,
+                                                           plan=pl))
+    res["codes all-X (B=n)"] = timeit(lambda: kernels.spmm_codes(
+        adj.rowptr, adj.col, adj.value, b.n, b.nnz, Xn, F, lc[:0], emb_out, D, b.n, plan=pl))
+    res["codes all-codes (B=0)"] = timeit(lambda: kernels.spmm_codes(
+        adj.rowptr, adj.col, adj.value, b.n, b.nnz, X[:0], F, lc_all, emb_out, D, 0, plan=pl))
+    for k, v in res.items():
+        print(f"{k:24s} {v:8.1f} us", flush=True)
+    # parity of the variants against the two-source result (bit-identical)
+    ref = kernels.spmm(adj.rowptr, adj.col, adj.value, b.n, b.nnz, X, F, X2=xt, B=b.B, plan=pl)
+    fz = kernels.spmm_codes(adj.rowptr, adj.col, adj.value, b.n, b.nnz, X, F, lc, emb_out, D,
+                            b.B, plan=pl)
+    print("codes == two-source:", bool(torch.equal(ref, fz)), flush=True)
+
+
 if __name__ == "__main__":
     what = sys.argv[1] if len(sys.argv) > 1 else "all"
     if what in ("vq", "all"):
         bench_vq()
+    if what == "codes":
+        bench_codes()
     if what in ("spmm", "all"):
         for s_ in os.environ.get("SPMM_S_LIST", "").split(","):
             pass

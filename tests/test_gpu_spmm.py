@@ -199,3 +199,93 @@ def test_arxiv_shaped_properties():
     torch.testing.assert_close(oxy, 2 * ox + oy, rtol=1e-4, atol=1e-4)
     ref = conv_ref.spmm_fp64(b.rowptr, b.col, b.val, x.cpu().numpy())
     assert np.abs(ox.cpu().numpy() - ref).max() < 1e-4
+
+
+@pytest.mark.parametrize("F,D,M", [(128, 4, 256), (128, 4, 50), (64, 4, 512), (256, 4, 128),
+                                   (64, 2, 200)])
+def test_spmm_codes_vs_two_source(F, D, M):
+    """Code-source SpMM (x_first_order never materialised, codebooks in LDS):
+    bit-identical to the two-source SpMM on the gathered x_first_order and
+    to the spmm_sum loop on rows of at most L edges."""
+    nb = F // D
+    assert kernels.spmm_codes_supported(F, nb, M, D)
+    g = graph.synthetic_graph(6000, 10, 40000, seed=F + M)
+    rp, cl, vl = graph.norm_adj(g, "GCN")
+    b = graph.k_hop_batch(rp, cl, vl, g.N, graph.cluster_batch(g, [1, 4, 6, 7]))
+    rng = np.random.default_rng(M)
+    X = rng.standard_normal((b.B, F)).astype(np.float32)
+    emb_out = rng.standard_normal((nb, M, 2 * D)).astype(np.float32)
+    codes = rng.integers(0, M, size=(g.N, nb)).astype(np.int16)
+    bidx, subset, adj = graph.batch_to_device(b, DEV)
+    codes_d = torch.from_numpy(codes).to(DEV)
+    emb_d = torch.from_numpy(emb_out).to(DEV)
+    xd = torch.from_numpy(X).to(DEV)
+    xt, lcodes = kernels.gather_codewords(subset, b.B, codes_d, emb_d, D, want_codes=True)
+    two = kernels.spmm(adj.rowptr, adj.col, adj.value, b.n, b.nnz, xd, F, X2=xt, B=b.B)
+    plan = adj.plan(F)
+    fused = kernels.spmm_codes(adj.rowptr, adj.col, adj.value, b.n, b.nnz, xd, F, lcodes, emb_d,
+                               D, b.B, plan=plan)
+    assert torch.equal(fused, two)
+    nop = kernels.spmm_codes(adj.rowptr, adj.col, adj.value, b.n, b.nnz, xd, F, lcodes, emb_d,
+                             D, b.B)
+    assert torch.equal(nop, two)
+    xin = conv_ref.gather_input(X, b.subset, b.B, codes, emb_out, D).numpy()
+    ref = conv_ref.spmm_seq(b.rowptr, b.col, b.val, xin)
+    inside = np.diff(b.rowptr) <= 128
+    assert np.array_equal(fused.cpu().numpy()[inside], ref[inside])
+    np.testing.assert_allclose(fused.cpu().numpy(), ref, rtol=1e-5, atol=1e-6)
+    # the grad halves (grad_first_order source) through col_offset
+    g2 = kernels.spmm_codes(adj.rowptr, adj.col, adj.value, b.n, b.nnz, xd, F, lcodes, emb_d,
+                            D, b.B, plan=plan, col_offset=D)
+    gt, _ = kernels.gather_codewords(subset, b.B, codes_d, emb_d, D, col_offset=D)
+    assert torch.equal(g2, kernels.spmm(adj.rowptr, adj.col, adj.value, b.n, b.nnz, xd, F,
+                                        X2=gt, B=b.B))
+
+
+def test_spmm_codes_unsorted_rows_hubs_and_edges():
+    """Rows whose columns alternate between X and code sources (not CSR
+    sorted), rows longer than L (carries), empty rows, and B = n_cols (no
+    code rows) / B = 0 (codes only)."""
+    rng = np.random.default_rng(11)
+    F, D, M = 128, 4, 256
+    nb = F // D
+    n_rows, n_cols, B = 2500, 3000, 1700
+    rowptr, col, val = _random_csr(n_rows, n_cols, 40, rng, hub_rows=(3, 1200), hub_deg=2900)
+    # shuffle the columns inside each row: X and code runs interleave
+    for i in range(n_rows):
+        s, e = rowptr[i], rowptr[i + 1]
+        col[s:e] = rng.permutation(col[s:e])
+    X = rng.standard_normal((B, F)).astype(np.float32)
+    emb_out = rng.standard_normal((nb, M, 2 * D)).astype(np.float32)
+    lc = rng.integers(0, M, size=(n_cols - B, nb)).astype(np.int16)
+    a = _dev_csr(rowptr, col, val, n_rows, n_cols)
+    xd = torch.from_numpy(X).to(DEV)
+    emb_d = torch.from_numpy(emb_out).to(DEV)
+    lcd = torch.from_numpy(lc).to(DEV)
+    out = kernels.spmm_codes(a.rowptr, a.col, a.value, n_rows, a.nnz(), xd, F, lcd, emb_d, D, B)
+    xin = np.concatenate([X, emb_out[np.arange(nb)[None, :], lc.astype(np.int64), :D]
+                          .reshape(n_cols - B, F)])
+    ref = conv_ref.spmm_seq(rowptr, col, val, xin)
+    inside = np.diff(rowptr) <= 128
+    assert np.array_equal(out.cpu().numpy()[inside], ref[inside])
+    ref64 = conv_ref.spmm_fp64(rowptr, col, val, xin)
+    scale = conv_ref.spmm_fp64(rowptr, col, np.abs(val), np.abs(xin)) + 1e-6
+    assert np.max(np.abs(out.cpu().numpy() - ref64) / scale) < 1e-5
+    # B = n_cols: a plain SpMM over X
+    xfull = torch.from_numpy(np.ascontiguousarray(xin)).to(DEV)
+    o2 = kernels.spmm_codes(a.rowptr, a.col, a.value, n_rows, a.nnz(), xfull, F,
+                            lcd[:0], emb_d, D, n_cols)
+    assert torch.equal(o2, kernels.spmm(a.rowptr, a.col, a.value, n_rows, a.nnz(), xfull, F))
+    # B = 0: every source is a code record
+    lc_all = torch.from_numpy(rng.integers(0, M, size=(n_cols, nb)).astype(np.int16)).to(DEV)
+    o3 = kernels.spmm_codes(a.rowptr, a.col, a.value, n_rows, a.nnz(), xd[:0], F, lc_all,
+                            emb_d, D, 0)
+    xin3 = emb_out[np.arange(nb)[None, :], lc_all.cpu().numpy().astype(np.int64), :D] \
+        .reshape(n_cols, F)
+    assert np.array_equal(o3.cpu().numpy()[inside],
+                          conv_ref.spmm_seq(rowptr, col, val, xin3)[inside])
+    # empty CSR
+    e = _dev_csr([0] * 6, [], [], 5, n_cols)
+    o4 = kernels.spmm_codes(e.rowptr, e.col, e.value, 5, 0, xd, F, lcd, emb_d, D, B)
+    assert torch.count_nonzero(o4) == 0
+    assert not kernels.spmm_codes_supported(128, 32, 1024, 4)   # 512 KiB of codebook

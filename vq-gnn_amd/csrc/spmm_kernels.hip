@@ -551,16 +551,17 @@ __device__ __forceinline__ void segment(const SpmmArgs& a, __amdgpu_buffer_rsrc_
   else wave_segment<V, U, FAR>(a, rs, win, eb, ee, lane, acc);
 }
 
-template <int V, int U, bool FAR, bool PAIR>
-__device__ __forceinline__ int wave_chunk(const SpmmArgs& a, __amdgpu_buffer_rsrc_t rs,
-                                          EdgeWindow<FAR>& win, RowWindow& rw, int chunk, int i,
-                                          int lane) {
+// Seg: seg(eb, ee, acc) sums edges [eb, ee) of the CSR into acc in CSR order
+// (the wave's edge window and sources live in the functor).  st: this lane
+// stores output columns.
+template <int V, class Seg>
+__device__ __forceinline__ int wave_chunk_rows(const SpmmArgs& a, Seg& seg, RowWindow& rw,
+                                               int chunk, int i, int lane, bool st) {
   const int e0 = chunk * a.S;
   const int e1 = min(e0 + a.S, a.nnz);
   const bool last = e1 == a.nnz;
   const int F = a.F4 * 4;
   const int ldo = (int)(a.ldo4 * 4);
-  const bool st = (!PAIR || lane < 32) && !(a.dbg & 2);    // lanes that own output columns
   int crow = -1;
   float acc[V];
   if (i > 0) {
@@ -569,7 +570,7 @@ __device__ __forceinline__ int wave_chunk(const SpmmArgs& a, __amdgpu_buffer_rsr
       const int rs0 = row_at(a, rw, i - 1, lane);
       if (ri - rs0 > a.L) {
         const int re = min(ri, e1);
-        segment<V, U, FAR, PAIR>(a, rs, win, e0, re, lane, acc);
+        seg(e0, re, acc);
         if (st) vstore<V>(a.carry + (int64_t)chunk * 2 * F + lane * V, acc);
         crow = i - 1;
       }
@@ -581,11 +582,11 @@ __device__ __forceinline__ int wave_chunk(const SpmmArgs& a, __amdgpu_buffer_rsr
     if (!(rb < e1 || last)) break;
     const int re_full = row_at(a, rw, i + 1, lane);
     if (re_full - rb <= a.L) {
-      segment<V, U, FAR, PAIR>(a, rs, win, rb, re_full, lane, acc);
+      seg(rb, re_full, acc);
       if (st) vstore<V>(a.out + (int64_t)i * ldo + lane * V, acc);
     } else {
       const int re = min(re_full, e1);
-      segment<V, U, FAR, PAIR>(a, rs, win, rb, re, lane, acc);
+      seg(rb, re, acc);
       if (re_full <= e1) {
         if (st) vstore<V>(a.out + (int64_t)i * ldo + lane * V, acc);
       } else {
@@ -598,6 +599,460 @@ __device__ __forceinline__ int wave_chunk(const SpmmArgs& a, __amdgpu_buffer_rsr
   }
   if (lane == 0) a.carry_row[chunk] = crow;
   return next >= 0 ? next : i;
+}
+
+template <int V, int U, bool FAR, bool PAIR>
+struct WaveSeg {
+  const SpmmArgs& a;
+  __amdgpu_buffer_rsrc_t rs;
+  EdgeWindow<FAR>& win;
+  int lane;
+  __device__ __forceinline__ void operator()(int eb, int ee, float (&acc)[V]) {
+    segment<V, U, FAR, PAIR>(a, rs, win, eb, ee, lane, acc);
+  }
+};
+
+template <int V, int U, bool FAR, bool PAIR>
+__device__ __forceinline__ int wave_chunk(const SpmmArgs& a, __amdgpu_buffer_rsrc_t rs,
+                                          EdgeWindow<FAR>& win, RowWindow& rw, int chunk, int i,
+                                          int lane) {
+  WaveSeg<V, U, FAR, PAIR> seg{a, rs, win, lane};
+  const bool st = (!PAIR || lane < 32) && !(a.dbg & 2);    // lanes that own output columns
+  return wave_chunk_rows<V>(a, seg, rw, chunk, i, lane, st);
+}
+
+// ---------------------------------------------------------------------------
+// Code-source SpMM: x_first_order is never materialised.  Rows j >= B of
+// x_input are concat_b codebook_b[code(j, b)][:D] (models.py:168-174), so the
+// codebooks' feature halves (nb*M*D floats, at most kCodesLdsFloats) are
+// staged once per workgroup into LDS, and an edge from an out-of-batch source
+// reads its 2*nb-byte code record (lcodes [B', nb], L2-resident) plus, per
+// lane, V columns from LDS — instead of a 4*F-byte row from x_first_order.
+// Rows, carries, CSR order and the separate mul/add are those of
+// spmm_wave_kernel (bit-identical output).  The edge window marks which of
+// its 64 edges come from codes (a ballot); a row is walked as runs of one
+// source type, each run U-unrolled like wave_segment.
+// Persistent: the LDS image allows one 16-wave workgroup per CU; the waves of
+// an XCD stride over that XCD's chunks, so at any time they work on
+// neighbouring chunks (the L2 locality of the dispatch-ordered kernel).
+// ---------------------------------------------------------------------------
+constexpr int kCodesThreads = 1024;
+constexpr int kCodesLdsFloats = 32768;   // 128 KiB of the CU's 160 KiB
+
+struct CodesSrc {
+  const int16_t* lcodes;   // [n_cols - B][ldlc]
+  uint32_t ldlcb;          // bytes per lcodes row
+  uint32_t lcspan;         // bytes of lcodes
+  const float* emb;        // feature half of codeword (b, m): emb + b*bstride + m*ldw + off
+  int64_t bstride;
+  int ldw, off, M, D, nb;
+};
+
+struct CodeWindow {
+  int wb;
+  uint32_t off;            // X row byte offset (j < B) or code-record byte offset (j >= B)
+  float w;
+  uint64_t cmask;          // bit l: edge wb + l reads codes
+};
+
+__device__ __forceinline__ void code_window_stage(const SpmmArgs& a, const CodesSrc& c,
+                                                  CodeWindow& win, int wb, int lane) {
+  win.wb = wb;
+  const int e = wb + lane;
+  const bool ok = e < a.nnz;
+  const int j = ok ? a.col[e] : 0;
+  win.w = ok ? a.val[e] : 0.f;
+  const bool code = ok && j >= a.B;
+  win.off = code ? (uint32_t)(j - a.B) * c.ldlcb : (uint32_t)j * a.ldxb;
+  const uint64_t bm = __ballot(code);
+  win.cmask = ((uint64_t)__builtin_amdgcn_readfirstlane((int)(bm >> 32)) << 32) |
+              (uint32_t)__builtin_amdgcn_readfirstlane((int)bm);
+}
+
+template <int V, int U>
+struct CodeSeg {
+  const SpmmArgs& a;
+  const CodesSrc& c;
+  __amdgpu_buffer_rsrc_t rsx;   // X
+  __amdgpu_buffer_rsrc_t rsc;   // lcodes
+  CodeWindow& win;
+  int lane;
+  uint32_t lo;                  // this lane's byte offset in an X row
+  uint32_t coff;                // this lane's byte offset in a code record
+  const float* cb;              // this lane's LDS codebook base (branch, first column)
+
+  __device__ __forceinline__ float wt(int k) const {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, win.w), k));
+  }
+  __device__ __forceinline__ void cw(unsigned code, float (&v)[V]) const {
+    const float* p = cb + code * (unsigned)c.D;
+    if constexpr (V == 1) {
+      v[0] = p[0];
+    } else if constexpr (V == 2) {
+      const float2 t = *reinterpret_cast<const float2*>(p);
+      v[0] = t.x;
+      v[1] = t.y;
+    } else {
+      const float4 t = *reinterpret_cast<const float4*>(p);
+      v[0] = t.x;
+      v[1] = t.y;
+      v[2] = t.z;
+      v[3] = t.w;
+    }
+  }
+  __device__ __forceinline__ unsigned code_at(int k) const {
+    return __builtin_amdgcn_raw_buffer_load_b16(rsc, coff, __builtin_amdgcn_readlane(win.off, k), 0);
+  }
+  // Runs are walked U edges at a time.  The short last group re-loads its
+  // last valid edge into the unused slots (no branches around the loads, so
+  // all U are in flight before the first add) and leaves its add chain early
+  // with a wave-uniform branch: a run's tail costs one memory latency, not one
+  // per edge.  (The empty asm keeps the compiler from turning the early exits
+  // into per-column selects.)
+  template <class Load>
+  __device__ __forceinline__ void run(int e, int lim, float (&acc)[V], Load&& load) {
+    for (; e + U <= lim; e += U) {
+      const int k0 = uni(e - win.wb);
+      float v[U][V];
+      float ww[U];
+      load(k0, U - 1, v, ww);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+#pragma unroll
+        for (int k = 0; k < V; ++k) acc[k] = __fadd_rn(acc[k], __fmul_rn(ww[u], v[u][k]));
+      }
+    }
+    if (e < lim) {
+      const int k0 = uni(e - win.wb);
+      const int cnt = uni(lim - e);
+      float v[U][V];
+      float ww[U];
+      load(k0, cnt - 1, v, ww);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (u >= cnt) break;
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int k = 0; k < V; ++k) acc[k] = __fadd_rn(acc[k], __fmul_rn(ww[u], v[u][k]));
+      }
+    }
+  }
+  __device__ __forceinline__ void x_run(int e, int lim, float (&acc)[V]) {
+    run(e, lim, acc, [&](int k0, int last, float (&v)[U][V], float (&ww)[U]) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int kk = k0 + min(u, last);
+        ww[u] = wt(kk);
+        buf_load<V>(rsx, lo, __builtin_amdgcn_readlane(win.off, kk), v[u]);
+      }
+    });
+  }
+  __device__ __forceinline__ void code_run(int e, int lim, float (&acc)[V]) {
+    run(e, lim, acc, [&](int k0, int last, float (&v)[U][V], float (&ww)[U]) {
+      unsigned cd[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int kk = k0 + min(u, last);
+        ww[u] = wt(kk);
+        cd[u] = code_at(kk);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) cw(cd[u], v[u]);
+    });
+  }
+  __device__ __forceinline__ void operator()(int eb, int ee, float (&acc)[V]) {
+#pragma unroll
+    for (int k = 0; k < V; ++k) acc[k] = 0.f;
+    int e = eb;
+    while (e < ee) {
+      if (e < win.wb || e >= win.wb + 64) code_window_stage(a, c, win, e, lane);
+      const int lim = uni(min(ee, win.wb + 64));
+      while (e < lim) {
+        // the run of edges with this edge's source type (CSR sorts a row's
+        // columns, so a row is one X run then one code run; any order works)
+        const int k = uni(e - win.wb);
+        const uint64_t m = win.cmask >> k;
+        const bool code = (m & 1ull) != 0;
+        const uint64_t t = code ? ~m : m;
+        const int r = uni(min(lim, e + (t ? (int)__builtin_ctzll(t) : 64)));
+        if (code) code_run(e, r, acc);
+        else x_run(e, r, acc);
+        e = r;
+      }
+    }
+  }
+};
+
+// ---------------------------------------------------------------------------
+// Flat chunk walk: the wave issues the loads of G consecutive edges at once,
+// across row boundaries, and then adds them in CSR order, closing a row (store
+// + reset) when the add reaches its end.  Rows are still summed sequentially
+// from zero in CSR order with separate mul and add (bit-identical), but up to
+// G rows are in flight per wave instead of at most U of one row, and a row's
+// tail costs no extra memory latency.  Segments (what the adds close) follow
+// wave_chunk_rows' ownership: the head piece of a long row that began in an
+// earlier chunk (carry slot 0), then the rows that start in the chunk (a row
+// longer than L cut at the chunk end: carry slot 1).
+// CODES: an edge whose source is >= B reads its code record and then its V
+// columns of the codeword from the LDS codebook (cb = this lane's base).
+// ---------------------------------------------------------------------------
+struct FlatSrc {
+  __amdgpu_buffer_rsrc_t rsx;   // X (CODES) or the X/X2 range
+  __amdgpu_buffer_rsrc_t rsc;   // lcodes (CODES)
+  uint32_t lo;                  // this lane's byte offset in an input row
+  uint32_t coff;                // this lane's byte offset in a code record
+  const float* cb;              // this lane's LDS codebook base (CODES)
+  uint32_t D;
+  uint32_t ldlcb;               // bytes per code record
+};
+
+template <bool CODES>
+__device__ __forceinline__ void flat_stage(const SpmmArgs& a, const FlatSrc& f, CodeWindow& win,
+                                           int wb, int lane) {
+  win.wb = wb;
+  const int e = wb + lane;
+  const bool ok = e < a.nnz;
+  const int j = ok ? a.col[e] : 0;
+  win.w = ok ? a.val[e] : 0.f;
+  if constexpr (CODES) {
+    const bool code = ok && j >= a.B;
+    win.off = code ? (uint32_t)(j - a.B) * f.ldlcb : (uint32_t)j * a.ldxb;
+    const uint64_t bm = __ballot(code);
+    win.cmask = ((uint64_t)__builtin_amdgcn_readfirstlane((int)(bm >> 32)) << 32) |
+                (uint32_t)__builtin_amdgcn_readfirstlane((int)bm);
+  } else {
+    win.off = j < a.B ? a.offx + (uint32_t)j * a.ldxb : a.offx2 + (uint32_t)(j - a.B) * a.ldx2b;
+    win.cmask = 0;
+  }
+}
+
+template <int V, int G, bool CODES>
+__device__ __forceinline__ void flat_chunk(const SpmmArgs& a, const FlatSrc& f, CodeWindow& win,
+                                           RowWindow& rw, int chunk, int i0, int lane) {
+  const int e0 = chunk * a.S;
+  const int e1 = min(e0 + a.S, a.nnz);
+  const bool last = e1 == a.nnz;
+  const int F = a.F4 * 4;
+  const int64_t ldo = a.ldo4 * 4;
+  const bool st = !(a.dbg & 2);
+  // rows starting in [e0, e1): [i0, ir); the last chunk also owns trailing empty rows
+  const int ir = chunk + 1 < a.nchunks
+                     ? uni(a.chunk_row ? min(a.chunk_row[chunk + 1], a.n_rows)
+                                       : lower_bound_i32(a.rowptr, a.n_rows, e1))
+                     : a.n_rows;
+  // one row window over [i0 - 1, i0 + 63): the closes below re-stage it only
+  // for chunks owning more than 62 rows (a dependent load there drains the
+  // group's loads)
+  {
+    const int lo = i0 > 0 ? i0 - 1 : 0;
+    const int hi = min(ir, lo + 63);
+    if (lo < rw.base || hi >= rw.base + 64) {
+      rw.base = lo;
+      rw.rp = a.rowptr[min(lo + lane, a.n_rows)];
+    }
+  }
+  // empty owned rows are zeroed up front, so that the add phase below closes
+  // at most one row per edge (one conditional store: the waitcnt pass keeps
+  // its per-load counts instead of draining at every edge)
+  for (int r = i0; r < ir; ++r) {
+    if (row_at(a, rw, r, lane) == row_at(a, rw, r + 1, lane) && st) {
+      float z[V];
+#pragma unroll
+      for (int k = 0; k < V; ++k) z[k] = 0.f;
+      vstore<V>(a.out + (int64_t)r * ldo + lane * V, z);
+    }
+  }
+  int crow = -1;
+  int i = i0;
+  int s_end = 0;
+  float* dptr = nullptr;   // wave-uniform destination row of the open segment
+  bool more = true;
+  bool head = false;
+  if (i0 > 0) {
+    const int ri = row_at(a, rw, i0, lane);
+    if (ri > e0) {
+      const int rs0 = row_at(a, rw, i0 - 1, lane);
+      if (ri - rs0 > a.L) {   // the piece of a long row that started before e0
+        head = true;
+        crow = i0 - 1;
+        s_end = min(ri, e1);
+        dptr = a.carry + (int64_t)chunk * 2 * F;
+      }
+    }
+  }
+  // next non-empty owned row: [start, s_end) -> dptr
+  auto next_row = [&]() -> bool {
+    while (more && i < ir) {
+      const int rb = row_at(a, rw, i, lane);
+      const int re_full = row_at(a, rw, i + 1, lane);
+      const int r = i++;
+      if (re_full == rb) continue;
+      if (re_full - rb <= a.L) {
+        s_end = re_full;
+        dptr = a.out + (int64_t)r * ldo;
+      } else {
+        s_end = min(re_full, e1);
+        if (re_full <= e1) {
+          dptr = a.out + (int64_t)r * ldo;
+        } else {
+          dptr = a.carry + ((int64_t)chunk * 2 + 1) * F;
+          more = false;
+        }
+      }
+      return true;
+    }
+    return false;
+  };
+  int E0, E;
+  if (head) {
+    E0 = e0;
+    E = s_end;
+  } else {
+    E0 = i0 < ir ? row_at(a, rw, i0, lane) : e0;
+    E = E0;
+  }
+  if (ir > i0) {
+    const int r = ir - 1;
+    const int rs = row_at(a, rw, r, lane), re = row_at(a, rw, r + 1, lane);
+    E = re - rs > a.L ? min(re, e1) : re;
+  }
+  bool live = head || next_row();
+  float acc[V];
+#pragma unroll
+  for (int k = 0; k < V; ++k) acc[k] = 0.f;
+  for (int e = E0; e < E; e += G) {
+    const int cnt = uni(min(G, E - e));
+    if (e < win.wb || e + cnt > win.wb + 64) flat_stage<CODES>(a, f, win, e, lane);
+    const int k0 = uni(e - win.wb);
+    float v[G][V];
+    float ww[G];
+#pragma unroll
+    for (int u = 0; u < G; ++u) {
+      const int k = k0 + min(u, cnt - 1);   // unused slots re-read the last edge (no add)
+      ww[u] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, win.w), k));
+      const uint32_t so = __builtin_amdgcn_readlane(win.off, k);
+      if constexpr (CODES) {
+        if ((win.cmask >> k) & 1ull) {   // the code, in v[u][0]'s register
+          v[u][0] = __builtin_bit_cast(
+              float, (unsigned)__builtin_amdgcn_raw_buffer_load_b16(f.rsc, f.coff, so, 0));
+        } else {
+          buf_load<V>(f.rsx, f.lo, so, v[u]);
+        }
+      } else {
+        buf_load<V>(f.rsx, f.lo, so, v[u]);
+      }
+    }
+    if constexpr (CODES) {
+#pragma unroll
+      for (int u = 0; u < G; ++u) {
+        if ((win.cmask >> (k0 + min(u, cnt - 1))) & 1ull) {
+          const float* p = f.cb + __builtin_bit_cast(unsigned, v[u][0]) * f.D;
+          if constexpr (V == 1) {
+            v[u][0] = p[0];
+          } else if constexpr (V == 2) {
+            const float2 t = *reinterpret_cast<const float2*>(p);
+            v[u][0] = t.x;
+            v[u][1] = t.y;
+          } else {
+            const float4 t = *reinterpret_cast<const float4*>(p);
+            v[u][0] = t.x;
+            v[u][1] = t.y;
+            v[u][2] = t.z;
+            v[u][3] = t.w;
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < G; ++u) {
+      if (u < cnt) {
+        if (e + u == s_end) {   // the open row ends before this edge: close it
+          if (st) vstore<V>(dptr + lane * V, acc);
+#pragma unroll
+          for (int k = 0; k < V; ++k) acc[k] = 0.f;
+          live = next_row();
+        }
+#pragma unroll
+        for (int k = 0; k < V; ++k) acc[k] = __fadd_rn(acc[k], __fmul_rn(ww[u], v[u][k]));
+      }
+    }
+  }
+  if (live && st) vstore<V>(dptr + lane * V, acc);
+  if (lane == 0) a.carry_row[chunk] = crow;
+}
+
+// Non-persistent flat kernel (one wave per chunk, as spmm_wave_kernel): X and
+// X2 as one 32-bit buffer range.
+template <int V, int G>
+__global__ void __launch_bounds__(kSpmmThreads)
+spmm_flat_kernel(SpmmArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int wave = uni(threadIdx.x >> 6);
+  int split = a.nchunks;
+  if (a.B < a.n_rows) split = min(a.nchunks, uni(a.rowptr[a.B]) / a.S);
+  const int ch = spmm_chunk_of(blockIdx.x, wave, kSpmmThreads / 64, a.nchunks, split);
+  if (ch < 0) return;
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.ubase, 0, a.span, 0x00020000);
+  const FlatSrc f{rs, rs, (uint32_t)lane * V * 4, 0, nullptr, 0, 0};
+  CodeWindow win;
+  win.wb = INT32_MIN / 2;
+  win.cmask = 0;
+  RowWindow rw;
+  rw.base = INT32_MIN / 2;
+  const int i = uni(a.chunk_row ? min(a.chunk_row[ch], a.n_rows)
+                                : lower_bound_i32(a.rowptr, a.n_rows, ch * a.S));
+  flat_chunk<V, G, false>(a, f, win, rw, ch, i, lane);
+}
+
+template <int V, int U>
+__global__ void __launch_bounds__(kCodesThreads)
+spmm_codes_kernel(SpmmArgs a, CodesSrc c) {
+  __shared__ float cbs[kCodesLdsFloats];
+  // stage the feature halves of every branch's codebook: cbs[(b*M + m)*D + k]
+  const int nbm = c.nb * c.M;
+  for (int t = threadIdx.x; t < nbm; t += kCodesThreads) {
+    const int b = t / c.M, m = t - b * c.M;
+    const float* src = c.emb + b * c.bstride + (int64_t)m * c.ldw + c.off;
+    if (c.D == 4 && ((reinterpret_cast<uintptr_t>(src) & 15) == 0)) {
+      *reinterpret_cast<float4*>(cbs + 4 * t) = *reinterpret_cast<const float4*>(src);
+    } else {
+      for (int k = 0; k < c.D; ++k) cbs[t * c.D + k] = src[k];
+    }
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int wave = uni(threadIdx.x >> 6);
+  constexpr int WPB = kCodesThreads / 64;
+  // this XCD's chunks: a contiguous 1/8 before the row-B split and a
+  // contiguous 1/8 after it (as spmm_chunk_of), strided over its waves
+  int split = a.nchunks;
+  if (a.B < a.n_rows) split = min(a.nchunks, uni(a.rowptr[a.B]) / a.S);
+  const int xcd = blockIdx.x % kNumXcd;
+  const int lw = (blockIdx.x / kNumXcd) * WPB + wave;
+  const int nwx = (gridDim.x / kNumXcd) * WPB;
+  const int c2 = a.nchunks - split;
+  const int a1 = xcd * split / kNumXcd, n1 = (xcd + 1) * split / kNumXcd - a1;
+  const int a2 = split + xcd * c2 / kNumXcd, n2 = split + (xcd + 1) * c2 / kNumXcd - a2;
+  const __amdgpu_buffer_rsrc_t rsx =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.X, 0, a.span, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsc =
+      __builtin_amdgcn_make_buffer_rsrc((void*)c.lcodes, 0, c.lcspan, 0x00020000);
+  const int col0 = lane * V;                 // first column of this lane
+  const int br = col0 / c.D;                 // its branch (V divides D)
+  CodeWindow win;
+  win.wb = INT32_MIN / 2;
+  win.cmask = 0;
+  RowWindow rw;
+  rw.base = INT32_MIN / 2;
+  const FlatSrc f{rsx, rsc, (uint32_t)lane * V * 4, (uint32_t)br * 2,
+                  cbs + (int64_t)br * c.M * c.D + (col0 - br * c.D), (uint32_t)c.D, c.ldlcb};
+  for (int t = lw; t < n1 + n2; t += nwx) {
+    const int ch = t < n1 ? a1 + t : a2 + (t - n1);
+    const int i = uni(a.chunk_row ? min(a.chunk_row[ch], a.n_rows)
+                                  : lower_bound_i32(a.rowptr, a.n_rows, ch * a.S));
+    flat_chunk<V, U, true>(a, f, win, rw, ch, i, lane);
+  }
 }
 
 // Each wave walks K consecutive chunks (its edge window and row cursor carry
@@ -848,6 +1303,32 @@ static void launch_spmm_wave(SpmmArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(spmm_fixup_kernel, dim3((a.nchunks + 255) / 256), dim3(256), 0, s, a);
 }
 
+// flat kernel group size (0 = off)
+static int spmm_flat() {
+  static const int g = env_int("VQGNN_SPMM_FLAT", 0);
+  return g;
+}
+
+template <int V>
+static void launch_spmm_flat(SpmmArgs& a, hipStream_t s) {
+  constexpr int WPB = kSpmmThreads / 64;
+  if (!a.chunk_row) {
+    int* cr = a.carry_row + align_up((size_t)a.nchunks * sizeof(int), 256) / sizeof(int);
+    hipLaunchKernelGGL(spmm_chunk_rows_kernel, dim3((a.nchunks + 255) / 256), dim3(256), 0, s,
+                       a.rowptr, a.n_rows, a.S, a.nchunks, cr);
+    a.chunk_row = cr;
+  }
+  const int per_xcd = (a.nchunks + kNumXcd - 1) / kNumXcd + 1;
+  const int grid = kNumXcd * ((per_xcd + WPB - 1) / WPB);
+  if (spmm_flat() == 8)
+    hipLaunchKernelGGL((spmm_flat_kernel<V, 8>), dim3(grid), dim3(kSpmmThreads), 0, s, a);
+  else if (spmm_flat() == 32)
+    hipLaunchKernelGGL((spmm_flat_kernel<V, 32>), dim3(grid), dim3(kSpmmThreads), 0, s, a);
+  else
+    hipLaunchKernelGGL((spmm_flat_kernel<V, 16>), dim3(grid), dim3(kSpmmThreads), 0, s, a);
+  hipLaunchKernelGGL(spmm_fixup_kernel, dim3((a.nchunks + 255) / 256), dim3(256), 0, s, a);
+}
+
 // 0 = automatic (wave kernel where it applies), 1 = lane-group kernel only,
 // 2 = wave kernel with 64-bit row addresses (FAR) even when the range fits
 static int spmm_mode() {
@@ -898,6 +1379,8 @@ static int dispatch_spmm(SpmmArgs& a, int64_t rows_x, int64_t rows_x2, hipStream
     } else if (F == 128 && pair) {
       if (near) launch_spmm_wave<4, 8, false, true>(a, s);
       else launch_spmm_wave<4, 8, true, true>(a, s);
+    } else if (F == 128 && near && spmm_flat() > 0) {
+      launch_spmm_flat<2>(a, s);
     } else if (F == 128) {
       if (near) launch_spmm_wave<2, 8, false>(a, s); else launch_spmm_wave<2, 8, true>(a, s);
     } else if (F == 256) {
@@ -1006,6 +1489,109 @@ extern "C" int vqgnn_spmm(const int32_t* rowptr, const int32_t* col, const float
   a.span = a.offx = a.ldxb = a.offx2 = a.ldx2b = 0;
   return X2 ? dispatch_spmm<true>(a, B, (int64_t)n_cols - B, s)
             : dispatch_spmm<false>(a, n_cols, 0, s);
+}
+
+extern "C" int vqgnn_spmm_codes_supported(int32_t F, int32_t nb, int32_t M, int32_t D) {
+  if (F != 64 && F != 128 && F != 256) return 0;
+  const int V = F / 64;
+  if (D <= 0 || nb <= 0 || M <= 0 || nb * D != F || D % V != 0) return 0;
+  return (int64_t)nb * M * D <= kCodesLdsFloats ? 1 : 0;
+}
+
+extern "C" int vqgnn_spmm_codes(const int32_t* rowptr, const int32_t* col, const float* val,
+                                int32_t n_rows, int32_t n_cols, int64_t nnz, int32_t B,
+                                const float* X, int64_t ldx, const int16_t* lcodes,
+                                int64_t ldlc, int32_t nb, const float* emb, int32_t M, int32_t D,
+                                int32_t ldw, int64_t emb_bstride, int32_t col_offset, int32_t F,
+                                float* out, int64_t ldo, const int32_t* plan, void* workspace,
+                                vqgnn_stream_t stream) {
+  clear_error();
+  VQGNN_REQUIRE(rowptr && out && n_rows >= 0, "spmm_codes: null pointer");
+  if (!vqgnn_spmm_codes_supported(F, nb, M, D)) {
+    set_error("spmm_codes: F=%d nb=%d M=%d D=%d outside the LDS codebook path", F, nb, M, D);
+    return VQGNN_ERR_UNSUPPORTED;
+  }
+  VQGNN_REQUIRE(ldx % 4 == 0 && ldo % 4 == 0 && ldx >= F && ldo >= F,
+                "spmm_codes: ldx/ldo must be multiples of 4 and >= F");
+  VQGNN_REQUIRE(((uintptr_t)X & 15) == 0 && ((uintptr_t)out & 15) == 0,
+                "spmm_codes: X/out must be 16-byte aligned");
+  VQGNN_REQUIRE(nnz < (int64_t)INT32_MAX, "spmm_codes: nnz >= 2^31");
+  VQGNN_REQUIRE(B >= 0 && B <= n_cols && ldlc >= nb, "spmm_codes: need 0 <= B <= n_cols, ldlc >= nb");
+  VQGNN_REQUIRE(col_offset >= 0 && col_offset + D <= ldw, "spmm_codes: bad codebook layout");
+  VQGNN_REQUIRE((uint64_t)B * (uint64_t)ldx * 4 < 0xFFFFFFFFull &&
+                (uint64_t)(n_cols - B) * (uint64_t)ldlc * 2 < 0xFFFFFFFFull,
+                "spmm_codes: X or lcodes spans 4 GiB");
+  hipStream_t s = as_stream(stream);
+  if (n_rows == 0) return VQGNN_OK;
+  if (nnz == 0) {
+    const int64_t tot = (int64_t)n_rows * F;
+    hipLaunchKernelGGL(zero_rows_kernel, dim3((tot + 255) / 256), dim3(256), 0, s, out, ldo,
+                       n_rows, F);
+    return check_launch("spmm_codes(zero)");
+  }
+  VQGNN_REQUIRE(col && val && (X || B == 0) && emb && workspace && (lcodes || B == n_cols),
+                "spmm_codes: null pointer");
+  SpmmArgs a;
+  memset(&a, 0, sizeof(a));
+  a.rowptr = rowptr;
+  a.col = col;
+  a.val = val;
+  a.n_rows = n_rows;
+  a.nnz = (int)nnz;
+  a.F4 = F / 4;
+  a.S = spmm_chunk_edges(a.F4);
+  a.L = spmm_long_row(a.S);
+  a.nchunks = (int)((nnz + a.S - 1) / a.S);
+  a.B = B;
+  a.X = X;
+  a.ldx4 = ldx / 4;
+  a.out = out;
+  a.ldo4 = ldo / 4;
+  a.carry = reinterpret_cast<float*>(workspace);
+  a.carry_row = reinterpret_cast<int*>(reinterpret_cast<char*>(workspace) +
+                                       align_up((size_t)a.nchunks * 2 * F * sizeof(float), 256));
+  a.kpw = 1;
+  a.chunk_row = plan;
+  a.dbg = env_int("VQGNN_SPMM_DEBUG", 0) & 2;
+  a.span = (uint32_t)((uint64_t)B * ldx * 4);
+  a.ldxb = (uint32_t)(ldx * 4);
+  CodesSrc c;
+  c.lcodes = lcodes;
+  c.ldlcb = (uint32_t)(ldlc * 2);
+  c.lcspan = (uint32_t)((uint64_t)(n_cols - B) * ldlc * 2);
+  c.emb = emb;
+  c.bstride = emb_bstride;
+  c.ldw = ldw;
+  c.off = col_offset;
+  c.M = M;
+  c.D = D;
+  c.nb = nb;
+  if (!plan) {
+    int* cr = a.carry_row + align_up((size_t)a.nchunks * sizeof(int), 256) / sizeof(int);
+    hipLaunchKernelGGL(spmm_chunk_rows_kernel, dim3((a.nchunks + 255) / 256), dim3(256), 0, s,
+                       a.rowptr, a.n_rows, a.S, a.nchunks, cr);
+    a.chunk_row = cr;
+  }
+  int dev = 0, ncu = 256;
+  (void)hipGetDevice(&dev);
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      ncu <= 0)
+    ncu = 256;
+  static const int per_cu = env_int("VQGNN_SPMM_CODES_WG", 1);
+  const int grid = kNumXcd * ((ncu * (per_cu < 1 ? 1 : per_cu) + kNumXcd - 1) / kNumXcd);
+  static const int uc = env_int("VQGNN_SPMM_CODES_G", 16);
+  if (F == 128) {
+    if (uc == 8) hipLaunchKernelGGL((spmm_codes_kernel<2, 8>), dim3(grid), dim3(kCodesThreads), 0, s, a, c);
+    else hipLaunchKernelGGL((spmm_codes_kernel<2, 16>), dim3(grid), dim3(kCodesThreads), 0, s, a, c);
+  } else if (F == 256) {
+    hipLaunchKernelGGL((spmm_codes_kernel<4, 8>), dim3(grid), dim3(kCodesThreads), 0, s, a, c);
+  } else {
+    hipLaunchKernelGGL((spmm_codes_kernel<1, 32>), dim3(grid), dim3(kCodesThreads), 0, s, a, c);
+  }
+  int rc = check_launch("spmm_codes");
+  if (rc) return rc;
+  hipLaunchKernelGGL(spmm_fixup_kernel, dim3((a.nchunks + 255) / 256), dim3(256), 0, s, a);
+  return check_launch("spmm_codes(fixup)");
 }
 
 extern "C" int vqgnn_gather_codewords(const int64_t* subset, int32_t B, int32_t n,

@@ -225,6 +225,41 @@ def spmm(rowptr, col, val, n_rows, nnz, X, F, X2=None, B=None, out=None, plan=No
     return out
 
 
+def spmm_codes_supported(F, nb, M, D) -> bool:
+    """True when vqgnn_spmm_codes applies (include/vqgnn.h §6c)."""
+    return bool(lib().vqgnn_spmm_codes_supported(int(F), int(nb), int(M), int(D)))
+
+
+def spmm_codes(rowptr, col, val, n_rows, nnz, X, F, lcodes, emb_out, D, B, out=None, plan=None,
+               col_offset=0):
+    """vqgnn_spmm with the out-of-batch rows read as codewords:
+    xin[j] = X[j] (j < B), concat_b emb_out[b, lcodes[j-B, b], col_offset:col_offset+D]
+    (j >= B) — x_input = cat([x, x_first_order]) of models.py:168-174 without
+    materialising x_first_order.  lcodes: gather_codewords(..., want_x=False,
+    want_codes=True)."""
+    require_gpu(X, "spmm_codes")
+    dev = X.device
+    nb, M = emb_out.shape[0], emb_out.shape[1]
+    if out is None:
+        out = torch.empty(n_rows, F, dtype=torch.float32, device=dev)
+    if lcodes.dtype != torch.int16 or lcodes.dim() != 2 or lcodes.shape[1] != nb or \
+            lcodes.stride(1) != 1:
+        raise ValueError("spmm_codes: lcodes must be int16 [n-B, nb], row-major")
+    if emb_out.stride(2) != 1 or emb_out.stride(1) != emb_out.shape[2]:
+        raise ValueError("spmm_codes: emb_out must be [nb, M, W] with contiguous rows")
+    if X.shape[0] < int(B):
+        raise ValueError(f"spmm_codes: X has {X.shape[0]} rows < B={B}")
+    L = lib()
+    ws = workspace(L.vqgnn_spmm_workspace(n_rows, nnz, F), dev)
+    n_cols = int(B) + lcodes.shape[0]
+    check(L.vqgnn_spmm_codes(ptr(rowptr), ptr(col), ptr(val), int(n_rows), n_cols, int(nnz),
+                             int(B), ptr(X), _ld(X), ptr(lcodes), lcodes.stride(0), nb,
+                             ptr(emb_out), M, int(D), emb_out.shape[2], emb_out.stride(0),
+                             int(col_offset), int(F), ptr(out), _ld(out), ptr(plan), ptr(ws),
+                             stream_ptr()), "spmm_codes")
+    return out
+
+
 def csr_transpose(rowptr, col, val, n_rows, n_cols, nnz, want_perm=False):
     """-> (t_rowptr, t_col, t_val[, t_perm]); t_perm[k] = input edge of entry k."""
     dev = rowptr.device
