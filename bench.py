@@ -43,10 +43,11 @@ def parse():
     # kernel events inside the timed region (the roofline kernel's launches);
     # off only to measure what they cost
     p.add_argument("--no-kernel-events", action="store_true")
-    # aggregation source for the out-of-batch rows: "codes" = code records +
-    # LDS-staged codebooks (x_first_order never materialised) where the
-    # codebook fits in LDS; "rows" = gathered x_first_order rows
-    p.add_argument("--spmm-source", default="auto", choices=["auto", "codes", "rows"])
+    # aggregation source for the out-of-batch rows: "rows" = gathered
+    # x_first_order rows (default: measured faster, 99+7 us vs 171+7 us at
+    # arxiv_gcn, profiles/r01c_*); "codes" = code records + LDS-staged
+    # codebooks (x_first_order never materialised) where the codebook fits
+    p.add_argument("--spmm-source", default="rows", choices=["codes", "rows"])
     return p.parse_args()
 
 
@@ -110,8 +111,8 @@ def main():
         gat = OurGATConv(F + 1, F + 1, bias=False, add_self_loops=False).to(dev)
     # per-batch adjacency preparation (like the reference's SparseTensor build
     # in the data loader): the SpMM chunk plan, computed once per batch
-    spmm_plan = adj.plan(F)
-    fused = gat is None and args.spmm_source != "rows" and kernels.spmm_codes_supported(F, nb, M, D)
+    spmm_plan = adj.plan(F, B=B)
+    fused = gat is None and args.spmm_source == "codes" and kernels.spmm_codes_supported(F, nb, M, D)
     if args.spmm_source == "codes" and not fused:
         raise SystemExit(f"--spmm-source codes: F={F} M={M} does not fit the LDS codebook path")
     # codebook state = one feature_update warm pass

@@ -231,6 +231,30 @@ int vqgnn_spmm_codes(const int32_t* rowptr, const int32_t* col, const float* val
                      int64_t ldo, const int32_t* plan, void* workspace,
                      vqgnn_stream_t stream);
 
+/* 6d. Segment-pair SpMM (F = 128): vqgnn_spmm with the same arguments, the
+ *     same row semantics and bit-identical output, on a segment plan: rows
+ *     (long rows: their S-aligned pieces) sorted by length inside 2048-row
+ *     windows and XCD ranges, two segments per wave (one per half-wave), so
+ *     one dwordx4 wave-instruction gathers two 512-B input rows.
+ *     plan: vqgnn_spmm_pair_plan_size(n_rows, nnz, F) int32, built once per
+ *     batch adjacency, F and B by vqgnn_spmm_pair_plan (scratch:
+ *     vqgnn_spmm_pair_plan_workspace bytes); B splits the rows into batch
+ *     and out-of-batch ranges for the XCD placement only.  workspace:
+ *     vqgnn_spmm_workspace(n_rows, nnz, F).  The plan covers rows
+ *     [0, n_rows) exactly as passed here.  When X and X2 lie more than 4 GiB
+ *     apart the call runs vqgnn_spmm with chunk_plan (6b, may be NULL).
+ *     Replaces convs.py:95 -> torch_sparse spmm_sum like 6.                  */
+int vqgnn_spmm_pair_supported(int32_t F);
+int64_t vqgnn_spmm_pair_plan_size(int32_t n_rows, int64_t nnz, int32_t F);
+size_t vqgnn_spmm_pair_plan_workspace(int32_t n_rows, int64_t nnz, int32_t F);
+int vqgnn_spmm_pair_plan(const int32_t* rowptr, int32_t n_rows, int64_t nnz, int32_t F,
+                         int32_t B, int32_t* plan, void* workspace, vqgnn_stream_t stream);
+int vqgnn_spmm_pair(const int32_t* rowptr, const int32_t* col, const float* val,
+                    int32_t n_rows, int32_t n_cols, int64_t nnz, int32_t B,
+                    const float* X, int64_t ldx, const float* X2, int64_t ldx2,
+                    int32_t F, float* out, int64_t ldo, const int32_t* plan,
+                    const int32_t* chunk_plan, void* workspace, vqgnn_stream_t stream);
+
 /* 7. CSR transpose (structure + values) for the backward product
  *    dX = A^T dOut (torch_sparse matmul autograd, convs.py:95).  Output CSR of
  *    A^T with rows sorted by column of A; within a row, entries ordered by

@@ -130,12 +130,54 @@ def bench_codes():
     print("codes == two-source:", bool(torch.equal(ref, fz)), flush=True)
 
 
+def bench_pair():
+    """Segment-pair SpMM (dwordx4, two segments per wave) against the chunk
+    wave kernel: time, plan build time, and bit-identity of the outputs."""
+    cfg = CONFIGS["arxiv_gcn"]
+    g, _, b = make_batch(cfg)
+    bidx, subset, adj = batch_to_device(b, dev)
+    F = 128
+    X = torch.randn(b.B, F, device=dev)
+    xt = torch.randn(b.n - b.B, F, device=dev)
+    Xn = torch.randn(b.n, F, device=dev)
+    pl = adj.plan(F)
+    tp = timeit(lambda: kernels.spmm_pair_plan(adj.rowptr, b.n, b.nnz, F, b.B), reps=5, warm=1)
+    pp = kernels.spmm_pair_plan(adj.rowptr, b.n, b.nnz, F, b.B)
+    hdr = pp.buf[:16].cpu().tolist()
+    print(f"pair plan: {tp:8.1f} us  segs={hdr[0]} long={hdr[1]} xcd_begin={hdr[2:11]}", flush=True)
+    res = {}
+    res["wave two-source"] = timeit(lambda: kernels.spmm(adj.rowptr, adj.col, adj.value, b.n,
+                                                         b.nnz, X, F, X2=xt, B=b.B, plan=pl))
+    res["pair two-source"] = timeit(lambda: kernels.spmm(adj.rowptr, adj.col, adj.value, b.n,
+                                                         b.nnz, X, F, X2=xt, B=b.B, plan=pp))
+    res["wave all-X"] = timeit(lambda: kernels.spmm(adj.rowptr, adj.col, adj.value, b.n, b.nnz,
+                                                    Xn, F, plan=pl))
+    res["pair all-X"] = timeit(lambda: kernels.spmm(adj.rowptr, adj.col, adj.value, b.n, b.nnz,
+                                                    Xn, F, plan=pp))
+    deg = np.diff(b.rowptr)
+    rows = torch.repeat_interleave(torch.arange(b.n, device=dev), torch.from_numpy(deg).to(dev))
+    hot = (torch.arange(b.nnz, device=dev) % 1024).to(torch.int32)
+    res["wave hot set"] = timeit(lambda: kernels.spmm(adj.rowptr, hot, adj.value, b.n, b.nnz, Xn,
+                                                      F, plan=pl))
+    res["pair hot set"] = timeit(lambda: kernels.spmm(adj.rowptr, hot, adj.value, b.n, b.nnz, Xn,
+                                                      F, plan=pp))
+    for k, v in res.items():
+        print(f"{k:24s} {v:8.1f} us  {b.nnz * 512 / v / 1e6:6.2f} TB/s gathered", flush=True)
+    ref = kernels.spmm(adj.rowptr, adj.col, adj.value, b.n, b.nnz, X, F, X2=xt, B=b.B, plan=pl)
+    got = kernels.spmm(adj.rowptr, adj.col, adj.value, b.n, b.nnz, X, F, X2=xt, B=b.B, plan=pp)
+    print("pair == wave:", bool(torch.equal(ref, got)),
+          "max|d| =", float((ref - got).abs().max()), flush=True)
+    del rows
+
+
 if __name__ == "__main__":
     what = sys.argv[1] if len(sys.argv) > 1 else "all"
     if what in ("vq", "all"):
         bench_vq()
     if what == "codes":
         bench_codes()
+    if what == "pair":
+        bench_pair()
     if what in ("spmm", "all"):
         for s_ in os.environ.get("SPMM_S_LIST", "").split(","):
             pass

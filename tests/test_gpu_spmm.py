@@ -289,3 +289,126 @@ def test_spmm_codes_unsorted_rows_hubs_and_edges():
     o4 = kernels.spmm_codes(e.rowptr, e.col, e.value, 5, 0, xd, F, lcd, emb_d, D, B)
     assert torch.count_nonzero(o4) == 0
     assert not kernels.spmm_codes_supported(128, 32, 1024, 4)   # 512 KiB of codebook
+
+
+# --- segment-pair SpMM (include/vqgnn.h §6d): bit-identical to vqgnn_spmm ---
+
+def _pair_vs_chunk(rowptr, col, val, n_rows, n_cols, F, B=None, x2_rows=0, seed=0):
+    rng = np.random.default_rng(seed)
+    a = _dev_csr(rowptr, col, val, n_rows, n_cols)
+    if x2_rows:
+        X = torch.from_numpy(rng.standard_normal((B, F)).astype(np.float32)).to(DEV)
+        X2 = torch.from_numpy(rng.standard_normal((x2_rows, F)).astype(np.float32)).to(DEV)
+    else:
+        X = torch.from_numpy(rng.standard_normal((n_cols, F)).astype(np.float32)).to(DEV)
+        X2 = None
+    chunk = kernels.spmm_plan(a.rowptr, n_rows, a.nnz(), F)
+    pp = kernels.spmm_pair_plan(a.rowptr, n_rows, a.nnz(), F, B if B is not None else n_rows,
+                                chunk=chunk)
+    ref = kernels.spmm(a.rowptr, a.col, a.value, n_rows, a.nnz(), X, F, X2=X2, B=B, plan=chunk)
+    got = kernels.spmm(a.rowptr, a.col, a.value, n_rows, a.nnz(), X, F, X2=X2, B=B, plan=pp)
+    return ref, got, pp, X, X2
+
+
+def test_pair_plan_covers_every_row_once():
+    rng = np.random.default_rng(3)
+    deg = rng.integers(0, 40, size=5000)
+    deg[rng.random(5000) < 0.2] = 0
+    deg[[7, 2500, 4999]] = [300, 1000, 257]       # long rows: S-aligned pieces
+    rowptr = np.zeros(5001, np.int64)
+    rowptr[1:] = np.cumsum(deg)
+    a = _dev_csr(rowptr, np.zeros(rowptr[-1], np.int64), np.zeros(rowptr[-1]), 5000, 10)
+    pp = kernels.spmm_pair_plan(a.rowptr, 5000, a.nnz(), 128, 3000)
+    hdr = pp.buf[:16].cpu().numpy()
+    nseg, nlong = int(hdr[0]), int(hdr[1])
+    xb = hdr[2:11]
+    assert xb[0] == 0 and xb[8] == nseg and np.all(np.diff(xb) >= 0)
+    segs = pp.buf[16:16 + 4 * nseg].view(-1, 4).cpu().numpy()
+    rows = segs[segs[:, 2] >= 0, 2]
+    long_rows = np.nonzero(deg > 256)[0]
+    assert nlong == len(long_rows)
+    # every short row exactly once (empty rows too), long rows only as pieces
+    assert np.array_equal(np.sort(rows), np.setdiff1d(np.arange(5000), long_rows))
+    pieces = segs[segs[:, 2] <= -2]
+    assert pieces[:, 1].sum() == deg[long_rows].sum()
+    # edges covered exactly once
+    cover = np.zeros(rowptr[-1], np.int32)
+    for st, ln, _, _ in segs:
+        cover[st:st + ln] += 1
+    assert np.all(cover == 1)
+    # inside each XCD range: row windows ascending, lengths descending per window
+    for x in range(8):
+        s = segs[xb[x]:xb[x + 1]]
+        if len(s) < 2:
+            continue
+        assert np.all(s[:, 1] <= 511)
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_pair_bit_identical_random(seed):
+    rng = np.random.default_rng(seed)
+    rowptr, col, val = _random_csr(4000, 3000, 40, rng, hub_rows=(11, 1999), hub_deg=2900)
+    ref, got, _, _, _ = _pair_vs_chunk(rowptr, col, val, 4000, 3000, 128, seed=seed)
+    assert torch.equal(ref, got)
+
+
+def test_pair_two_source_and_long_rows_vs_oracle():
+    rng = np.random.default_rng(5)
+    n_rows, B, n2 = 3000, 1800, 1200
+    n_cols = B + n2
+    deg = rng.integers(0, 30, size=n_rows)
+    deg[100:140] = rng.integers(257, 900, size=40)
+    rowptr = np.zeros(n_rows + 1, np.int64)
+    rowptr[1:] = np.cumsum(deg)
+    col = np.concatenate([np.sort(rng.choice(n_cols, size=d, replace=False)) for d in deg])
+    val = rng.standard_normal(col.shape[0]).astype(np.float32)
+    ref, got, _, X, X2 = _pair_vs_chunk(rowptr, col, val, n_rows, n_cols, 128, B=B, x2_rows=n2)
+    assert torch.equal(ref, got)
+    xin = np.concatenate([X.cpu().numpy(), X2.cpu().numpy()])
+    exact = conv_ref.spmm_seq(rowptr, col, val, xin)
+    short = np.diff(rowptr) <= 256
+    assert np.array_equal(got.cpu().numpy()[short], exact[short])
+    f64 = conv_ref.spmm_fp64(rowptr, col, val, xin)
+    scale = conv_ref.spmm_fp64(rowptr, col, np.abs(val), np.abs(xin)) + 1e-6
+    assert np.max(np.abs(got.cpu().numpy() - f64) / scale) < 1e-5
+
+
+def test_pair_empty_rows_and_tiny():
+    rowptr = [0, 0, 2, 2, 3, 3, 3]
+    ref, got, _, _, _ = _pair_vs_chunk(rowptr, [1, 4, 9], [1.0, 2.0, 3.0], 6, 10, 128)
+    assert torch.equal(ref, got)
+    assert torch.count_nonzero(got[[0, 2, 4, 5]]) == 0
+
+
+def test_pair_far_apart_falls_back():
+    """X and X2 more than 4 GiB apart: the pair call runs the chunk kernels."""
+    rng = np.random.default_rng(9)
+    B, n2 = 500, 300
+    rowptr, col, val = _random_csr(800, B + n2, 20, rng)
+    a = _dev_csr(rowptr, col, val, 800, B + n2)
+    X = torch.randn(B, 128, device=DEV)
+    gap = torch.empty(5 << 30, dtype=torch.uint8, device=DEV)
+    X2 = torch.randn(n2, 128, device=DEV)
+    if abs(X2.data_ptr() - X.data_ptr()) < (4 << 30):
+        pytest.skip("allocator placed the buffers close together")
+    pp = a.plan(128, B=B)
+    got = kernels.spmm(a.rowptr, a.col, a.value, 800, a.nnz(), X, 128, X2=X2, B=B, plan=pp)
+    chunk = kernels.spmm_plan(a.rowptr, 800, a.nnz(), 128)
+    ref = kernels.spmm(a.rowptr, a.col, a.value, 800, a.nnz(), X, 128, X2=X2, B=B, plan=chunk)
+    del gap
+    assert torch.equal(ref, got)
+
+
+def test_pair_arxiv_batch_bit_identical():
+    cfg = graph.CONFIGS["arxiv_gcn"]
+    _, _, b = graph.make_batch(cfg)
+    _, _, adj = graph.batch_to_device(b, DEV)
+    F = 128
+    X = torch.randn(b.B, F, device=DEV)
+    X2 = torch.randn(b.n - b.B, F, device=DEV)
+    pp = adj.plan(F, B=b.B)
+    assert isinstance(pp, kernels.PairPlan)
+    got = kernels.spmm(adj.rowptr, adj.col, adj.value, b.n, b.nnz, X, F, X2=X2, B=b.B, plan=pp)
+    chunk = kernels.spmm_plan(adj.rowptr, b.n, b.nnz, F)
+    ref = kernels.spmm(adj.rowptr, adj.col, adj.value, b.n, b.nnz, X, F, X2=X2, B=b.B, plan=chunk)
+    assert torch.equal(ref, got)

@@ -59,7 +59,7 @@ class GatherSpMMFunction(torch.autograd.Function):
         xc = x if (x.stride(1) == 1 and x.stride(0) % 4 == 0 and
                    x.data_ptr() % 16 == 0) else x.contiguous()
         out = kernels.spmm(adj.rowptr, adj.col, adj.value, n, adj.nnz(), xc, F, X2=x_first, B=B,
-                           plan=adj.plan(F))
+                           plan=adj.plan(F, B=B))
         ctx.adj, ctx.B, ctx.hook = adj, B, hook
         return out
 
@@ -75,7 +75,8 @@ class GatherSpMMFunction(torch.autograd.Function):
             F = dout.shape[1]
             # rows [0, B) of A^T = columns [0, B) of A; the merge kernel bounds
             # the walk with the full nnz, so no host read of t_rowptr[B] is needed
-            dx = kernels.spmm(at.rowptr, at.col, at.value, B, at.nnz(), dout, F, plan=at.plan(F))
+            dx = kernels.spmm(at.rowptr, at.col, at.value, B, at.nnz(), dout, F,
+                              plan=at.plan(F, n_rows=B))
         return dx, None, None, None, None
 
 

@@ -23,8 +23,10 @@
 #include "common.h"
 
 #include <cstdlib>
+#include <utility>
 #include <cstring>
 #include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
 
 namespace vqgnn {
 
@@ -1702,4 +1704,539 @@ extern "C" int vqgnn_csr_expand_rows(const int32_t* rowptr, int32_t n_rows, int6
   hipLaunchKernelGGL(expand_rows_kernel, dim3((n + 255) / 256), dim3(256), 0, as_stream(stream),
                      rowptr, n_rows, rows, (int32_t*)nullptr, n);
   return check_launch("csr_expand_rows");
+}
+
+// ===========================================================================
+// Segment-pair SpMM (F = 128).  Same row semantics and bits as vqgnn_spmm:
+// a row of at most L edges is summed whole from 0 in CSR order with separate
+// mul and add; a longer row is cut at the global S-aligned chunk boundaries
+// (the pieces spmm_wave_kernel leaves as carries) and its pieces are added in
+// order by spmm_pair_fixup_kernel (first piece as the initial value, as
+// spmm_fixup_kernel does) — so the output is bit-identical to vqgnn_spmm.
+//
+// Why: the gather of a 512-B row per wave-instruction (dwordx2 per lane) runs
+// at ~35 G rows/s from L2, dwordx4 with two rows per instruction at ~62 G
+// rows/s (scripts/probes/gather_shape.hip on MI355X); the per-instruction cost
+// dominates.  Here each half-wave owns one segment (a row, or a piece of a
+// long row): one buffer_load_dwordx4 fetches edge k of both halves' segments.
+// The two segments of a pair have (nearly) equal lengths because the plan
+// sorts segments by length inside row windows, so the halves rarely idle.
+// Per half-wave step: the edge's input-row offset and weight come from a
+// staged 32-edge window by ds_bpermute (LDS crossbar, no VALU), one v_add for
+// the lane's column offset, then 2 v_pk_mul + 2 v_pk_add.
+//
+// Plan (built once per batch and F, on the device, vqgnn_spmm_pair_plan):
+//   hdr[16]      : [0] segments, [1] long rows, [2..10] xcd_begin[0..8]
+//   segs[cap]    : int4 {first edge, length, dst, 0}; dst >= 0: output row;
+//                  dst <= -2: carry slot -dst-2 (a piece of a long row)
+//   longrows[lc] : int4 {row, first slot, pieces, 0}
+// Segment order: key = (xcd, row window of 2048 rows, -length).  XCD x gets an
+// edge-balanced contiguous range of the batch rows (< B) and one of the
+// out-of-batch rows, as spmm_wave_kernel's chunk placement does, so the
+// gathers of an XCD stay cluster-local in its L2; length-sorting only inside
+// 2048-row windows keeps that locality (LRU simulation of the arxiv batch:
+// 64.9% L2 hits against 64.5% in CSR order, 56% for a global length sort).
+// ===========================================================================
+
+namespace vqgnn {
+
+constexpr int kPairHdr = 16;
+constexpr int kPairWinShift = 11;   // row windows of 2048 rows
+
+static inline int64_t pair_seg_cap(int32_t n_rows, int64_t nnz, int S, int L) {
+  return (int64_t)n_rows + nnz / S + nnz / (L > 0 ? L : 1) + 16;
+}
+static inline int64_t pair_long_cap(int64_t nnz, int L) { return nnz / (L > 0 ? L : 1) + 1; }
+
+// per row: segments and carry slots it needs
+__global__ void pair_count_kernel(const int32_t* __restrict__ rowptr, int n_rows, int S, int L,
+                                  int32_t* __restrict__ nseg, int32_t* __restrict__ nslot) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n_rows) return;
+  const int rs = rowptr[r], re = rowptr[r + 1];
+  const int len = re - rs;
+  if (len <= L) {
+    nseg[r] = 1;
+    nslot[r] = 0;
+  } else {
+    const int np = (re - 1) / S - rs / S + 1;
+    nseg[r] = np;
+    nslot[r] = np;
+  }
+}
+
+__device__ __forceinline__ uint32_t pair_key(int xcd, int r, int len) {
+  const uint32_t win = min((uint32_t)r >> kPairWinShift, (1u << 19) - 1);
+  return ((uint32_t)xcd << 28) | (win << 9) | (uint32_t)(511 - min(len, 511));
+}
+
+// per row: its segment records (unsorted), sort keys, long-row entries
+__global__ void pair_fill_kernel(const int32_t* __restrict__ rowptr, int n_rows, int B, int S,
+                                 int L, const int32_t* __restrict__ seg_off,
+                                 const int32_t* __restrict__ slot_off, int4* __restrict__ useg,
+                                 uint32_t* __restrict__ keys, int4* __restrict__ longrows,
+                                 int32_t* __restrict__ nlong) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n_rows) return;
+  const int rs = rowptr[r], re = rowptr[r + 1];
+  const int len = re - rs;
+  // edge-balanced XCD ranges: batch rows and out-of-batch rows separately
+  const int64_t eb = rowptr[B], en = rowptr[n_rows];
+  int xcd;
+  if (r < B) xcd = eb > 0 ? (int)((int64_t)rs * kNumXcd / eb) : 0;
+  else xcd = en > eb ? (int)((int64_t)(rs - eb) * kNumXcd / (en - eb)) : 0;
+  xcd = min(max(xcd, 0), kNumXcd - 1);
+  const int p0 = seg_off[r];
+  if (len <= L) {
+    useg[p0] = make_int4(rs, len, r, 0);
+    keys[p0] = pair_key(xcd, r, len);
+    return;
+  }
+  const int np = (re - 1) / S - rs / S + 1;
+  const int sb = slot_off[r];
+  const int li = atomicAdd(nlong, 1);
+  longrows[li] = make_int4(r, sb, np, 0);
+  for (int i = 0; i < np; ++i) {
+    const int a = i == 0 ? rs : (rs / S + i) * S;
+    const int b = min(re, (rs / S + i + 1) * S);
+    useg[p0 + i] = make_int4(a, b - a, -(sb + i) - 2, 0);
+    keys[p0 + i] = pair_key(xcd, r, b - a);
+  }
+}
+
+__global__ void pair_pad_kernel(uint32_t* __restrict__ keys, uint32_t* __restrict__ iota,
+                                const int32_t* __restrict__ seg_off,
+                                const int32_t* __restrict__ nseg, int n_rows, int64_t cap) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= cap) return;
+  const int64_t total = n_rows > 0 ? (int64_t)seg_off[n_rows - 1] + nseg[n_rows - 1] : 0;
+  if (i >= total) keys[i] = 0xFFFFFFFFu;
+  iota[i] = (uint32_t)i;
+}
+
+__global__ void pair_gather_kernel(const int4* __restrict__ useg, const uint32_t* __restrict__ idx,
+                                   const uint32_t* __restrict__ skeys, int4* __restrict__ segs,
+                                   int64_t cap) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= cap) return;
+  segs[i] = skeys[i] == 0xFFFFFFFFu ? make_int4(0, 0, -1, 0) : useg[idx[i]];
+}
+
+// hdr: segment count, long-row count, xcd_begin[0..8] (binary search on the
+// sorted keys)
+__global__ void pair_hdr_kernel(const uint32_t* __restrict__ skeys, int64_t cap,
+                                const int32_t* __restrict__ nlong, int32_t* __restrict__ hdr) {
+  const int t = threadIdx.x;
+  if (t <= kNumXcd) {
+    int64_t lo = 0, hi = cap;
+    const uint32_t k = (uint32_t)t << 28;
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (skeys[mid] < k) lo = mid + 1; else hi = mid;
+    }
+    hdr[2 + t] = (int32_t)lo;
+    if (t == kNumXcd) hdr[0] = (int32_t)lo;
+  }
+  if (t == 0) hdr[1] = *nlong;
+}
+
+struct PairArgs {
+  const int32_t* col;
+  const float* val;
+  const int4* segs;
+  const int32_t* hdr;
+  const int4* longrows;
+  const char* ubase;
+  uint32_t span, offx, ldxb, offx2, ldx2b;
+  int B;
+  float* out;
+  int64_t ldo;   // floats
+  float* carry;  // [slots][128]
+  int dbg;       // experiments: 1 = no gathers, 2 = no stores, 8 = no adds
+};
+
+constexpr int kPairG = 8;   // steps (edges per half) whose loads are in flight together
+
+// Window of a half's next 32 edges: lane c of the half holds edge k0 + c as
+// (input-row byte offset, weight).  Edges past the segment get the offset
+// `span` (outside the buffer range: the load returns 0) and weight 0, so a
+// masked step adds +0 — a no-op on the accumulator, which is never -0 (it
+// starts at +0 and round-to-nearest sums give -0 only from two -0s) — and
+// no step needs a guard.
+struct PairWin {
+  uint32_t o;
+  float w;
+};
+
+__device__ __forceinline__ PairWin pair_window(const PairArgs& a, int start, int len, int k0,
+                                               int c) {
+  const int kk = k0 + c;
+  PairWin r{a.span, 0.f};
+  if (kk < len) {
+    const int j = a.col[start + kk];
+    r.w = a.val[start + kk];
+    r.o = j < a.B ? a.offx + (uint32_t)j * a.ldxb : a.offx2 + (uint32_t)(j - a.B) * a.ldx2b;
+  }
+  return r;
+}
+
+// issue the gathers of steps kw .. kw+G-1 of the window (kw = 0 or 16): the
+// row offset by ds_bpermute from the half's window lane (immediate offset),
+// one v_add for this lane's column bytes, one dwordx4 load for both halves
+// Broadcast lane K of each 32-lane half to the whole half: ds_swizzle in
+// bitmask mode (and 0, or K): no address operand, unlike ds_bpermute
+template <int K>
+__device__ __forceinline__ int half_bcast(int v) {
+  return __builtin_amdgcn_ds_swizzle(v, K << 5);
+}
+
+template <int DBG, int KW>
+__device__ __forceinline__ void pair_issue_k(const __amdgpu_buffer_rsrc_t& rs, const PairWin& win,
+                                             uint32_t lo, float4* x, float* w) {
+  auto step = [&](auto uc) {
+    constexpr int u = decltype(uc)::value;
+    const uint32_t o = (uint32_t)half_bcast<KW + u>((int)win.o);
+    w[u] = __builtin_bit_cast(float, half_bcast<KW + u>(__builtin_bit_cast(int, win.w)));
+    if constexpr (DBG & 1) {
+      x[u] = make_float4(__builtin_bit_cast(float, o), 0.f, 0.f, 0.f);
+    } else {
+      x[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, o + lo, 0, 0));
+    }
+  };
+  [&]<int... U>(std::integer_sequence<int, U...>) {
+    (step(std::integral_constant<int, U>{}), ...);
+  }(std::make_integer_sequence<int, kPairG>{});
+}
+
+// issue the gathers of steps k0 .. k0+G-1 (window slot (k0 & 31) / G)
+template <int DBG = 0>
+__device__ __forceinline__ void pair_issue(const __amdgpu_buffer_rsrc_t& rs, const PairWin& win,
+                                           int k0, uint32_t lo, float4* x, float* w) {
+  static_assert(kPairG == 8, "window slots assume 8-step groups");
+  switch ((k0 >> 3) & 3) {
+    case 0: pair_issue_k<DBG, 0>(rs, win, lo, x, w); break;
+    case 1: pair_issue_k<DBG, 8>(rs, win, lo, x, w); break;
+    case 2: pair_issue_k<DBG, 16>(rs, win, lo, x, w); break;
+    default: pair_issue_k<DBG, 24>(rs, win, lo, x, w); break;
+  }
+}
+
+// acc += w * x per column with separate IEEE mul and add (-ffp-contract=off),
+// written as explicit 2-wide vectors: one v_pk_mul_f32 + one v_pk_add_f32 per
+// column pair (left to the SLP vectoriser, the scalar form was re-paired
+// across edges with v_mov shuffles)
+typedef float pair_f2 __attribute__((ext_vector_type(2)));
+
+template <int DBG = 0>
+__device__ __forceinline__ void pair_add(const float4* x, const float* w, pair_f2& lo,
+                                         pair_f2& hi) {
+#pragma unroll
+  for (int u = 0; u < kPairG; ++u) {
+    if constexpr (DBG & 8) {
+      asm volatile("" ::"v"(x[u].x), "v"(x[u].y), "v"(x[u].z), "v"(x[u].w), "v"(w[u]));
+      continue;
+    }
+    const pair_f2 ww = {w[u], w[u]};
+    const pair_f2 a = {x[u].x, x[u].y};
+    const pair_f2 b = {x[u].z, x[u].w};
+    lo = lo + ww * a;
+    hi = hi + ww * b;
+  }
+}
+
+__device__ __forceinline__ void pair_segs(const PairArgs& a, int sb, int se, int q, int4& s0,
+                                          int4& s1) {
+  const int i0 = sb + 2 * q;
+  const int4 t0 = a.segs[i0];
+  const int4 t1 = i0 + 1 < se ? a.segs[i0 + 1] : make_int4(0, 0, -1, 0);
+  // wave-uniform records: keep them in SGPRs
+  s0 = make_int4(__builtin_amdgcn_readfirstlane(t0.x), __builtin_amdgcn_readfirstlane(t0.y),
+                 __builtin_amdgcn_readfirstlane(t0.z), 0);
+  s1 = make_int4(__builtin_amdgcn_readfirstlane(t1.x), __builtin_amdgcn_readfirstlane(t1.y),
+                 __builtin_amdgcn_readfirstlane(t1.z), 0);
+}
+
+// Waves of XCD x walk that XCD's pairs with a stride.  The next pair's
+// window loads are issued behind the current pair's first gathers, and the
+// segment records of the pair after that one pair earlier still (scalar
+// loads).  (A software pipeline over 8-step groups — the next group's gathers
+// issued before the current group's adds — measured 20% slower: 102 VGPRs,
+// 4 waves/SIMD, against 64 VGPRs and 8 waves/SIMD here.)
+template <int DBG>
+__global__ void __launch_bounds__(kSpmmThreads)
+spmm_pair_kernel(PairArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int half = lane >> 5;
+  const int c = lane & 31;
+  const int xcd = blockIdx.x % kNumXcd;
+  const int wx = __builtin_amdgcn_readfirstlane((blockIdx.x / kNumXcd) * (kSpmmThreads / 64) +
+                                                (threadIdx.x >> 6));
+  const int nwx = (gridDim.x / kNumXcd) * (kSpmmThreads / 64);
+  const int sb = __builtin_amdgcn_readfirstlane(a.hdr[2 + xcd]);
+  const int se = __builtin_amdgcn_readfirstlane(a.hdr[3 + xcd]);
+  const int npairs = (se - sb + 1) >> 1;
+  if (wx >= npairs) return;
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.ubase, 0, a.span, 0x00020000);
+  const uint32_t lo = (uint32_t)c * 16;
+  int q = wx;
+  int4 s0, s1, n0, n1;
+  pair_segs(a, sb, se, q, s0, s1);
+  PairWin win = pair_window(a, half ? s1.x : s0.x, half ? s1.y : s0.y, 0, c);
+  if (q + nwx < npairs) pair_segs(a, sb, se, q + nwx, n0, n1);
+  while (true) {
+    const int qn = q + nwx;
+    const int my_start = half ? s1.x : s0.x;
+    const int my_len = half ? s1.y : s0.y;
+    const int emax = max(s0.y, s1.y);
+    pair_f2 alo = {0.f, 0.f}, ahi = {0.f, 0.f};
+    float4 x[kPairG];
+    float w[kPairG];
+    if (emax > 0) pair_issue<DBG>(rs, win, 0, lo, x, w);
+    // next pair: its window now, the one after's segment records
+    PairWin nwin{a.span, 0.f};
+    int4 m0 = make_int4(0, 0, -1, 0), m1 = m0;
+    if (qn < npairs) {
+      nwin = pair_window(a, half ? n1.x : n0.x, half ? n1.y : n0.y, 0, c);
+      if (qn + nwx < npairs) pair_segs(a, sb, se, qn + nwx, m0, m1);
+    }
+    if (emax > 0) pair_add<DBG>(x, w, alo, ahi);
+#pragma unroll 1
+    for (int k0 = kPairG; k0 < emax; k0 += kPairG) {   // segments longer than kPairG
+      if ((k0 & 31) == 0) win = pair_window(a, my_start, my_len, k0, c);
+      pair_issue<DBG>(rs, win, k0, lo, x, w);
+      pair_add<DBG>(x, w, alo, ahi);
+    }
+    const float4 acc = make_float4(alo.x, alo.y, ahi.x, ahi.y);
+    const int d = half ? s1.z : s0.z;
+    if (DBG & 2) {
+      if (acc.x == 1234.5f) a.out[0] = acc.y;   // keep the sums alive
+    } else if (d >= 0) {
+      *reinterpret_cast<float4*>(a.out + (int64_t)d * a.ldo + c * 4) = acc;
+    } else if (d <= -2) {
+      *reinterpret_cast<float4*>(a.carry + (int64_t)(-d - 2) * 128 + c * 4) = acc;
+    }
+    if (qn >= npairs) break;
+    q = qn;
+    s0 = n0;
+    s1 = n1;
+    n0 = m0;
+    n1 = m1;
+    win = nwin;
+  }
+}
+
+// long rows: out[row] = piece0 + piece1 + ... in order; one half-wave per row,
+// up to 8 piece loads in flight ahead of the in-order adds
+__global__ void __launch_bounds__(kSpmmThreads)
+spmm_pair_fixup_kernel(PairArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int c = lane & 31;
+  const int nlong = a.hdr[1];
+  const int nh = gridDim.x * (kSpmmThreads / 32);
+  for (int h = blockIdx.x * (kSpmmThreads / 32) + (threadIdx.x >> 5); h < nlong; h += nh) {
+    const int4 lr = a.longrows[h];
+    const float4* p = reinterpret_cast<const float4*>(a.carry + (int64_t)lr.y * 128) + c;
+    float4 acc = p[0];
+    for (int i = 1; i < lr.z; i += 8) {
+      float4 t[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) t[u] = i + u < lr.z ? p[(int64_t)(i + u) * 32] : acc;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        if (i + u < lr.z) {
+          acc.x = __fadd_rn(acc.x, t[u].x);
+          acc.y = __fadd_rn(acc.y, t[u].y);
+          acc.z = __fadd_rn(acc.z, t[u].z);
+          acc.w = __fadd_rn(acc.w, t[u].w);
+        }
+      }
+    }
+    *reinterpret_cast<float4*>(a.out + (int64_t)lr.x * a.ldo + c * 4) = acc;
+  }
+}
+
+struct PairPlanWs {
+  int32_t *nseg, *nslot, *seg_off, *slot_off, *counter;
+  uint32_t *keys, *skeys, *iota, *sidx;
+  int4* useg;
+  void* temp;
+  size_t temp_bytes;
+};
+
+static size_t pair_temp_bytes(int64_t n_rows, int64_t cap) {
+  size_t a = 0, b = 0;
+  (void)rocprim::exclusive_scan(nullptr, a, (const int32_t*)nullptr, (int32_t*)nullptr, 0,
+                                (size_t)(n_rows > 0 ? n_rows : 1), rocprim::plus<int32_t>(),
+                                (hipStream_t)0);
+  (void)rocprim::radix_sort_pairs(nullptr, b, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                                  (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                                  (size_t)(cap > 0 ? cap : 1), 0, 32, (hipStream_t)0);
+  return a > b ? a : b;
+}
+
+static PairPlanWs pair_ws_layout(void* ws, int32_t n_rows, int64_t cap, size_t* total) {
+  PairPlanWs w{};
+  char* p = reinterpret_cast<char*>(ws);
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    char* q = p ? p + off : nullptr;
+    off += align_up(bytes > 0 ? bytes : 1, 256);
+    return q;
+  };
+  const size_t nr = (size_t)(n_rows > 0 ? n_rows : 1);
+  w.nseg = (int32_t*)take(nr * 4);
+  w.nslot = (int32_t*)take(nr * 4);
+  w.seg_off = (int32_t*)take(nr * 4);
+  w.slot_off = (int32_t*)take(nr * 4);
+  w.counter = (int32_t*)take(256);
+  w.keys = (uint32_t*)take((size_t)cap * 4);
+  w.skeys = (uint32_t*)take((size_t)cap * 4);
+  w.iota = (uint32_t*)take((size_t)cap * 4);
+  w.sidx = (uint32_t*)take((size_t)cap * 4);
+  w.useg = (int4*)take((size_t)cap * 16);
+  w.temp_bytes = pair_temp_bytes(n_rows, cap);
+  w.temp = take(w.temp_bytes);
+  if (total) *total = off;
+  return w;
+}
+
+}  // namespace vqgnn
+
+using namespace vqgnn;
+
+extern "C" int vqgnn_spmm_pair_supported(int32_t F) { return F == 128 ? 1 : 0; }
+
+extern "C" int64_t vqgnn_spmm_pair_plan_size(int32_t n_rows, int64_t nnz, int32_t F) {
+  if (n_rows < 0 || nnz < 0 || F <= 0) return 0;
+  const int S = spmm_chunk_edges((F + 3) / 4), L = spmm_long_row(S);
+  return kPairHdr + 4 * pair_seg_cap(n_rows, nnz, S, L) + 4 * pair_long_cap(nnz, L);
+}
+
+extern "C" size_t vqgnn_spmm_pair_plan_workspace(int32_t n_rows, int64_t nnz, int32_t F) {
+  if (n_rows < 0 || nnz < 0 || F <= 0) return 256;
+  const int S = spmm_chunk_edges((F + 3) / 4), L = spmm_long_row(S);
+  size_t total = 0;
+  (void)pair_ws_layout(nullptr, n_rows, pair_seg_cap(n_rows, nnz, S, L), &total);
+  return total;
+}
+
+extern "C" int vqgnn_spmm_pair_plan(const int32_t* rowptr, int32_t n_rows, int64_t nnz,
+                                    int32_t F, int32_t B, int32_t* plan, void* workspace,
+                                    vqgnn_stream_t stream) {
+  clear_error();
+  VQGNN_REQUIRE(vqgnn_spmm_pair_supported(F), "spmm_pair_plan: F=%d unsupported", F);
+  VQGNN_REQUIRE(rowptr && plan && workspace && n_rows >= 0 && nnz >= 0 &&
+                    nnz < (int64_t)INT32_MAX,
+                "spmm_pair_plan: bad arguments");
+  VQGNN_REQUIRE(B >= 0 && B <= n_rows, "spmm_pair_plan: need 0 <= B <= n_rows (B=%d)", B);
+  VQGNN_REQUIRE((n_rows >> kPairWinShift) < (1 << 19), "spmm_pair_plan: too many rows");
+  hipStream_t s = as_stream(stream);
+  const int S = spmm_chunk_edges((F + 3) / 4), L = spmm_long_row(S);
+  const int64_t cap = pair_seg_cap(n_rows, nnz, S, L);
+  PairPlanWs w = pair_ws_layout(workspace, n_rows, cap, nullptr);
+  int32_t* hdr = plan;
+  int4* segs = reinterpret_cast<int4*>(plan + kPairHdr);
+  int4* longrows = segs + cap;
+  (void)hipMemsetAsync(w.counter, 0, 256, s);
+  if (n_rows == 0) {
+    (void)hipMemsetAsync(hdr, 0, kPairHdr * 4, s);
+    return check_launch("spmm_pair_plan(empty)");
+  }
+  const int nbk = (n_rows + 255) / 256;
+  hipLaunchKernelGGL(pair_count_kernel, dim3(nbk), dim3(256), 0, s, rowptr, n_rows, S, L, w.nseg,
+                     w.nslot);
+  size_t tb = w.temp_bytes;
+  hipError_t e = rocprim::exclusive_scan(w.temp, tb, w.nseg, w.seg_off, 0, (size_t)n_rows,
+                                         rocprim::plus<int32_t>(), s);
+  tb = w.temp_bytes;
+  if (e == hipSuccess)
+    e = rocprim::exclusive_scan(w.temp, tb, w.nslot, w.slot_off, 0, (size_t)n_rows,
+                                rocprim::plus<int32_t>(), s);
+  if (e != hipSuccess) {
+    set_error("spmm_pair_plan: scan failed (%s)", hipGetErrorString(e));
+    return VQGNN_ERR_LAUNCH;
+  }
+  const int cbk = (int)((cap + 255) / 256);
+  hipLaunchKernelGGL(pair_pad_kernel, dim3(cbk), dim3(256), 0, s, w.keys, w.iota, w.seg_off,
+                     w.nseg, n_rows, cap);
+  hipLaunchKernelGGL(pair_fill_kernel, dim3(nbk), dim3(256), 0, s, rowptr, n_rows, B, S, L,
+                     w.seg_off, w.slot_off, w.useg, w.keys, longrows, w.counter);
+  tb = w.temp_bytes;
+  e = rocprim::radix_sort_pairs(w.temp, tb, w.keys, w.skeys, w.iota, w.sidx, (size_t)cap, 0, 32,
+                                s);
+  if (e != hipSuccess) {
+    set_error("spmm_pair_plan: sort failed (%s)", hipGetErrorString(e));
+    return VQGNN_ERR_LAUNCH;
+  }
+  hipLaunchKernelGGL(pair_gather_kernel, dim3(cbk), dim3(256), 0, s, w.useg, w.sidx, w.skeys,
+                     segs, cap);
+  hipLaunchKernelGGL(pair_hdr_kernel, dim3(1), dim3(64), 0, s, w.skeys, cap, w.counter, hdr);
+  return check_launch("spmm_pair_plan");
+}
+
+extern "C" int vqgnn_spmm_pair(const int32_t* rowptr, const int32_t* col, const float* val,
+                               int32_t n_rows, int32_t n_cols, int64_t nnz, int32_t B,
+                               const float* X, int64_t ldx, const float* X2, int64_t ldx2,
+                               int32_t F, float* out, int64_t ldo, const int32_t* plan,
+                               const int32_t* chunk_plan, void* workspace,
+                               vqgnn_stream_t stream) {
+  clear_error();
+  VQGNN_REQUIRE(vqgnn_spmm_pair_supported(F), "spmm_pair: F=%d unsupported", F);
+  VQGNN_REQUIRE(rowptr && out && plan && n_rows >= 0, "spmm_pair: null pointer");
+  VQGNN_REQUIRE(ldx % 4 == 0 && ldo % 4 == 0 && ldx >= F && ldo >= F,
+                "spmm_pair: ldx/ldo must be multiples of 4 and >= F");
+  VQGNN_REQUIRE(!X2 || (ldx2 % 4 == 0 && ldx2 >= F && ((uintptr_t)X2 & 15) == 0),
+                "spmm_pair: X2 must be 16-byte aligned with ldx2 a multiple of 4, >= F");
+  VQGNN_REQUIRE(((uintptr_t)X & 15) == 0 && ((uintptr_t)out & 15) == 0,
+                "spmm_pair: X/out must be 16-byte aligned");
+  VQGNN_REQUIRE(nnz < (int64_t)INT32_MAX, "spmm_pair: nnz >= 2^31");
+  VQGNN_REQUIRE(n_cols >= 0 && (!X2 || (B >= 0 && B <= n_cols)),
+                "spmm_pair: need 0 <= B <= n_cols with X2 (n_cols=%d B=%d)", n_cols, B);
+  if (n_rows == 0 || nnz == 0)
+    return vqgnn_spmm(rowptr, col, val, n_rows, n_cols, nnz, B, X, ldx, X2, ldx2, F, out, ldo,
+                      chunk_plan, workspace, stream);
+  VQGNN_REQUIRE(col && val && X && workspace, "spmm_pair: null pointer");
+  SpmmArgs t{};
+  t.X = X;
+  t.ldx4 = ldx / 4;
+  t.X2 = X2;
+  t.ldx24 = X2 ? ldx2 / 4 : 0;
+  const int64_t rows_x = X2 ? B : n_cols, rows_x2 = X2 ? (int64_t)n_cols - B : 0;
+  // X and X2 more than 4 GiB apart: the chunk kernels (64-bit row addresses)
+  if (!wave_layout(t, rows_x, rows_x2) || t.span > 0xFFFFF000u)
+    return vqgnn_spmm(rowptr, col, val, n_rows, n_cols, nnz, B, X, ldx, X2, ldx2, F, out, ldo,
+                      chunk_plan, workspace, stream);
+  PairArgs a;
+  a.col = col;
+  a.val = val;
+  a.hdr = plan;
+  a.segs = reinterpret_cast<const int4*>(plan + kPairHdr);
+  const int S = spmm_chunk_edges(F / 4), L = spmm_long_row(S);
+  a.longrows = a.segs + pair_seg_cap(n_rows, nnz, S, L);
+  a.ubase = t.ubase;
+  a.span = t.span;
+  a.offx = t.offx;
+  a.ldxb = t.ldxb;
+  a.offx2 = t.offx2;
+  a.ldx2b = t.ldx2b;
+  a.B = X2 ? B : INT32_MAX;
+  a.out = out;
+  a.ldo = ldo;
+  a.carry = reinterpret_cast<float*>(workspace);
+  hipStream_t s = as_stream(stream);
+  static const int bpc = env_int("VQGNN_PAIR_BPC", 8);   // workgroups per CU
+  const int grid = 256 * (bpc > 0 ? bpc : 8);
+  static const int dbg = env_int("VQGNN_SPMM_DEBUG", 0);
+  a.dbg = dbg;
+  switch (a.dbg & 11) {
+    case 0: hipLaunchKernelGGL(spmm_pair_kernel<0>, dim3(grid), dim3(kSpmmThreads), 0, s, a); break;
+    case 1: hipLaunchKernelGGL(spmm_pair_kernel<1>, dim3(grid), dim3(kSpmmThreads), 0, s, a); break;
+    case 2: hipLaunchKernelGGL(spmm_pair_kernel<2>, dim3(grid), dim3(kSpmmThreads), 0, s, a); break;
+    case 8: hipLaunchKernelGGL(spmm_pair_kernel<8>, dim3(grid), dim3(kSpmmThreads), 0, s, a); break;
+    case 10: hipLaunchKernelGGL(spmm_pair_kernel<10>, dim3(grid), dim3(kSpmmThreads), 0, s, a); break;
+    default: hipLaunchKernelGGL(spmm_pair_kernel<3>, dim3(grid), dim3(kSpmmThreads), 0, s, a); break;
+  }
+  hipLaunchKernelGGL(spmm_pair_fixup_kernel, dim3(256), dim3(kSpmmThreads), 0, s, a);
+  return check_launch("spmm_pair");
 }

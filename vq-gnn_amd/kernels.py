@@ -205,6 +205,31 @@ def spmm_plan(rowptr, n_rows, nnz, F):
     return plan
 
 
+class PairPlan:
+    """Segment plan of a CSR for vqgnn_spmm_pair (include/vqgnn.h §6d): built
+    for feature width F, batch split B and rows [0, n_rows); ``chunk`` is the
+    chunk plan (§6b) the call falls back to when X and X2 are far apart."""
+
+    def __init__(self, buf, F, B, n_rows, chunk=None):
+        self.buf, self.F, self.B, self.n_rows, self.chunk = buf, F, B, n_rows, chunk
+
+
+def spmm_pair_supported(F) -> bool:
+    return bool(lib().vqgnn_spmm_pair_supported(int(F)))
+
+
+def spmm_pair_plan(rowptr, n_rows, nnz, F, B, chunk=None):
+    """Build the segment-pair plan (device-side, once per batch adjacency)."""
+    L = lib()
+    dev = rowptr.device
+    m = L.vqgnn_spmm_pair_plan_size(int(n_rows), int(nnz), int(F))
+    buf = torch.empty(max(m, 1), dtype=torch.int32, device=dev)
+    ws = workspace(L.vqgnn_spmm_pair_plan_workspace(int(n_rows), int(nnz), int(F)), dev)
+    check(L.vqgnn_spmm_pair_plan(ptr(rowptr), int(n_rows), int(nnz), int(F), int(B), ptr(buf),
+                                 ptr(ws), stream_ptr()), "spmm_pair_plan")
+    return PairPlan(buf, int(F), int(B), int(n_rows), chunk)
+
+
 def spmm(rowptr, col, val, n_rows, nnz, X, F, X2=None, B=None, out=None, plan=None):
     """out[i] = sum_e val[e] * xin[col[e]]; xin = X rows (< B), X2 rows (>= B).
     Every column index must be < the rows of xin (X rows, or B + X2 rows)."""
@@ -218,6 +243,16 @@ def spmm(rowptr, col, val, n_rows, nnz, X, F, X2=None, B=None, out=None, plan=No
     n_cols = Bv + X2.shape[0] if X2 is not None else X.shape[0]
     if X2 is not None and X.shape[0] < Bv:
         raise ValueError(f"spmm: X has {X.shape[0]} rows < B={Bv}")
+    if isinstance(plan, PairPlan):
+        if plan.F != F or plan.n_rows != int(n_rows):
+            raise ValueError(f"spmm: pair plan built for F={plan.F}, n_rows={plan.n_rows}; "
+                             f"called with F={F}, n_rows={n_rows}")
+        check(L.vqgnn_spmm_pair(ptr(rowptr), ptr(col), ptr(val), int(n_rows), int(n_cols),
+                                int(nnz), Bv, ptr(X), _ld(X), ptr(X2),
+                                _ld(X2) if X2 is not None else 0, F, ptr(out), _ld(out),
+                                ptr(plan.buf), ptr(plan.chunk), ptr(ws), stream_ptr()),
+              "spmm_pair")
+        return out
     check(L.vqgnn_spmm(ptr(rowptr), ptr(col), ptr(val), int(n_rows), int(n_cols), int(nnz), Bv,
                        ptr(X), _ld(X),
                        ptr(X2), _ld(X2) if X2 is not None else 0, F, ptr(out), _ld(out),
@@ -237,6 +272,8 @@ def spmm_codes(rowptr, col, val, n_rows, nnz, X, F, lcodes, emb_out, D, B, out=N
     (j >= B) — x_input = cat([x, x_first_order]) of models.py:168-174 without
     materialising x_first_order.  lcodes: gather_codewords(..., want_x=False,
     want_codes=True)."""
+    if isinstance(plan, PairPlan):   # the code-source kernel walks chunks
+        plan = plan.chunk
     require_gpu(X, "spmm_codes")
     dev = X.device
     nb, M = emb_out.shape[0], emb_out.shape[1]
