@@ -396,6 +396,31 @@ int vqgnn_partition(const int64_t* rowptr, const int32_t* col, int64_t N, int32_
                     int64_t* perm, int64_t* ptr, int32_t* iterations, void* workspace,
                     vqgnn_stream_t stream);
 
+/* ------------------------------------------------------------------------ *
+ * 11. VQ-GNN v1 compressed adjacency: mapper(batch, c,
+ *     num_M, gnn_type) of vq_gnn_v1/utils/dataloader.py:144-192, called per
+ *     branch at vq_gnn_v1/models.py:170.  Inputs (device): A_BN COO (bn_row =
+ *     local batch row, bn_col = global node, bn_val) of E entries; nb_val
+ *     (A_NB_v, may be NULL); A_BB COO in local ids (bb_* NULL: no A_BB) of E2
+ *     entries with batch_idx [B]; codes: int16 codeword of node j at
+ *     codes[j*ldc] (one branch of the node-major c_indices); deg_inv [B]
+ *     (self-loop values; unused for SAGE).  Output: CSR of dim = B + M,
+ *     out_rowptr int64 [dim+1], out_col int32 / out_val fp32 of capacity
+ *     vqgnn_mapper_capacity(...), out_nnz (device int64).  Coalescing sums
+ *     repeated (row, col) sequentially in concatenation order (stable radix
+ *     sort + one thread per key = torch_sparse coalesce's segment_csr);
+ *     status (device int64) = 1 if a code is outside [0, M).
+ * ------------------------------------------------------------------------ */
+int64_t vqgnn_mapper_capacity(int64_t E, int64_t E2, int32_t B, int32_t has_nb, int32_t has_bb,
+                              int32_t conv_type);
+size_t vqgnn_mapper_workspace(int64_t E, int64_t E2, int32_t B, int32_t has_nb, int32_t has_bb);
+int vqgnn_mapper(const int32_t* bn_row, const int32_t* bn_col, const float* bn_val, int64_t E,
+                 const float* nb_val, const int32_t* bb_row, const int32_t* bb_col,
+                 const float* bb_val, int64_t E2, const int64_t* batch_idx, int32_t B,
+                 const int16_t* codes, int64_t ldc, int32_t M, const float* deg_inv,
+                 int32_t conv_type, int64_t* out_rowptr, int32_t* out_col, float* out_val,
+                 int64_t* out_nnz, int64_t* status, void* workspace, vqgnn_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -117,6 +117,13 @@ SIGNATURES = {
     "vqgnn_partition_workspace": (_size, [_i64]),
     "vqgnn_partition": (ctypes.c_int, [_c_void_p, _c_void_p, _i64, _i32, _c_void_p, _c_void_p,
                                        _c_void_p, _c_void_p, _c_void_p]),
+    # §11 v1 compressed adjacency
+    "vqgnn_mapper_capacity": (_i64, [_i64, _i64, _i32, _i32, _i32, _i32]),
+    "vqgnn_mapper_workspace": (_size, [_i64, _i64, _i32, _i32, _i32]),
+    "vqgnn_mapper": (ctypes.c_int, [_c_void_p, _c_void_p, _c_void_p, _i64, _c_void_p, _c_void_p,
+                                    _c_void_p, _c_void_p, _i64, _c_void_p, _i32, _c_void_p, _i64,
+                                    _i32, _c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p,
+                                    _c_void_p, _c_void_p, _c_void_p, _c_void_p]),
     "vqgnn_coo_to_csr_workspace": (_size, [_i64, _i64, _i64]),
     "vqgnn_coo_to_csr": (ctypes.c_int, [_c_void_p, _c_void_p, _c_void_p, _i64, _i64, _i64,
                                         _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,

@@ -533,3 +533,50 @@ def partition(rowptr, col, N, num_parts):
     check(L.vqgnn_partition(ptr(rowptr), ptr(col), int(N), int(num_parts), ptr(perm), ptr(ptr_),
                             ctypes.addressof(steps), ptr(ws), stream_ptr()), "partition")
     return perm[:N], ptr_, int(steps.value)
+
+
+_CONV = {"GCN": 0, "SAGE": 1, "GAT": 2}
+
+
+def mapper(bn, c, num_B, num_M, gnn_type="GCN", nb_val=None, bb=None, batch_idx=None,
+           deg_inv=None):
+    """vqgnn_mapper (include/vqgnn.h §11): the v1 compressed (B+M)^2 adjacency
+    as (rowptr int64 [B+M+1], col int32, val fp32) device tensors.
+    bn = (row, col, val) of A_BN; c = int16 codes of one branch ([N], any
+    stride); bb = (row, col, val) of A_BB in local ids or None."""
+    require_gpu(bn[2], "mapper")
+    dev = bn[2].device
+    L = lib()
+    i32 = lambda t: t.to(device=dev, dtype=torch.int32).contiguous()
+    f32 = lambda t: t.to(device=dev, dtype=torch.float32).contiguous()
+    r, j, v = i32(bn[0]), i32(bn[1]), f32(bn[2])
+    E = int(v.numel())
+    nbv = f32(nb_val) if nb_val is not None else None
+    if bb is not None:
+        br, bs, bv = i32(bb[0]), i32(bb[1]), f32(bb[2])
+        E2 = int(bv.numel())
+        bi = batch_idx.to(device=dev, dtype=torch.int64).contiguous()
+    else:
+        br = bs = bv = bi = None
+        E2 = 0
+    if c.dtype != torch.int16:
+        raise ValueError("mapper: codes must be int16 (c_indices)")
+    ldc = c.stride(0) if c.dim() == 1 else c.stride(0)
+    conv = _CONV[gnn_type] if gnn_type in _CONV else _CONV["GAT"]
+    di = f32(deg_inv) if deg_inv is not None else None
+    B, M = int(num_B), int(num_M)
+    cap = L.vqgnn_mapper_capacity(E, E2, B, int(nbv is not None), int(bb is not None), conv)
+    rowptr = torch.empty(B + M + 1, dtype=torch.int64, device=dev)
+    col = torch.empty(max(cap, 1), dtype=torch.int32, device=dev)
+    val = torch.empty(max(cap, 1), dtype=torch.float32, device=dev)
+    nnz = torch.zeros(1, dtype=torch.int64, device=dev)
+    status = torch.zeros(1, dtype=torch.int64, device=dev)
+    ws = workspace(L.vqgnn_mapper_workspace(E, E2, B, int(nbv is not None), int(bb is not None)),
+                   dev)
+    check(L.vqgnn_mapper(ptr(r), ptr(j), ptr(v), E, ptr(nbv), ptr(br), ptr(bs), ptr(bv), E2,
+                         ptr(bi), B, ptr(c), ldc, M, ptr(di), conv, ptr(rowptr), ptr(col),
+                         ptr(val), ptr(nnz), ptr(status), ptr(ws), stream_ptr()), "mapper")
+    n = int(nnz.item())
+    if int(status.item()) != 0:
+        raise ValueError("mapper: a codeword index is outside [0, num_M)")
+    return rowptr, col[:n], val[:n]

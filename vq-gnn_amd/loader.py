@@ -193,3 +193,18 @@ class OurDataLoader(torch.utils.data.DataLoader):
 
 
 __all__ = ["DeviceGraph", "SubgraphBatch", "OurDataLoader", "prepare_batch_input"]
+
+
+def mapper(batch, c, num_M, gnn_type, device=None):
+    """VQ-GNN v1 ``mapper`` (vq_gnn_v1/utils/dataloader.py:144-192) on the
+    device: ``batch = (deg_inv, A_BN, A_BB, A_NB_v, batch_idx)`` as the v1
+    collate returns it (A_BN / A_BB as (row, col, value) COO triples, A_BB
+    and A_NB_v may be None); ``c`` the branch's codes (int16 ``c_indices``).
+    Returns the (B+M) x (B+M) adjacency as a ``CSR`` (torch_sparse
+    ``SparseTensor`` surface), GCN symmetrised, as the reference does."""
+    deg_inv, A_BN, A_BB, A_NB_v, batch_idx = batch
+    B = int(batch_idx.shape[0])
+    rowptr, col, val = kernels.mapper(A_BN, c, B, num_M, gnn_type, nb_val=A_NB_v, bb=A_BB,
+                                      batch_idx=batch_idx, deg_inv=deg_inv)
+    dim = B + int(num_M)
+    return CSR(rowptr, col, val, (dim, dim))
