@@ -24,7 +24,11 @@ neighbour is replaced by its codeword node ``B + c[j]``:
 
 Third-party semantics restated: torch_sparse ``coalesce`` / ``SparseStorage``
 (sort + ``segment_csr``), ``SparseTensor.to_symmetric(reduce='sum')``.  The
-sorts are taken as stable (CPU ``torch.sort`` / ``argsort``).  The reference
+sorts are taken as stable.  CPU ``torch.argsort`` (stable=False, what
+torch_sparse calls) is not stable at every size on torch 2.10 (checked: it
+differs from the stable order at 1,000 keys, matches at 10 and 10^5), so for a
+(row, col) repeated three or more times the reference's own summation order
+is unspecified; the stable order is the deterministic choice.  The reference
 ships no fixtures for this function: parity is pinned by the hand-computed
 known answers in ``tests/test_mapper_oracle.py``.
 """
@@ -107,3 +111,51 @@ def mapper(bn_row, bn_col, bn_val, c, num_B, num_M, gnn_type="GCN", nb_val=None,
     rowptr = np.zeros(dim + 1, np.int64)
     np.add.at(rowptr, r + 1, 1)
     return np.cumsum(rowptr), cc, s.astype(np.float32)
+
+
+def mapper_torch(bn_row, bn_col, bn_val, c, num_B, num_M, gnn_type="GCN", nb_val=None, bb=None,
+                 batch_idx=None, deg_inv=None):
+    """The same op sequence in CPU torch tensors (the CPU baseline of
+    scripts/bench_mapper.py): torch.cat, a stable sort by row * dim + col,
+    index_add_ over the unique keys (sequential per key on the CPU), the
+    value > 0 mask, the self loops, a stable sort, and to_symmetric."""
+    import torch
+    B, M = int(num_B), int(num_M)
+    dim = B + M
+    cm = c[bn_col].long() + B
+    rows, cols, vals = [bn_row.long()], [cm], [bn_val]
+    if nb_val is not None:
+        rows.append(cm)
+        cols.append(bn_row.long())
+        vals.append(nb_val)
+    if bb is not None:
+        br, bs, bv = bb[0].long(), bb[1].long(), bb[2]
+        rows += [br, br]
+        cols += [bs, c[batch_idx[bs]].long() + B]
+        vals += [bv, -1.0 * bv]
+        if nb_val is not None:
+            rows.append(c[batch_idx[br]].long() + B)
+            cols.append(bs)
+            vals.append(-1.0 * bv)
+    key = torch.cat(rows) * dim + torch.cat(cols)
+    val = torch.cat(vals)
+
+    def coalesce(key, val):
+        key, perm = torch.sort(key, stable=True)
+        uk, inv = torch.unique_consecutive(key, return_inverse=True)
+        s = torch.zeros(uk.numel(), dtype=val.dtype).index_add_(0, inv, val[perm])
+        return uk, s
+
+    key, s = coalesce(key, val)
+    keep = s > 0
+    key, s = key[keep], s[keep]
+    if gnn_type != "SAGE":
+        loops = torch.arange(B, dtype=torch.int64)
+        key = torch.cat([key, loops * dim + loops])
+        s = torch.cat([s, deg_inv])
+    key, perm = torch.sort(key, stable=True)
+    s = s[perm]
+    if gnn_type == "GCN":
+        r, cc = key // dim, key % dim
+        key, s = coalesce(torch.cat([key, cc * dim + r]), torch.cat([s, s]))
+    return key, s

@@ -91,24 +91,43 @@ __global__ void mapper_heads_kernel(const unsigned long long* __restrict__ k, in
   if (i < n) head[i] = (i == 0 || k[i] != k[i - 1]) ? 1 : 0;
 }
 
-// one thread per unique key: sequential fp32 sum from 0 over its run (the
-// segment_csr loop); pos = inclusive scan of head.  keep_pos: drop sums <= 0
-// (the value_input > 0 slice) by writing a flag for the compaction.
-__global__ void mapper_segsum_kernel(const unsigned long long* __restrict__ k,
-                                     const float* __restrict__ v, const int32_t* __restrict__ head,
+// start of every run of equal keys: starts[pos[i] - 1] = i at each head;
+// starts[nu] = n closes the last run
+__global__ void mapper_starts_kernel(const int32_t* __restrict__ head,
                                      const int32_t* __restrict__ pos, int64_t n,
-                                     unsigned long long* __restrict__ uk, float* __restrict__ us,
-                                     int32_t* __restrict__ keep, int positive_only) {
+                                     int32_t* __restrict__ starts) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n || !head[i]) return;
+  if (i < n && head[i]) starts[pos[i] - 1] = (int32_t)i;
+  if (i == n - 1) starts[pos[i]] = (int32_t)n;
+}
+
+// one thread per unique key: sequential fp32 sum from 0 over its run (the
+// segment_csr loop), values fetched 8 at a time ahead of the in-order adds.
+// positive_only: keep flag = sum > 0 (the value_input > 0 slice).  The
+// padding key (dim*dim, above every entry, sorted last) is never summed.
+__global__ void mapper_segsum_kernel(const unsigned long long* __restrict__ k,
+                                     const float* __restrict__ v,
+                                     const int32_t* __restrict__ starts,
+                                     const int32_t* __restrict__ nu_dev,
+                                     unsigned long long* __restrict__ uk, float* __restrict__ us,
+                                     int32_t* __restrict__ keep, int positive_only,
+                                     unsigned long long pad) {
+  const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= *nu_dev) return;
+  const int64_t a = starts[u], b = starts[u + 1];
+  const unsigned long long key = k[a];
   float s = 0.f;
-  int64_t j = i;
-  do {
-    s = __fadd_rn(s, v[j]);
-    ++j;
-  } while (j < n && !head[j]);
-  const int64_t u = pos[i] - 1;
-  uk[u] = k[i];
+  if (key != pad) {
+    for (int64_t j = a; j < b; j += 8) {
+      float t[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) t[q] = j + q < b ? v[j + q] : 0.f;
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        if (j + q < b) s = __fadd_rn(s, t[q]);
+    }
+  }
+  uk[u] = key;
   us[u] = s;
   if (keep) keep[u] = positive_only ? (s > 0.f ? 1 : 0) : 1;
 }
@@ -142,7 +161,7 @@ __global__ void mapper_compact_kernel(const unsigned long long* __restrict__ uk,
 __global__ void mapper_sym_kernel(const unsigned long long* __restrict__ k,
                                   const float* __restrict__ v, const int64_t* __restrict__ count,
                                   int64_t dim, unsigned long long* __restrict__ k2,
-                                  float* __restrict__ v2, int64_t cap) {
+                                  float* __restrict__ v2, int64_t cap, unsigned long long pad) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t n = *count;
   if (i >= cap) return;
@@ -153,25 +172,26 @@ __global__ void mapper_sym_kernel(const unsigned long long* __restrict__ k,
     k2[n + i] = c * dim + r;
     v2[n + i] = v[i];
   } else if (i >= 2 * n && i < cap) {
-    k2[i] = ~0ull;   // padding sorts last
+    k2[i] = pad;   // padding sorts last
     v2[i] = 0.f;
   }
 }
 
 __global__ void mapper_pad_kernel(unsigned long long* __restrict__ k, float* __restrict__ v,
-                                  const int64_t* __restrict__ count, int64_t cap) {
+                                  const int64_t* __restrict__ count, int64_t cap,
+                                  unsigned long long pad) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < cap && i >= *count) {
-    k[i] = ~0ull;
+    k[i] = pad;
     v[i] = 0.f;
   }
 }
 
 __global__ void mapper_count_kernel(const int32_t* __restrict__ nu,
                                     const unsigned long long* __restrict__ k,
-                                    int64_t* __restrict__ count) {
+                                    int64_t* __restrict__ count, unsigned long long pad) {
   const int64_t m = *nu;
-  *count = (m > 0 && k[m - 1] == ~0ull) ? m - 1 : m;
+  *count = (m > 0 && k[m - 1] == pad) ? m - 1 : m;
 }
 
 // CSR from sorted keys: rowptr[r] = first entry with row >= r; col, val
@@ -206,7 +226,7 @@ static int key_bits(int64_t dim) {
 struct MapperWs {
   unsigned long long *k0, *k1, *k2;
   float *v0, *v1, *v2;
-  int32_t *head, *pos, *keep, *kpos, *nu;
+  int32_t *head, *pos, *keep, *kpos, *nu, *starts;
   int64_t* count;
   void* temp;
   size_t temp_bytes;
@@ -236,6 +256,7 @@ static MapperWs mapper_ws(void* ws, int64_t cap, size_t* total) {
   w.pos = (int32_t*)take(c * 4);
   w.keep = (int32_t*)take(c * 4);
   w.kpos = (int32_t*)take(c * 4);
+  w.starts = (int32_t*)take(c * 4 + 4);
   w.nu = (int32_t*)take(256);
   w.count = (int64_t*)take(256);
   size_t a = 0, b = 0;
@@ -255,7 +276,7 @@ static MapperWs mapper_ws(void* ws, int64_t cap, size_t* total) {
 static hipError_t sort_coalesce(MapperWs& w, unsigned long long* k_in, float* v_in, int64_t n,
                                 int bits, unsigned long long* k_out, float* v_out,
                                 unsigned long long* uk, float* us, int positive_only,
-                                hipStream_t s) {
+                                unsigned long long pad, hipStream_t s) {
   size_t tb = w.temp_bytes;
   hipError_t e = rocprim::radix_sort_pairs(w.temp, tb, k_in, k_out, v_in, v_out, (size_t)n, 0,
                                            bits, s);
@@ -265,10 +286,12 @@ static hipError_t sort_coalesce(MapperWs& w, unsigned long long* k_in, float* v_
   tb = w.temp_bytes;
   e = rocprim::inclusive_scan(w.temp, tb, w.head, w.pos, (size_t)n, rocprim::plus<int32_t>(), s);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(mapper_segsum_kernel, dim3(nbk), dim3(256), 0, s, k_out, v_out, w.head,
-                     w.pos, n, uk, us, w.keep, positive_only);
   // unique count = pos[n-1]
   (void)hipMemcpyAsync(w.nu, w.pos + (n - 1), sizeof(int32_t), hipMemcpyDeviceToDevice, s);
+  hipLaunchKernelGGL(mapper_starts_kernel, dim3(nbk), dim3(256), 0, s, w.head, w.pos, n,
+                     w.starts);
+  hipLaunchKernelGGL(mapper_segsum_kernel, dim3(nbk), dim3(256), 0, s, k_out, v_out, w.starts,
+                     w.nu, uk, us, w.keep, positive_only, pad);
   return hipSuccess;
 }
 
@@ -318,7 +341,9 @@ extern "C" int vqgnn_mapper(const int32_t* bn_row, const int32_t* bn_col, const 
   (void)hipMemsetAsync(status, 0, sizeof(int64_t), s);
   (void)hipMemsetAsync(w.count, 0, sizeof(int64_t), s);
   (void)hipMemsetAsync(w.nu, 0, sizeof(int32_t), s);
-  const int bits = key_bits(dim);
+  // keys are row * dim + col < dim^2; dim^2 pads the fixed-capacity sorts
+  const unsigned long long pad = (unsigned long long)dim * (unsigned long long)dim;
+  const int bits = key_bits(dim) + 1;
   MapperIn a{bn_row, bn_col, bn_val, nb_val, E, bb_row, bb_col, bb_val, bb ? E2 : 0,
              batch_idx, B, M, codes, ldc, status};
   hipError_t e = hipSuccess;
@@ -326,7 +351,7 @@ extern "C" int vqgnn_mapper(const int32_t* bn_row, const int32_t* bn_col, const 
     hipLaunchKernelGGL(mapper_build_kernel, dim3((n_in + 255) / 256), dim3(256), 0, s, a, n_in,
                        w.k0, w.v0);
     // coalesce(): stable sort + sequential sums, then value > 0
-    e = sort_coalesce(w, w.k0, w.v0, n_in, bits, w.k1, w.v1, w.k2, w.v2, 1, s);
+    e = sort_coalesce(w, w.k0, w.v0, n_in, bits, w.k1, w.v1, w.k2, w.v2, 1, pad, s);
     if (e == hipSuccess) {
       size_t tb = w.temp_bytes;
       e = rocprim::inclusive_scan(w.temp, tb, w.keep, w.kpos, (size_t)n_in,
@@ -346,10 +371,10 @@ extern "C" int vqgnn_mapper(const int32_t* bn_row, const int32_t* bn_col, const 
   const int64_t n1 = n_in + (loops ? B : 0);   // capacity of the list
   // SparseTensor(row=, col=, value=): stable sort (self loops behind equal keys)
   hipLaunchKernelGGL(mapper_pad_kernel, dim3((n1 + 255) / 256 + 1), dim3(256), 0, s, w.k0, w.v0,
-                     w.count, n1);
+                     w.count, n1, pad);
   size_t tb = w.temp_bytes;
   if (n1 > 0)
-    e = rocprim::radix_sort_pairs(w.temp, tb, w.k0, w.k1, w.v0, w.v1, (size_t)n1, 0, 64, s);
+    e = rocprim::radix_sort_pairs(w.temp, tb, w.k0, w.k1, w.v0, w.v1, (size_t)n1, 0, bits, s);
   if (e != hipSuccess) {
     set_error("mapper: sort failed: %s", hipGetErrorString(e));
     return VQGNN_ERR_LAUNCH;
@@ -360,14 +385,14 @@ extern "C" int vqgnn_mapper(const int32_t* bn_row, const int32_t* bn_col, const 
     // to_symmetric(): [A ; A^T] sorted, repeats summed sequentially
     const int64_t n2 = 2 * n1;
     hipLaunchKernelGGL(mapper_sym_kernel, dim3((n2 + 255) / 256), dim3(256), 0, s, w.k1, w.v1,
-                       w.count, dim, w.k0, w.v0, n2);
-    e = sort_coalesce(w, w.k0, w.v0, n2, 64, w.k1, w.v1, w.k2, w.v2, 0, s);
+                       w.count, dim, w.k0, w.v0, n2, pad);
+    e = sort_coalesce(w, w.k0, w.v0, n2, bits, w.k1, w.v1, w.k2, w.v2, 0, pad, s);
     if (e != hipSuccess) {
       set_error("mapper: symmetric coalesce failed: %s", hipGetErrorString(e));
       return VQGNN_ERR_LAUNCH;
     }
-    // the padding keys (~0) form one trailing unique key: not an entry
-    hipLaunchKernelGGL(mapper_count_kernel, dim3(1), dim3(1), 0, s, w.nu, w.k2, w.count);
+    // the padding keys form one trailing unique key: not an entry
+    hipLaunchKernelGGL(mapper_count_kernel, dim3(1), dim3(1), 0, s, w.nu, w.k2, w.count, pad);
     fk = w.k2;
     fv = w.v2;
   }

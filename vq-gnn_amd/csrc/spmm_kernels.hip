@@ -833,7 +833,6 @@ __device__ __forceinline__ void flat_chunk(const SpmmArgs& a, const FlatSrc& f, 
                                            RowWindow& rw, int chunk, int i0, int lane) {
   const int e0 = chunk * a.S;
   const int e1 = min(e0 + a.S, a.nnz);
-  const bool last = e1 == a.nnz;
   const int F = a.F4 * 4;
   const int64_t ldo = a.ldo4 * 4;
   const bool st = !(a.dbg & 2);
