@@ -406,8 +406,7 @@ def test_pair_arxiv_batch_bit_identical():
     F = 128
     X = torch.randn(b.B, F, device=DEV)
     X2 = torch.randn(b.n - b.B, F, device=DEV)
-    pp = adj.plan(F, B=b.B)
-    assert isinstance(pp, kernels.PairPlan)
+    pp = kernels.spmm_pair_plan(adj.rowptr, b.n, b.nnz, F, b.B)
     got = kernels.spmm(adj.rowptr, adj.col, adj.value, b.n, b.nnz, X, F, X2=X2, B=b.B, plan=pp)
     chunk = kernels.spmm_plan(adj.rowptr, b.n, b.nnz, F)
     ref = kernels.spmm(adj.rowptr, adj.col, adj.value, b.n, b.nnz, X, F, X2=X2, B=b.B, plan=chunk)
