@@ -7,6 +7,10 @@ One step = one layer step on a synthetic arxiv-shaped mini-batch (SURVEY.md §8d
         EMA finalize), c_indices scattered in place;
   (ii)  codeword gather for the B' out-of-batch rows (x_first_order);
   (iii) two-source CSR SpMM over all nnz edges, all n rows.
+With update() semantics the EMA finalize is queued after (ii)+(iii): the
+gather reads the codebook from before this step's update, as the reference's
+forward does (its update runs in the backward hook, models.py:181-185), and
+with N > 1 the all-reduce of the EMA statistics overlaps (ii)+(iii).
 value = edges of all ranks / time.  Inputs are resident in HBM before timing.
 
 Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
@@ -122,11 +126,11 @@ def main():
     ev = []
 
     def step(record):
-        e = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if record else None
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(5)] if record else None
         if record:
             e[0].record()
         if W == 2 * D:
-            bank.update(Xd, Gd, 0, nb, True, codes=codes, batch_idx=bidx)
+            bank.update(Xd, Gd, 0, nb, True, codes=codes, batch_idx=bidx, defer=True)
         else:
             bank.feature_update(Xd, 0, nb, True, codes=codes, batch_idx=bidx)
         if record:
@@ -147,9 +151,12 @@ def main():
         else:
             kernels.spmm(adj.rowptr, adj.col, adj.value, n, nnz, Xd, F, X2=x_first, B=B,
                          plan=spmm_plan)
-        bank.sync_codes()   # multi-GPU: other ranks' codes, exchanged behind gather + SpMM
         if record:
             e[3].record()
+        bank.finish_update()  # EMA finalize (multi-GPU: after the overlapped all-reduce)
+        bank.sync_codes()   # multi-GPU: other ranks' codes, exchanged behind gather + SpMM
+        if record:
+            e[4].record()
             ev.append(e)
 
     def barrier():
@@ -199,7 +206,8 @@ def main():
     ms_step = dt / args.steps * 1e3
     value = total_edges * args.steps / dt
 
-    vq_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
+    # VQ update = BN + assign (e0 -> e1) + the deferred finalize (e3 -> e4)
+    vq_ms = float(np.mean([e[0].elapsed_time(e[1]) + e[3].elapsed_time(e[4]) for e in ev]))
     gather_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in ev]))
     spmm_ms = float(np.mean([e[2].elapsed_time(e[3]) for e in ev]))
     assign_ms = float(np.mean([a.elapsed_time(b) for a, b in assign_ev]))

@@ -31,8 +31,10 @@ class CodebookSync:
         self.world = dist.get_world_size(group)
         self._count_cache = {}
 
-    def allreduce_(self, t: torch.Tensor) -> None:
-        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+    def allreduce_(self, t: torch.Tensor, async_op: bool = False):
+        """In-place sum over the ranks; async_op=True returns the work (its
+        wait() orders the current stream after the collective)."""
+        return dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=async_op)
 
     def global_count(self, B: int) -> int:
         if B in self._count_cache:

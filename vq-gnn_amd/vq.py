@@ -77,6 +77,11 @@ class VQBank(nn.Module):
         # multi-GPU: codes of the other ranks' batches arrive asynchronously
         # (dist.PendingCodes); sync_codes() lands them
         self._pending_codes = None
+        # update(defer=True): the finalize (and, multi-GPU, the wait for the
+        # asynchronous all-reduce of the EMA statistics) left for
+        # finish_update(), so work that reads the pre-update codebook (the
+        # reference forward's gather + aggregation) runs in between
+        self._pending_finalize = None
         # last batched call's logging stash (vq.py:208-214, :276-277)
         self.last_batch = None       # [4, nb*D] mean_f, std_f, mean_g, std_g
         self.last_inputs = None      # (X, G) of the last update()
@@ -155,6 +160,7 @@ class VQBank(nn.Module):
 
     def feature_update(self, X, b0, nbr, training, idx_out=None, codes=None, batch_idx=None):
         """vq.py:160-202 for branches [b0, b0+nbr): X is [B, nbr*D] (a row-major view)."""
+        self.finish_update()
         self.sync_codes()
         D, F = self.D, nbr * self.D
         sl = self._sel(b0, nbr)
@@ -202,8 +208,31 @@ class VQBank(nn.Module):
             self._clean(D, b0, nbr)
             self._finish()
 
-    def update(self, X, G, b0, nbr, training, idx_out=None, codes=None, batch_idx=None):
-        """vq.py:204-279 for branches [b0, b0+nbr): X, G are [B, nbr*D] views."""
+    def finish_update(self):
+        """Complete an update(defer=True): wait for the EMA-statistics
+        all-reduce (multi-GPU; a stream wait, not a host wait) and run the
+        finalize.  A no-op when nothing is pending."""
+        p, self._pending_finalize = self._pending_finalize, None
+        if p is None:
+            return
+        work, fin_args, fin_kw, clean = p
+        if work is not None:
+            work.wait()
+        kernels.vq_ema_finalize(*fin_args, **fin_kw)
+        self._clean(*clean)
+        self._finish()
+
+    def update(self, X, G, b0, nbr, training, idx_out=None, codes=None, batch_idx=None,
+               defer=False):
+        """vq.py:204-279 for branches [b0, b0+nbr): X, G are [B, nbr*D] views.
+
+        defer=True (training): return after the assign with the finalize
+        pending (finish_update()); multi-GPU, the all-reduce of the EMA
+        statistics is then asynchronous and overlaps what the caller queues
+        before finish_update().  Until then emb / emb_out hold the codebook
+        from before this update, as the reference's forward sees it (the
+        hook's update runs after the aggregation, models.py:181-185)."""
+        self.finish_update()
         self.sync_codes()
         D, F = self.D, nbr * self.D
         sl = self._sel(b0, nbr)
@@ -247,19 +276,25 @@ class VQBank(nn.Module):
             stats = self._assign(X, G, coef, scale, self.emb[sl], D, 2 * D,
                                  idx_out=idx_out, codes=codes, batch_idx=batch_idx,
                                  want_stats=training, stat_count=count, stats_out=slab)
+        work = None
         if comm is not None:
             stats = kernels.vq_ema_reduce(stats)
-            comm.allreduce_(stats)
-            if local is not None:
-                self._exchange_codes(batch_idx, local, codes)
+            if defer:
+                if local is not None:      # codes first: the all-reduce is waited on later
+                    self._exchange_codes(batch_idx, local, codes)
+                work = comm.allreduce_(stats, async_op=True)
+            else:
+                comm.allreduce_(stats)
+                if local is not None:
+                    self._exchange_codes(batch_idx, local, codes)
         if training:
-            kernels.vq_ema_finalize(stats, D, 2 * D, self.decay, self.warm_up_flag, scale,
-                                    self.epsilon, self.cs[sl], self.ema_w[sl], self.emb[sl],
-                                    self.emb_out[sl], self.rm_f[sl], self.rv_f[sl],
-                                    self.rm_g[sl], self.rv_g[sl], self.bad_flag, count,
-                                    zero_after=True)
-            self._clean(2 * D, b0, nbr)
-            self._finish()
+            fin_args = (stats, D, 2 * D, self.decay, self.warm_up_flag, scale, self.epsilon,
+                        self.cs[sl], self.ema_w[sl], self.emb[sl], self.emb_out[sl],
+                        self.rm_f[sl], self.rv_f[sl], self.rm_g[sl], self.rv_g[sl],
+                        self.bad_flag, count)
+            self._pending_finalize = (work, fin_args, dict(zero_after=True), (2 * D, b0, nbr))
+            if not defer:
+                self.finish_update()
 
 
 class _BNView(nn.Module):
