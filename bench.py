@@ -44,6 +44,9 @@ def parse():
     # rehearsal of the N>1 path on one GPU: --backend gloo with
     # VQGNN_BENCH_ONE_DEVICE=1 puts every rank on cuda:0
     p.add_argument("--backend", default="nccl", choices=["nccl", "gloo"])
+    # rehearsal of the multi-GPU host path on one process (world size 1 under
+    # torch.distributed.run): the collectives run on a single rank
+    p.add_argument("--force-comm", action="store_true")
     # kernel events inside the timed region (the roofline kernel's launches);
     # off only to measure what they cost
     p.add_argument("--no-kernel-events", action="store_true")
@@ -74,7 +77,7 @@ def main():
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     comm = None
-    if world > 1:
+    if world > 1 or args.force_comm:
         if args.backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -176,6 +179,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step(False)
+    t_issue = time.perf_counter() - t0      # host time to enqueue the K steps
     torch.cuda.synchronize()
     barrier()
     t1 = time.perf_counter()
@@ -277,9 +281,10 @@ def main():
             kernels=dict(vq_update_ms=vq_ms, codeword_gather_ms=gather_ms, spmm_ms=spmm_ms,
                          spmm=rl_spmm, vq_assign=rl_vq),
             cpu_baseline=cpu,
+            host_issue_ms_per_step=t_issue / args.steps * 1e3,
         )
         print(json.dumps(out))
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

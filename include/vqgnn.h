@@ -396,6 +396,26 @@ int vqgnn_partition(const int64_t* rowptr, const int32_t* col, int64_t N, int32_
                     int64_t* perm, int64_t* ptr, int32_t* iterations, void* workspace,
                     vqgnn_stream_t stream);
 
+/* 5b. Multi-GPU code exchange wire format (keeps every replica's c_indices
+ *     identical; models.py:46/:63 across ranks).  A record per batch row:
+ *     int32 node id (-1 = padding), then nb codes as uint8 (M <= 256) or
+ *     int16, padded to 4 bytes (vqgnn_codes_wire_record).
+ *     vqgnn_pack_codes: rows [0, B) of (batch_idx, local [B][nb]) and
+ *     padding up to max_B into send; with codes != NULL also scatters them
+ *     into this rank's own c_indices at once.
+ *     vqgnn_scatter_wire: all ranks' records (rank-major, as
+ *     all_gather_into_tensor lays them out) into codes; a node held by
+ *     several records takes the LAST record's codes (deterministic: a
+ *     per-node atomicMax of the record index, then only the winner writes).
+ *     winner: int32 [N], all -1 on entry, all -1 again on exit.              */
+int32_t vqgnn_codes_wire_record(int32_t nb, int32_t M);
+int vqgnn_pack_codes(const int64_t* batch_idx, int32_t B, const int16_t* local, int32_t nb,
+                     int32_t M, int32_t max_B, uint8_t* send, int16_t* codes, int64_t ldc,
+                     vqgnn_stream_t stream);
+int vqgnn_scatter_wire(const uint8_t* recv, int64_t n_records, int32_t nb, int32_t M,
+                       int32_t* winner, int64_t N, int16_t* codes, int64_t ldc,
+                       vqgnn_stream_t stream);
+
 /* ------------------------------------------------------------------------ *
  * 11. VQ-GNN v1 compressed adjacency: mapper(batch, c,
  *     num_M, gnn_type) of vq_gnn_v1/utils/dataloader.py:144-192, called per

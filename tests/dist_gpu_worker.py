@@ -59,6 +59,16 @@ def main(out_dir):
         for k in ("emb", "emb_out", "ema_w", "cs", "rm_f", "rv_f", "rm_g", "rv_g"):
             res["ref_" + k] = getattr(ref, k).cpu().numpy()
         res["ref_codes"] = rc.cpu().numpy()
+    # repeated nodes across ranks: nodes 0..9 in both ranks' rows with
+    # rank-specific codes; every replica keeps the LAST record's (rank 1)
+    sync = bank.comm
+    c2 = torch.zeros(N, nb, dtype=torch.int16, device=dev)
+    ids = torch.cat([torch.arange(10), torch.arange(100 + 10 * rank, 110 + 10 * rank)]).to(dev)
+    loc = (torch.arange(20, device=dev)[:, None] + 7 * (rank + 1) +
+           torch.arange(nb, device=dev)[None]).to(torch.int16) % M
+    sync.start_codes_exchange(ids, loc.contiguous(), c2, max_B=24, M=M).wait()
+    torch.cuda.synchronize()
+    res["dup_codes"] = c2.cpu().numpy()
     np.savez(os.path.join(out_dir, f"r{rank}.npz"), **res)
     dist.barrier()
     dist.destroy_process_group()

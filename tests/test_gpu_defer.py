@@ -18,8 +18,8 @@ def _bank(nb, M, D):
     return bank.to(DEV)
 
 
-def test_deferred_finalize_same_state():
-    vqmod.STRICT_BAD_INIT = False
+def test_deferred_finalize_same_state(monkeypatch):
+    monkeypatch.setattr(vqmod, "STRICT_BAD_INIT", False)
     nb, M, D, B, N = 8, 64, 4, 3000, 5000
     X = torch.randn(B, nb * D, device=DEV)
     G = torch.randn(B, nb * D, device=DEV) * 1e-3

@@ -38,3 +38,11 @@ def test_two_ranks_match_union_batch(tmp_path):
         np.testing.assert_allclose(r0[k], r0["ref_" + k], rtol=1e-6, atol=1e-7)
     for k in ("emb", "emb_out", "ema_w", "cs"):
         np.testing.assert_allclose(r0[k], r0["ref_" + k], rtol=1e-5, atol=1e-6)
+    # repeated nodes across ranks: identical replicas, the last rank's codes
+    np.testing.assert_array_equal(r0["dup_codes"], r1["dup_codes"])
+    M, nb = 64, 6
+    last = (np.arange(10)[:, None] + 7 * 2 + np.arange(nb)[None]) % M
+    np.testing.assert_array_equal(r0["dup_codes"][:10], last)
+    for rk in range(2):
+        own = (np.arange(10, 20)[:, None] + 7 * (rk + 1) + np.arange(nb)[None]) % M
+        np.testing.assert_array_equal(r0["dup_codes"][100 + 10 * rk:110 + 10 * rk], own)

@@ -117,6 +117,12 @@ SIGNATURES = {
     "vqgnn_partition_workspace": (_size, [_i64]),
     "vqgnn_partition": (ctypes.c_int, [_c_void_p, _c_void_p, _i64, _i32, _c_void_p, _c_void_p,
                                        _c_void_p, _c_void_p, _c_void_p]),
+    # §5b multi-GPU code exchange
+    "vqgnn_codes_wire_record": (_i32, [_i32, _i32]),
+    "vqgnn_pack_codes": (ctypes.c_int, [_c_void_p, _i32, _c_void_p, _i32, _i32, _i32, _c_void_p,
+                                        _c_void_p, _i64, _c_void_p]),
+    "vqgnn_scatter_wire": (ctypes.c_int, [_c_void_p, _i64, _i32, _i32, _c_void_p, _i64, _c_void_p,
+                                          _i64, _c_void_p]),
     # §11 v1 compressed adjacency
     "vqgnn_mapper_capacity": (_i64, [_i64, _i64, _i32, _i32, _i32, _i32]),
     "vqgnn_mapper_workspace": (_size, [_i64, _i64, _i32, _i32, _i32]),

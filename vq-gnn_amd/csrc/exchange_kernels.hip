@@ -1,0 +1,134 @@
+// Multi-GPU code exchange wire format (no counterpart in the single-process
+// reference; keeps every replica's c_indices — models.py:46/:63 — identical).
+//
+// One record per batch row: int32 node id (-1 = padding) followed by the row's
+// nb codes as uint8 (M <= 256) or int16, padded to a multiple of 4 bytes.  A
+// rank packs its rows (and scatters them into its own c_indices at once), one
+// all_gather_into_tensor moves the records, and every rank scatters all of
+// them with "the last record wins" for a node several ranks hold — the order
+// of the union batch on one GPU (index_put with repeated indices writes in
+// order on the CPU).  The winner is chosen deterministically (an atomicMax of
+// the record index per node, then only the winner writes), so every replica
+// resolves repeats the same way; the per-node winner table returns to -1
+// after each scatter, so it needs one initialisation only.
+
+#include "common.h"
+
+namespace vqgnn {
+
+__host__ __device__ inline int wire_code_bytes(int M) { return M <= 256 ? 1 : 2; }
+__host__ __device__ inline int wire_record_bytes(int nb, int M) {
+  return (4 + nb * wire_code_bytes(M) + 3) / 4 * 4;
+}
+
+// one thread per row; the common shape (uint8 wire, nb % 4 == 0, aligned
+// rows) moves whole words: 8-byte reads of 4 codes, 4-byte record writes
+__global__ void pack_codes_kernel(const int64_t* __restrict__ batch_idx, int B,
+                                  const int16_t* __restrict__ local, int nb, int M, int max_B,
+                                  uint8_t* __restrict__ send, int16_t* __restrict__ codes,
+                                  int64_t ldc, int vec) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= max_B) return;
+  const int rec = wire_record_bytes(nb, M);
+  uint8_t* p = send + (int64_t)r * rec;
+  if (r >= B) {
+    *reinterpret_cast<int32_t*>(p) = -1;
+    return;
+  }
+  const int64_t node = batch_idx[r];
+  *reinterpret_cast<int32_t*>(p) = (int32_t)node;
+  const int16_t* l = local + (int64_t)r * nb;
+  int16_t* c = (codes && node >= 0) ? codes + node * ldc : nullptr;
+  if (vec) {
+    uint32_t* pw = reinterpret_cast<uint32_t*>(p + 4);
+    for (int b = 0; b < nb; b += 4) {
+      const uint2 t = *reinterpret_cast<const uint2*>(l + b);   // 4 int16 codes
+      pw[b / 4] = (t.x & 0xFFu) | ((t.x >> 16 & 0xFFu) << 8) | ((t.y & 0xFFu) << 16) |
+                  ((t.y >> 16 & 0xFFu) << 24);
+      if (c) *reinterpret_cast<uint2*>(c + b) = t;
+    }
+    return;
+  }
+  if (wire_code_bytes(M) == 1) {
+    for (int b = 0; b < nb; ++b) p[4 + b] = (uint8_t)l[b];
+  } else {
+    int16_t* q = reinterpret_cast<int16_t*>(p + 4);
+    for (int b = 0; b < nb; ++b) q[b] = l[b];
+  }
+  if (c)
+    for (int b = 0; b < nb; ++b) c[b] = l[b];
+}
+
+__global__ void wire_winner_kernel(const uint8_t* __restrict__ recv, int64_t n, int rec,
+                                   int64_t N, int32_t* __restrict__ winner) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int32_t node = *reinterpret_cast<const int32_t*>(recv + i * rec);
+  if (node >= 0 && node < N) atomicMax(winner + node, (int32_t)i);
+}
+
+__global__ void wire_scatter_kernel(const uint8_t* __restrict__ recv, int64_t n, int rec, int nb,
+                                    int M, int64_t N, int32_t* __restrict__ winner,
+                                    int16_t* __restrict__ codes, int64_t ldc, int vec) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint8_t* p = recv + i * rec;
+  const int32_t node = *reinterpret_cast<const int32_t*>(p);
+  if (node < 0 || node >= N || winner[node] != (int32_t)i) return;
+  int16_t* c = codes + (int64_t)node * ldc;
+  if (vec) {
+    const uint32_t* pw = reinterpret_cast<const uint32_t*>(p + 4);
+    for (int b = 0; b < nb; b += 4) {
+      const uint32_t w = pw[b / 4];
+      *reinterpret_cast<uint2*>(c + b) =
+          make_uint2((w & 0xFFu) | ((w >> 8 & 0xFFu) << 16), (w >> 16 & 0xFFu) | ((w >> 24) << 16));
+    }
+  } else if (wire_code_bytes(M) == 1) {
+    for (int b = 0; b < nb; ++b) c[b] = (int16_t)p[4 + b];
+  } else {
+    const int16_t* q = reinterpret_cast<const int16_t*>(p + 4);
+    for (int b = 0; b < nb; ++b) c[b] = q[b];
+  }
+  winner[node] = -1;   // only the winner clears: the losers compare against any other value
+}
+
+}  // namespace vqgnn
+
+using namespace vqgnn;
+
+extern "C" int32_t vqgnn_codes_wire_record(int32_t nb, int32_t M) {
+  return wire_record_bytes(nb, M);
+}
+
+extern "C" int vqgnn_pack_codes(const int64_t* batch_idx, int32_t B, const int16_t* local,
+                                int32_t nb, int32_t M, int32_t max_B, uint8_t* send,
+                                int16_t* codes, int64_t ldc, vqgnn_stream_t stream) {
+  clear_error();
+  VQGNN_REQUIRE(B >= 0 && max_B >= B && nb > 0 && M > 0 && M <= 32768,
+                "pack_codes: bad shape (B=%d max_B=%d nb=%d M=%d)", B, max_B, nb, M);
+  if (max_B == 0) return VQGNN_OK;
+  VQGNN_REQUIRE(send && (B == 0 || (batch_idx && local)), "pack_codes: null pointer");
+  // word-wise path: uint8 wire, 4 | nb, 8-byte aligned local rows and codes rows
+  const int vec = M <= 256 && nb % 4 == 0 && ((uintptr_t)local & 7) == 0 &&
+                  (!codes || (((uintptr_t)codes & 7) == 0 && ldc % 4 == 0));
+  hipLaunchKernelGGL(pack_codes_kernel, dim3((max_B + 255) / 256), dim3(256), 0,
+                     as_stream(stream), batch_idx, B, local, nb, M, max_B, send, codes, ldc, vec);
+  return check_launch("pack_codes");
+}
+
+extern "C" int vqgnn_scatter_wire(const uint8_t* recv, int64_t n_records, int32_t nb, int32_t M,
+                                  int32_t* winner, int64_t N, int16_t* codes, int64_t ldc,
+                                  vqgnn_stream_t stream) {
+  clear_error();
+  VQGNN_REQUIRE(n_records >= 0 && nb > 0 && M > 0 && N >= 0, "scatter_wire: bad shape");
+  if (n_records == 0) return VQGNN_OK;
+  VQGNN_REQUIRE(recv && winner && codes, "scatter_wire: null pointer");
+  const int rec = wire_record_bytes(nb, M);
+  const dim3 grid((unsigned)((n_records + 255) / 256));
+  hipLaunchKernelGGL(wire_winner_kernel, grid, dim3(256), 0, as_stream(stream), recv, n_records,
+                     rec, N, winner);
+  const int vec = M <= 256 && nb % 4 == 0 && ((uintptr_t)codes & 7) == 0 && ldc % 4 == 0;
+  hipLaunchKernelGGL(wire_scatter_kernel, grid, dim3(256), 0, as_stream(stream), recv, n_records,
+                     rec, nb, M, N, winner, codes, ldc, vec);
+  return check_launch("scatter_wire");
+}

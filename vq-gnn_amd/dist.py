@@ -30,6 +30,7 @@ class CodebookSync:
         self.count_group = count_group
         self.world = dist.get_world_size(group)
         self._count_cache = {}
+        self._wire = {}       # persistent code-exchange buffers per shape
 
     def allreduce_(self, t: torch.Tensor, async_op: bool = False):
         """In-place sum over the ranks; async_op=True returns the work (its
@@ -89,11 +90,30 @@ class CodebookSync:
         kernels.scatter_codes(all_idx.to(torch.int64), all_loc.to(torch.int16), codes)
 
     def start_codes_exchange(self, batch_idx, local, codes, max_B=None, M=32767):
-        """Asynchronous allgather_codes_: returns a PendingCodes whose wait()
-        scatters the gathered codes (call it before ``codes`` is next read
-        for nodes of other ranks' batches)."""
-        pending, all_idx, all_loc = self.gather_codes(batch_idx, local, max_B, M, async_op=True)
-        return PendingCodes(pending, all_idx, all_loc, codes)
+        """Asynchronous code exchange on the device (include/vqgnn.h §5b): the
+        rank's rows packed into a persistent send buffer (and scattered into
+        its own ``codes`` at once), one all_gather_into_tensor, and a
+        PendingCodes whose wait() scatters every rank's records with "the
+        last record wins" for repeated nodes (the same on every replica).
+        Call wait() before ``codes`` is next read for other ranks' nodes."""
+        B, nb = local.shape
+        if max_B is None:
+            max_B = self.global_max(B)
+        send, recv, winner = self._wire_buffers(max_B, nb, M, codes.shape[0], local.device)
+        kernels.pack_codes(batch_idx, local, M, max_B, send, codes=codes)
+        work = dist.all_gather_into_tensor(recv, send, group=self.group, async_op=True)
+        return PendingWire(work, recv, self.world * max_B, nb, M, winner, codes)
+
+    def _wire_buffers(self, max_B, nb, M, N, device):
+        key = (max_B, nb, M, N, str(device))
+        buf = self._wire.get(key)
+        if buf is None:
+            rec = kernels.codes_wire_record(nb, M)
+            send = torch.empty(max_B * rec, dtype=torch.uint8, device=device)
+            recv = torch.empty(self.world * max_B * rec, dtype=torch.uint8, device=device)
+            winner = torch.full((N,), -1, dtype=torch.int32, device=device)
+            buf = self._wire[key] = (send, recv, winner)
+        return buf
 
 
     def global_max(self, B: int) -> int:
@@ -116,6 +136,20 @@ class PendingCodes:
         kernels.scatter_codes(self.all_idx.to(torch.int64), self.all_loc.to(torch.int16),
                               self.codes)
         self.works = []
+
+class PendingWire:
+    """An in-flight all_gather of packed code records (start_codes_exchange)."""
+
+    def __init__(self, work, recv, n_records, nb, M, winner, codes):
+        self.work, self.recv, self.n, self.nb, self.M = work, recv, n_records, nb, M
+        self.winner, self.codes = winner, codes
+
+    def wait(self):
+        if self.work is not None:
+            self.work.wait()
+            self.work = None
+            kernels.scatter_wire(self.recv, self.n, self.nb, self.M, self.winner, self.codes)
+
 
 def _device_of(group):
     backend = dist.get_backend(group)

@@ -188,6 +188,27 @@ def gather_codewords(subset, B, codes, emb_out, D, col_offset=0, want_x=True,
     return xt, lc
 
 
+def codes_wire_record(nb: int, M: int) -> int:
+    """Bytes per record of the multi-GPU code exchange (include/vqgnn.h §5b)."""
+    return int(lib().vqgnn_codes_wire_record(int(nb), int(M)))
+
+
+def pack_codes(batch_idx, local, M, max_B, send, codes=None):
+    """Records of (batch_idx, local codes) + padding into ``send`` (uint8);
+    with ``codes`` the rows are also scattered into this rank's c_indices."""
+    B, nb = local.shape
+    check(lib().vqgnn_pack_codes(ptr(batch_idx), B, ptr(local), nb, int(M), int(max_B), ptr(send),
+                                 ptr(codes), codes.stride(0) if codes is not None else 0,
+                                 stream_ptr()), "pack_codes")
+
+
+def scatter_wire(recv, n_records, nb, M, winner, codes):
+    """All ranks' records into ``codes``; the last record of a node wins."""
+    check(lib().vqgnn_scatter_wire(ptr(recv), int(n_records), int(nb), int(M), ptr(winner),
+                                   codes.shape[0], ptr(codes), codes.stride(0), stream_ptr()),
+          "scatter_wire")
+
+
 def scatter_codes(batch_idx: torch.Tensor, local: torch.Tensor, codes: torch.Tensor) -> None:
     """codes[batch_idx[i]] = local[i] (batch_idx < 0 entries are padding)."""
     B, nb = local.shape

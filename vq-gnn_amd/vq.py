@@ -125,8 +125,8 @@ class VQBank(nn.Module):
             p.wait()
 
     def _exchange_codes(self, batch_idx, local, codes):
-        """Own codes now (local scatter), everyone's asynchronously."""
-        kernels.scatter_codes(batch_idx, local, codes)
+        """Own codes now (scattered by the pack kernel), everyone's
+        asynchronously (landed by sync_codes)."""
         self._pending_codes = self.comm.start_codes_exchange(batch_idx, local, codes,
                                                              self.comm_max_B, self.M)
 
