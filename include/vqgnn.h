@@ -396,6 +396,14 @@ int vqgnn_partition(const int64_t* rowptr, const int32_t* col, int64_t N, int32_
                     int64_t* perm, int64_t* ptr, int32_t* iterations, void* workspace,
                     vqgnn_stream_t stream);
 
+/* 5a. Measurement (bench.py): vqgnn_assign_timing(1) starts recording every
+ *     vq_assign_kernel launch with a start/stop event pair taken by
+ *     hipExtLaunchKernel (the kernel's own duration); _read syncs on them and
+ *     writes up to cap durations in ms, returns the count; (0) stops and
+ *     frees the events.                                                       */
+int vqgnn_assign_timing(int32_t enable);
+int32_t vqgnn_assign_timing_read(float* ms, int32_t cap);
+
 /* 5b. Multi-GPU code exchange wire format (keeps every replica's c_indices
  *     identical; models.py:46/:63 across ranks).  A record per batch row:
  *     int32 node id (-1 = padding), then nb codes as uint8 (M <= 256) or

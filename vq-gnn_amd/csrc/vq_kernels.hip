@@ -14,6 +14,10 @@
 
 #include "common.h"
 
+#include <hip/hip_ext.h>
+
+#include <vector>
+
 #include <cfloat>
 #include <cstdlib>
 #include <cmath>
@@ -1151,6 +1155,26 @@ extern "C" size_t vqgnn_vq_assign_workspace(int32_t B, int32_t nb, int32_t M, in
   return g.fused ? 256 : align_up((size_t)nb * B * sizeof(int), 256);
 }
 
+// Measurement facility for bench.py: while enabled, every vq_assign_kernel
+// launch is issued with hipExtLaunchKernelGGL and a start/stop event pair, so
+// its duration is the kernel's own (no gap before the launch, unlike events
+// recorded around it on the stream).  Library-owned events, one mutex.
+static std::mutex g_timing_mu;
+static bool g_timing_on = false;
+static std::vector<std::pair<hipEvent_t, hipEvent_t>> g_timing_ev;
+
+static void timing_events(hipEvent_t* a, hipEvent_t* b) {
+  *a = *b = nullptr;
+  std::lock_guard<std::mutex> lk(g_timing_mu);
+  if (!g_timing_on) return;
+  if (hipEventCreate(a) != hipSuccess || hipEventCreate(b) != hipSuccess) {
+    (void)hipGetLastError();
+    *a = *b = nullptr;
+    return;
+  }
+  g_timing_ev.emplace_back(*a, *b);
+}
+
 template <int KC>
 static int launch_assign(const float* X, int64_t ldx, const float* G, int64_t ldg, int B,
                          int nb, int D, int M, int W, const float* coef, float grad_scale,
@@ -1178,10 +1202,12 @@ static int launch_assign(const float* X, int64_t ldx, const float* G, int64_t ld
     const void* fn = (const void*)vq_assign_kernel<KC, FU, WMV>;                              \
     if (lds > 64 * 1024)                                                                      \
       (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);    \
-    hipLaunchKernelGGL((vq_assign_kernel<KC, FU, WMV>), dim3(wgs), dim3(kAsgWaves * 64), lds, \
-                       s, X, ldx, G, ldg, B, nb, D, M, W, coef, grad_scale, emb, ldw,          \
-                       emb_bstride, idx_out, codes, ldc, batch_idx, idx32, parts,             \
-                       g.rows_per_part, g.chunk, sh.f, sh.g);                                 \
+    hipEvent_t ev0, ev1;                                                                      \
+    timing_events(&ev0, &ev1);                                                                \
+    hipExtLaunchKernelGGL((vq_assign_kernel<KC, FU, WMV>), dim3(wgs), dim3(kAsgWaves * 64),    \
+                          (uint32_t)lds, s, ev0, ev1, 0, X, ldx, G, ldg, B, nb, D, M, W, coef, \
+                          grad_scale, emb, ldw, emb_bstride, idx_out, codes, ldc, batch_idx,   \
+                          idx32, parts, g.rows_per_part, g.chunk, sh.f, sh.g);                \
   } while (0)
 #define VQ_LAUNCH_WM(FU)                                                                      \
   do {                                                                                        \
@@ -1298,4 +1324,31 @@ extern "C" int vqgnn_vq_ema_finalize(int64_t* ema_parts, int32_t nparts, int32_t
                      grad_scale, epsilon, cluster_size, cs_bstride, ema_w, embedding,
                      embedding_output, emb_bstride, rm_f, rv_f, rm_g, rv_g, bad_init);
   return check_launch("ema_finalize");
+}
+
+extern "C" int vqgnn_assign_timing(int32_t enable) {
+  std::lock_guard<std::mutex> lk(g_timing_mu);
+  for (auto& e : g_timing_ev) {
+    (void)hipEventDestroy(e.first);
+    (void)hipEventDestroy(e.second);
+  }
+  g_timing_ev.clear();
+  g_timing_on = enable != 0;
+  return VQGNN_OK;
+}
+
+extern "C" int32_t vqgnn_assign_timing_read(float* ms, int32_t cap) {
+  std::lock_guard<std::mutex> lk(g_timing_mu);
+  int32_t n = 0;
+  for (auto& e : g_timing_ev) {
+    if (n >= cap) break;
+    float t = 0.f;
+    if (hipEventSynchronize(e.second) != hipSuccess ||
+        hipEventElapsedTime(&t, e.first, e.second) != hipSuccess) {
+      (void)hipGetLastError();
+      t = -1.f;
+    }
+    ms[n++] = t;
+  }
+  return n;
 }
