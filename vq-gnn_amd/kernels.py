@@ -117,9 +117,10 @@ def vq_assign(X, G, coef, grad_scale, emb, D, W, idx_out=None, codes=None, batch
     L = lib()
     parts = None
     ws = None
+    # scratch: EMA row ids (non-fused) or the filtered path's row lists
+    ws = workspace(L.vqgnn_vq_assign_workspace(B, nb, M, W), X.device)
     if want_stats:
         P = L.vqgnn_vq_ema_parts(B, nb, M, W)
-        ws = workspace(L.vqgnn_vq_assign_workspace(B, nb, M, W), X.device)
     ldc = 0
     if codes is not None:
         if codes.dtype != torch.int16 or codes.stride(1) != 1:
