@@ -404,6 +404,16 @@ int vqgnn_partition(const int64_t* rowptr, const int32_t* col, int64_t N, int32_
 int vqgnn_assign_timing(int32_t enable);
 int32_t vqgnn_assign_timing_read(float* ms, int32_t cap);
 
+/* 5a'. Filtered assign (opt-in): for D = 4, W in {4, 8} and
+ *     one LDS-resident codebook, vqgnn_vq_assign first scores every codeword
+ *     with bf16-split MFMAs, resolves rows whose best and second-best scores
+ *     are more than twice the error bound apart exactly among 4 candidates,
+ *     and sends the remaining rows through the exact kernel (bit-identical
+ *     outputs either way; with timing on, one event span covers both).
+ *     mode 1 on, 0 off, -1 the VQGNN_ASSIGN_FILTER environment variable
+ *     (default off).                                                          */
+void vqgnn_assign_filter(int32_t mode);
+
 /* 5b. Multi-GPU code exchange wire format (keeps every replica's c_indices
  *     identical; models.py:46/:63 across ranks).  A record per batch row:
  *     int32 node id (-1 = padding), then nb codes as uint8 (M <= 256) or

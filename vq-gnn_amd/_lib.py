@@ -120,6 +120,7 @@ SIGNATURES = {
     # §5a measurement
     "vqgnn_assign_timing": (ctypes.c_int, [_i32]),
     "vqgnn_assign_timing_read": (_i32, [_c_void_p, _i32]),
+    "vqgnn_assign_filter": (None, [_i32]),
     # §5b multi-GPU code exchange
     "vqgnn_codes_wire_record": (_i32, [_i32, _i32]),
     "vqgnn_pack_codes": (ctypes.c_int, [_c_void_p, _i32, _c_void_p, _i32, _i32, _i32, _c_void_p,

@@ -17,6 +17,7 @@
 #include <hip/hip_ext.h>
 
 #include <vector>
+#include <atomic>
 
 #include <cfloat>
 #include <cstdlib>
@@ -337,6 +338,7 @@ constexpr size_t kLdsBudget = 160 * 1024;
 // codewords of LDS slack after each staged chunk: the sweep prefetches one
 // tile pair ahead without a bound check (staged as e = 0, |e|^2 = +inf)
 constexpr int kSweepSlack = 32;
+constexpr int kFilterSlack = 48;   // the filter sweep reads 64 codewords a step
 
 struct AssignGeom {
   int parts;          // row parts per branch (= EMA partial slabs)
@@ -924,17 +926,25 @@ __device__ __forceinline__ unsigned short f2bf(float v) {   // round to nearest 
   return (unsigned short)(u >> 16);
 }
 __device__ __forceinline__ float bf2f(unsigned short h) { return __uint_as_float((unsigned)h << 16); }
+// v rounded to bf16 (nearest even), kept as a float
+__device__ __forceinline__ float bf_round(float v) {
+  unsigned u = __float_as_uint(v);
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return __uint_as_float(u & 0xFFFF0000u);
+}
 
-__device__ __forceinline__ float vmed3(float a, float b, float c) {
+// v_min_f32 a, b with an unused operand `after`: the asm depends on it, so it
+// is scheduled after the instruction producing `after`
+__device__ __forceinline__ float vmin_after(float a, float b, float after) {
   float r;
-  asm("v_med3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b), "v"(after));
   return r;
 }
 
 // LDS bytes of the filter kernel: 4 bf16 planes of 16 B per codeword, |e|^2,
 // the bound constants, the fused EMA accumulators
 static size_t filter_lds_bytes(int M, int W, bool fused) {
-  const int mp = (M + 15) / 16 * 16 + kSweepSlack;
+  const int mp = (M + 15) / 16 * 16 + kFilterSlack;
   size_t b = (size_t)4 * mp * 16 + (size_t)mp * 4 + 16 * 4;
   if (fused) b = align_up(b, 8) + (size_t)M * (W + 1) * sizeof(unsigned long long);
   return b;
@@ -958,7 +968,7 @@ vq_assign_filter_kernel(const float* __restrict__ X, int64_t ldx,
   const int wg = xcd_remap(blockIdx.x, gridDim.x);
   const int b = wg % nb;
   const int part = wg / nb;
-  const int mp = (M + 15) / 16 * 16 + kSweepSlack;     // codewords per plane
+  const int mp = (M + 15) / 16 * 16 + kFilterSlack;    // codewords per plane
   char* fpl = reinterpret_cast<char*>(smem);             // [4][mp][16 B]
   float* se = reinterpret_cast<float*>(fpl + (size_t)4 * mp * 16);   // [mp]
   float* bnd = se + mp;                                  // [W] max|e_k|, [W] max|e|^2
@@ -1097,72 +1107,101 @@ vq_assign_filter_kernel(const float* __restrict__ X, int64_t ldx,
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
       float s = 0.f, t = 0.f;
-      unsigned short hh[W], ll[W];
 #pragma unroll
       for (int k = 0; k < W; ++k) {
         const float v = __shfl(xk[g][k >> 2], j + 16 * (k & 3));
         xr[g][k] = v;
         s = (k == 0) ? __fmul_rn(v, v) : __fadd_rn(s, __fmul_rn(v, v));
         t = fmaf(fabsf(v), bound_e[k], t);
-        const unsigned short h = f2bf(v);
-        hh[k] = f2bf(-2.f * v);
-        ll[k] = f2bf(-2.f * (v - bf2f(h)));
       }
       sx[g] = s;
       eps[g] = fmaf(t, 0x1p-13f, (bound_ee + s) * 0x1p-18f);
-      // slots 8q..8q+7 of [-2xh | -2xh | -2xl | 1 1 1 | 0...]
+      // this lane's slots 8q..8q+7 of [-2xh | -2xh | -2xl | 1 1 1 | 0...]:
+      // every non-constant slot i holds x[i % W], high part (-2h, exact) or
+      // low part (bf16(-2(x - h))), so one rounding path per slot:
+      // W = 8: q 0,1 high, q 2 low, q 3 constants;
+      // W = 4: q 0 high, q 1 low (i < 4) / constants, q 2,3 zero
+      const bool lo_lane = W == 8 ? (q == 2) : (q == 1);
       unsigned short sl[8];
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        unsigned short v0 = 0, v1 = 0, v2 = 0, v3 = 0;
-        auto slot = [&](int k) -> unsigned short {
-          if (k < W) return hh[k];
-          if (k < 2 * W) return hh[k - W];
-          if (k < 3 * W) return ll[k - 2 * W];
-          if (k < 3 * W + 3) return (unsigned short)0x3F80;
-          return (unsigned short)0;
-        };
-        v0 = slot(i);
-        v1 = slot(8 + i);
-        v2 = slot(16 + i);
-        v3 = slot(24 + i);
-        sl[i] = q == 0 ? v0 : (q == 1 ? v1 : (q == 2 ? v2 : v3));
+        const float v = xr[g][i % W];
+        const float h = bf_round(v);
+        const float u = lo_lane ? v - h : h;
+        const unsigned short val = (unsigned short)(__float_as_uint(bf_round(-2.f * u)) >> 16);
+        const unsigned short one = i < 3 ? (unsigned short)0x3F80 : (unsigned short)0;
+        unsigned short r;
+        if constexpr (W == 8) {
+          r = q == 3 ? one : val;
+        } else {
+          const unsigned short one4 = (i >= 4 && i < 7) ? (unsigned short)0x3F80 : (unsigned short)0;
+          r = q >= 2 ? (unsigned short)0 : ((q == 1 && i >= 4) ? one4 : val);
+        }
+        sl[i] = r;
       }
 #pragma unroll
       for (int i = 0; i < 8; ++i) bop[g][i] = (short)sl[i];
     }
 
     // ---- sweep: smallest and second-smallest score per lane, tile of the smallest
-    float m1[NG], m2[NG];
-    int mark[NG];
+    // Four tiles per iteration (the planes hold kFilterSlack >= 48 codewords
+    // of +inf slack past M rounded to 16), even and odd tiles into two
+    // independent (m1, m2, mark) sets so the min chains overlap.  Each score
+    // is first read by the compiler's v_med3 (the MFMA -> VALU wait states
+    // are only inserted for instructions the compiler emits); the running
+    // minimum is a plain v_min taking the new second-smallest as a dummy
+    // operand, so it is ordered after that read (fmed3(p1, v, -inf) would
+    // add canonicalising v_max on every score).
+    float m1[2][NG], m2[2][NG];
+    int mark[2][NG];
 #pragma unroll
-    for (int g = 0; g < NG; ++g) {
-      m1[g] = INFINITY;
-      m2[g] = INFINITY;
-      mark[g] = 0;
-    }
-    const char* lds = reinterpret_cast<const char*>(smem);
-    bf16x8 a_n = *reinterpret_cast<const bf16x8*>(lds + aoff);
-    for (int m0 = 0; m0 < M; m0 += 16) {
-      const bf16x8 a = a_n;
-      a_n = *reinterpret_cast<const bf16x8*>(lds + aoff + (uint32_t)(m0 + 16) * 16u);
+    for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
       for (int g = 0; g < NG; ++g) {
-        const floatx4 d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bop[g], floatx4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-        const float o = m1[g];
-        float p1 = m1[g], p2 = m2[g];
-#pragma unroll
-        // compiler builtins, not inline asm: the MFMA -> VALU read hazard
-        // (wait states) is only inserted for instructions the compiler
-        // emits; min(p1, v) = med3(p1, v, -inf)
-        for (int r = 0; r < 4; ++r) {
-          p2 = __builtin_amdgcn_fmed3f(p1, d[r], p2);
-          p1 = __builtin_amdgcn_fmed3f(p1, d[r], -INFINITY);
-        }
-        mark[g] = (p1 < o) ? m0 : mark[g];
-        m1[g] = p1;
-        m2[g] = p2;
+        m1[s2][g] = INFINITY;
+        m2[s2][g] = INFINITY;
+        mark[s2][g] = 0;
       }
+    const char* lds = reinterpret_cast<const char*>(smem);
+    for (int m0 = 0; m0 < M; m0 += 64) {
+      bf16x8 a[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        a[t] = *reinterpret_cast<const bf16x8*>(lds + aoff + (uint32_t)(m0 + 16 * t) * 16u);
+      floatx4 d[4][NG];
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int g = 0; g < NG; ++g)
+          d[t][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[t], bop[g], floatx4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int s2 = t & 1;
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+          const float o = m1[s2][g];
+          float p1 = o, p2 = m2[s2][g];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            p2 = __builtin_amdgcn_fmed3f(p1, d[t][g][r], p2);
+            p1 = vmin_after(p1, d[t][g][r], p2);
+          }
+          mark[s2][g] = (p1 < o) ? m0 + 16 * t : mark[s2][g];
+          m1[s2][g] = p1;
+          m2[s2][g] = p2;
+        }
+      }
+    }
+    float m1m[NG], m2m[NG];
+    int markm[NG];
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      // merge the two sets; an equal minimum in both makes the row undecided
+      // (r2 == r1), so either mark serves
+      const bool lo = m1[1][g] < m1[0][g];
+      m1m[g] = lo ? m1[1][g] : m1[0][g];
+      m2m[g] = fminf(fmaxf(m1[0][g], m1[1][g]), fminf(m2[0][g], m2[1][g]));
+      markm[g] = lo ? mark[1][g] : mark[0][g];
     }
 
     int bidx[NG];
@@ -1171,8 +1210,8 @@ vq_assign_filter_kernel(const float* __restrict__ X, int64_t ldx,
     for (int g = 0; g < NG; ++g) {
       // the row's two smallest scores over its 4 q-lanes, and the lowest
       // (tile, lane) holding the smallest
-      float r1 = m1[g], r2 = m2[g];
-      int key = mark[g] + 4 * q;
+      float r1 = m1m[g], r2 = m2m[g];
+      int key = markm[g] + 4 * q;
 #pragma unroll
       for (int sft = 16; sft <= 32; sft <<= 1) {
         const float o1 = __shfl_xor(r1, sft), o2 = __shfl_xor(r2, sft);
@@ -1540,9 +1579,16 @@ static void timing_events(hipEvent_t* a, hipEvent_t* b) {
 }
 
 // filtered path (§3b): D = 4 and W in {4 (features), 8 (features, grads)},
-// one codebook chunk, fused or no EMA statistics; VQGNN_ASSIGN_FILTER=0 off
+// one codebook chunk, fused or no EMA statistics.  Opt-in
+// (VQGNN_ASSIGN_FILTER=1): bit-exact, but measured no faster than the exact
+// kernel at arxiv_gcn (filter 155-160 us + 18 us list pass vs 172-184 us;
+// W = 4: 178 vs 117 us), DESIGN.md §4.1
+static std::atomic<int> g_filter_mode{-1};   // -1: VQGNN_ASSIGN_FILTER decides
+
 static bool filter_applies(int D, int W, int M, bool want_ema, bool fused) {
-  static const int on = env_int_vq("VQGNN_ASSIGN_FILTER", 1);
+  static const int env_on = env_int_vq("VQGNN_ASSIGN_FILTER", 0);
+  const int mode = g_filter_mode.load(std::memory_order_relaxed);
+  const int on = mode < 0 ? env_on : mode;
   if (!on || D != 4 || (W != 4 && W != 8) || (want_ema && !fused)) return false;
   return filter_lds_bytes(M, W, want_ema) <= kLdsBudget;
 }
@@ -1579,7 +1625,8 @@ static void launch_filter(const float* X, int64_t ldx, const float* G, int64_t l
                           int D, int M, const float* coef, float grad_scale, const float* emb,
                           int ldw, int64_t emb_bstride, int64_t* idx_out, int16_t* codes,
                           int64_t ldc, const int64_t* batch_idx, unsigned long long* parts,
-                          int shift_f, int shift_g, int* rlist, int* rcnt, hipStream_t s) {
+                          int shift_f, int shift_g, int* rlist, int* rcnt, hipEvent_t ev0,
+                          hipStream_t s) {
   const size_t lds = filter_lds_bytes(M, W, FU);
   const void* fn = (const void*)vq_assign_filter_kernel<W, FU>;
   if (lds > 64 * 1024)
@@ -1590,10 +1637,8 @@ static void launch_filter(const float* X, int64_t ldx, const float* G, int64_t l
   if (np < 1) np = 1;
   if (np > row_blocks) np = row_blocks;
   const int rpp = (B + np - 1) / np;
-  hipEvent_t ev0, ev1;
-  timing_events(&ev0, &ev1);
   hipExtLaunchKernelGGL((vq_assign_filter_kernel<W, FU>), dim3(np * nb), dim3(kAsgWaves * 64),
-                        (uint32_t)lds, s, ev0, ev1, 0, X, ldx, G, ldg, B, nb, D, M, coef,
+                        (uint32_t)lds, s, ev0, nullptr, 0, X, ldx, G, ldg, B, nb, D, M, coef,
                         grad_scale, emb, ldw, emb_bstride, idx_out, codes, ldc, batch_idx, parts,
                         rpp, shift_f, shift_g, rlist, rcnt);
 }
@@ -1624,7 +1669,10 @@ static int launch_assign(const float* X, int64_t ldx, const float* G, int64_t ld
   // decide go through the exact kernel below in its row-list mode
   const int* rlist = nullptr;
   const int* rcnt = nullptr;
+  // timing (bench): one span from the filter's start to the list pass's end
+  hipEvent_t tev0 = nullptr, tev1 = nullptr;
   if (workspace && filter_applies(D, W, M, want_ema, fused)) {
+    timing_events(&tev0, &tev1);
     int* cnt = reinterpret_cast<int*>(workspace);
     int* list = cnt + align_up((size_t)nb * sizeof(int), 256) / sizeof(int);
     (void)hipMemsetAsync(cnt, 0, (size_t)nb * sizeof(int), s);
@@ -1632,20 +1680,20 @@ static int launch_assign(const float* X, int64_t ldx, const float* G, int64_t ld
       if (want_ema)
         launch_filter<8, true>(X, ldx, G, ldg, B, nb, D, M, coef, grad_scale, emb, ldw,
                                emb_bstride, idx_out, codes, ldc, batch_idx, parts, sh.f, sh.g,
-                               list, cnt, s);
+                               list, cnt, tev0, s);
       else
         launch_filter<8, false>(X, ldx, G, ldg, B, nb, D, M, coef, grad_scale, emb, ldw,
                                 emb_bstride, idx_out, codes, ldc, batch_idx, parts, sh.f, sh.g,
-                                list, cnt, s);
+                                list, cnt, tev0, s);
     } else {
       if (want_ema)
         launch_filter<4, true>(X, ldx, G, ldg, B, nb, D, M, coef, grad_scale, emb, ldw,
                                emb_bstride, idx_out, codes, ldc, batch_idx, parts, sh.f, sh.g,
-                               list, cnt, s);
+                               list, cnt, tev0, s);
       else
         launch_filter<4, false>(X, ldx, G, ldg, B, nb, D, M, coef, grad_scale, emb, ldw,
                                 emb_bstride, idx_out, codes, ldc, batch_idx, parts, sh.f, sh.g,
-                                list, cnt, s);
+                                list, cnt, tev0, s);
     }
     int rc = check_launch("vq_assign_filter");
     if (rc) return rc;
@@ -1659,6 +1707,7 @@ static int launch_assign(const float* X, int64_t ldx, const float* G, int64_t ld
       (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);    \
     hipEvent_t ev0 = nullptr, ev1 = nullptr;                                                  \
     if (!rlist) timing_events(&ev0, &ev1);                                                    \
+    else ev1 = tev1;                                                                          \
     hipExtLaunchKernelGGL((vq_assign_kernel<KC, FU, WMV>), dim3(wgs), dim3(kAsgWaves * 64),    \
                           (uint32_t)lds, s, ev0, ev1, 0, X, ldx, G, ldg, B, nb, D, M, W, coef, \
                           grad_scale, emb, ldw, emb_bstride, idx_out, codes, ldc, batch_idx,   \
@@ -1689,6 +1738,10 @@ static int launch_assign(const float* X, int64_t ldx, const float* G, int64_t ld
                        sh.f, sh.g);
   }
   return check_launch("vq_ema_partial");
+}
+
+extern "C" void vqgnn_assign_filter(int32_t mode) {
+  g_filter_mode.store(mode < 0 ? -1 : (mode ? 1 : 0), std::memory_order_relaxed);
 }
 
 extern "C" int vqgnn_vq_assign(const float* X, int64_t ldx, const float* G, int64_t ldg,
