@@ -405,7 +405,9 @@ static int env_int_vq(const char* name, int dflt) {
 constexpr int kAsgWaves = 8;    // waves per workgroup
 constexpr int kAsgGroups = 2;   // 16-row groups per wave and iteration
 
-template <int KC, bool FUSED, int WM>
+// LIST: the row-list pass behind the filtered path (rows rlist[b*B + i],
+// i < rcnt[b]); the default instantiation carries none of it
+template <int KC, bool FUSED, int WM, bool LIST = false>
 __global__ void __launch_bounds__(kAsgWaves * 64)
 vq_assign_kernel(const float* __restrict__ X, int64_t ldx,
                  const float* __restrict__ Gr, int64_t ldg,
@@ -572,7 +574,7 @@ __device__ __forceinline__ void stage_chunk(const float* __restrict__ E, int ldw
   }
 }
 
-template <int KC, bool FUSED, int WM>
+template <int KC, bool FUSED, int WM, bool LIST>
 __global__ void __launch_bounds__(kAsgWaves * 64)
 vq_assign_kernel(const float* __restrict__ X, int64_t ldx,
                  const float* __restrict__ Gr, int64_t ldg,
@@ -631,12 +633,15 @@ vq_assign_kernel(const float* __restrict__ X, int64_t ldx,
   // rlist (the exact pass behind vq_assign_filter_kernel): this branch's rows
   // are rlist[b*B + i], i < rcnt[b], split over the parts in-kernel
   int b_rows = B, rpp = rows_per_part;
-  if (rlist) {
+  if constexpr (LIST) {
     b_rows = rcnt[b];
     const int nparts = (int)gridDim.x / nb;
     rpp = (b_rows + nparts - 1) / nparts;
   }
-  auto act = [&](int r) { return rlist ? rlist[(int64_t)b * B + r] : r; };
+  auto act = [&](int r) {
+    if constexpr (LIST) return rlist[(int64_t)b * B + r];
+    else return r;
+  };
   const int part_begin = part * rpp;
   const int part_end = min(b_rows, part_begin + rpp);
   const int n_iters = part_end > part_begin ? (part_end - part_begin + NG * 16 * WV - 1) /
@@ -1671,7 +1676,8 @@ static int launch_assign(const float* X, int64_t ldx, const float* G, int64_t ld
   const int* rcnt = nullptr;
   // timing (bench): one span from the filter's start to the list pass's end
   hipEvent_t tev0 = nullptr, tev1 = nullptr;
-  if (workspace && filter_applies(D, W, M, want_ema, fused)) {
+  if (workspace && filter_applies(D, W, M, want_ema, fused) &&
+      ((KC == 1 && wm == 1) || (KC == 2 && wm == 2))) {
     timing_events(&tev0, &tev1);
     int* cnt = reinterpret_cast<int*>(workspace);
     int* list = cnt + align_up((size_t)nb * sizeof(int), 256) / sizeof(int);
@@ -1700,18 +1706,30 @@ static int launch_assign(const float* X, int64_t ldx, const float* G, int64_t ld
     rlist = list;
     rcnt = cnt;
   }
-#define VQ_LAUNCH(FU, WMV)                                                                    \
+#define VQ_LAUNCH_L(FU, WMV, LI)                                                              \
   do {                                                                                        \
-    const void* fn = (const void*)vq_assign_kernel<KC, FU, WMV>;                              \
+    const void* fn = (const void*)vq_assign_kernel<KC, FU, WMV, LI>;                          \
     if (lds > 64 * 1024)                                                                      \
       (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);    \
     hipEvent_t ev0 = nullptr, ev1 = nullptr;                                                  \
-    if (!rlist) timing_events(&ev0, &ev1);                                                    \
+    if (!LI) timing_events(&ev0, &ev1);                                                       \
     else ev1 = tev1;                                                                          \
-    hipExtLaunchKernelGGL((vq_assign_kernel<KC, FU, WMV>), dim3(wgs), dim3(kAsgWaves * 64),    \
+    hipExtLaunchKernelGGL((vq_assign_kernel<KC, FU, WMV, LI>), dim3(wgs), dim3(kAsgWaves * 64),\
                           (uint32_t)lds, s, ev0, ev1, 0, X, ldx, G, ldg, B, nb, D, M, W, coef, \
                           grad_scale, emb, ldw, emb_bstride, idx_out, codes, ldc, batch_idx,   \
                           idx32, parts, g.rows_per_part, g.chunk, sh.f, sh.g, rlist, rcnt);   \
+  } while (0)
+  // the list pass exists for the filter's shapes only (W = D = 4: KC 1, WM 1;
+  // W = 2D = 8: KC 2, WM 2)
+#define VQ_LAUNCH(FU, WMV)                                                                    \
+  do {                                                                                        \
+    if constexpr ((KC == 1 && WMV == 1) || (KC == 2 && WMV == 2)) {                           \
+      if (rlist) {                                                                            \
+        VQ_LAUNCH_L(FU, WMV, true);                                                           \
+        break;                                                                                \
+      }                                                                                       \
+    }                                                                                         \
+    VQ_LAUNCH_L(FU, WMV, false);                                                              \
   } while (0)
 #define VQ_LAUNCH_WM(FU)                                                                      \
   do {                                                                                        \
@@ -1722,6 +1740,7 @@ static int launch_assign(const float* X, int64_t ldx, const float* G, int64_t ld
   if (fused) VQ_LAUNCH_WM(true); else VQ_LAUNCH_WM(false);
 #undef VQ_LAUNCH_WM
 #undef VQ_LAUNCH
+#undef VQ_LAUNCH_L
   int rc = check_launch("vq_assign");
   if (rc || !want_ema || fused) return rc;
   const size_t acc_bytes = (size_t)M * (W + 1) * sizeof(unsigned long long);
