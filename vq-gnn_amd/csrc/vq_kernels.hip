@@ -966,7 +966,7 @@ vq_assign_filter_kernel(const float* __restrict__ X, int64_t ldx,
                         const int64_t* __restrict__ batch_idx,
                         unsigned long long* __restrict__ partial,
                         int rows_per_part, int shift_f, int shift_g,
-                        int* __restrict__ rlist, int* __restrict__ rcnt) {
+                        int* __restrict__ rlist, int* __restrict__ rcnt, int m_sweep) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int KC = W / 4, NG = kAsgGroups, WV = kAsgWaves, NT = WV * 64;
   const int F = nb * D;
@@ -1168,7 +1168,7 @@ vq_assign_filter_kernel(const float* __restrict__ X, int64_t ldx,
         mark[s2][g] = 0;
       }
     const char* lds = reinterpret_cast<const char*>(smem);
-    for (int m0 = 0; m0 < M; m0 += 64) {
+    for (int m0 = 0; m0 < m_sweep; m0 += 64) {
       bf16x8 a[4];
 #pragma unroll
       for (int t = 0; t < 4; ++t)
@@ -1642,10 +1642,14 @@ static void launch_filter(const float* X, int64_t ldx, const float* G, int64_t l
   if (np < 1) np = 1;
   if (np > row_blocks) np = row_blocks;
   const int rpp = (B + np - 1) / np;
+  // codewords swept: M (VQGNN_FILTER_MSWEEP: a profiling knob that shortens
+  // the sweep and breaks the results; never set outside measurements)
+  static const int msw_env = env_int_vq("VQGNN_FILTER_MSWEEP", -1);
+  const int m_sweep = msw_env >= 0 && msw_env < M ? msw_env : M;
   hipExtLaunchKernelGGL((vq_assign_filter_kernel<W, FU>), dim3(np * nb), dim3(kAsgWaves * 64),
                         (uint32_t)lds, s, ev0, nullptr, 0, X, ldx, G, ldg, B, nb, D, M, coef,
                         grad_scale, emb, ldw, emb_bstride, idx_out, codes, ldc, batch_idx, parts,
-                        rpp, shift_f, shift_g, rlist, rcnt);
+                        rpp, shift_f, shift_g, rlist, rcnt, m_sweep);
 }
 
 template <int KC>
