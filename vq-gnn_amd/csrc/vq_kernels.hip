@@ -418,7 +418,7 @@ vq_assign_kernel(const float* __restrict__ X, int64_t ldx,
                  const int64_t* __restrict__ batch_idx,
                  int* __restrict__ idx32, unsigned long long* __restrict__ partial,
                  int rows_per_part, int chunk, int shift_f, int shift_g,
-                 const int* __restrict__ rlist, const int* __restrict__ rcnt);
+                 const int* __restrict__ rlist, const int* __restrict__ rcnt, int m_sweep);
 
 // k-slot layout: 0 general (W < 4*KC, padded), 1 W == 4*KC == D (features),
 // 2 W == 4*KC == 2*D (features then grads)
@@ -585,7 +585,7 @@ vq_assign_kernel(const float* __restrict__ X, int64_t ldx,
                  const int64_t* __restrict__ batch_idx,
                  int* __restrict__ idx32, unsigned long long* __restrict__ partial,
                  int rows_per_part, int chunk, int shift_f, int shift_g,
-                 const int* __restrict__ rlist, const int* __restrict__ rcnt) {
+                 const int* __restrict__ rlist, const int* __restrict__ rcnt, int m_sweep) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int NG = kAsgGroups, WV = kAsgWaves, NT = WV * 64, K4 = 4 * KC;
   const int F = nb * D;
@@ -793,7 +793,8 @@ vq_assign_kernel(const float* __restrict__ X, int64_t ldx,
       Frag<KC> a_n1 = lds_frag<KC>(reinterpret_cast<const float*>(lds + ao + 16 * KC * 4));
       float4 s_n0 = *reinterpret_cast<const float4*>(lds + so);
       float4 s_n1 = *reinterpret_cast<const float4*>(lds + so + 64);
-      for (int m0 = 0; m0 < mcount; m0 += 32) {
+      const int mlim = min(mcount, m_sweep);
+      for (int m0 = 0; m0 < mlim; m0 += 32) {
         const Frag<KC> a_0 = a_n0, a_1 = a_n1;
         const float4 s_0 = s_n0, s_1 = s_n1;
         a_n0 = lds_frag<KC>(reinterpret_cast<const float*>(lds + ao + 32 * KC * 4));
@@ -1721,7 +1722,8 @@ static int launch_assign(const float* X, int64_t ldx, const float* G, int64_t ld
     hipExtLaunchKernelGGL((vq_assign_kernel<KC, FU, WMV, LI>), dim3(wgs), dim3(kAsgWaves * 64),\
                           (uint32_t)lds, s, ev0, ev1, 0, X, ldx, G, ldg, B, nb, D, M, W, coef, \
                           grad_scale, emb, ldw, emb_bstride, idx_out, codes, ldc, batch_idx,   \
-                          idx32, parts, g.rows_per_part, g.chunk, sh.f, sh.g, rlist, rcnt);   \
+                          idx32, parts, g.rows_per_part, g.chunk, sh.f, sh.g, rlist, rcnt,    \
+                          m_sweep);                                                           \
   } while (0)
   // the list pass exists for the filter's shapes only (W = D = 4: KC 1, WM 1;
   // W = 2D = 8: KC 2, WM 2)
@@ -1741,6 +1743,10 @@ static int launch_assign(const float* X, int64_t ldx, const float* G, int64_t ld
     else if (wm == 2) VQ_LAUNCH(FU, 2);                                                       \
     else VQ_LAUNCH(FU, 0);                                                                    \
   } while (0)
+  // codewords swept per chunk: all (VQGNN_ASSIGN_MSWEEP: a profiling knob that
+  // shortens the sweep and breaks the results; never set outside measurements)
+  static const int msw_env = env_int_vq("VQGNN_ASSIGN_MSWEEP", -1);
+  const int m_sweep = msw_env >= 0 ? msw_env : (1 << 30);
   if (fused) VQ_LAUNCH_WM(true); else VQ_LAUNCH_WM(false);
 #undef VQ_LAUNCH_WM
 #undef VQ_LAUNCH
