@@ -1,5 +1,6 @@
-"""Debug (GPU): fallback counts of the filtered assign path and agreement with
-the exact path (VQGNN_ASSIGN_FILTER=0 build path) on the microbench data."""
+"""Debug (GPU): undecided-row counts of the filtered assign path (switched on
+here with vqgnn_assign_filter(1)), determinism, and agreement with an fp64
+argmin on the microbench data."""
 import os
 import sys
 
@@ -23,6 +24,7 @@ coef = torch.zeros(4, F, device=dev)
 coef[0] = 1.0
 coef[2] = 1.0
 L = lib()
+L.vqgnn_assign_filter(1)
 W = 2 * D
 for trial in range(2):
     ws = torch.zeros(L.vqgnn_vq_assign_workspace(B, nb, M, W) // 4 + 64, dtype=torch.int32,
