@@ -951,7 +951,7 @@ __device__ __forceinline__ float vmin_after(float a, float b, float after) {
 // the bound constants, the fused EMA accumulators
 static size_t filter_lds_bytes(int M, int W, bool fused) {
   const int mp = (M + 15) / 16 * 16 + kFilterSlack;
-  size_t b = (size_t)4 * mp * 16 + (size_t)mp * 4 + 16 * 4;
+  size_t b = (size_t)4 * mp * 16 + (size_t)mp * 4 + kAsgWaves * 16 * 4;
   if (fused) b = align_up(b, 8) + (size_t)M * (W + 1) * sizeof(unsigned long long);
   return b;
 }
@@ -977,20 +977,24 @@ vq_assign_filter_kernel(const float* __restrict__ X, int64_t ldx,
   const int mp = (M + 15) / 16 * 16 + kFilterSlack;    // codewords per plane
   char* fpl = reinterpret_cast<char*>(smem);             // [4][mp][16 B]
   float* se = reinterpret_cast<float*>(fpl + (size_t)4 * mp * 16);   // [mp]
-  float* bnd = se + mp;                                  // [W] max|e_k|, [W] max|e|^2
-  unsigned long long* acc =
-      reinterpret_cast<unsigned long long*>(fpl + (((size_t)4 * mp * 16 + (size_t)mp * 4 + 64 + 7) / 8) * 8);
+  float* bnd = se + mp;              // [wave][16]: per-wave max|e_k| (W), max|e|^2
+  unsigned long long* acc = reinterpret_cast<unsigned long long*>(
+      fpl + (((size_t)4 * mp * 16 + (size_t)mp * 4 + WV * 64 + 7) / 8) * 8);
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int q = lane >> 4, j = lane & 15;
   const float* E = emb + (int64_t)b * emb_bstride;
 
-  if (tid < 16) reinterpret_cast<unsigned*>(bnd)[tid] = 0u;
   if constexpr (FUSED) {
     for (int i = tid; i < M * (W + 1); i += NT) acc[i] = 0ull;
   }
   __syncthreads();
   // ---- staging: bf16 split planes, exact |e|^2 (reference order), bounds ----
+  // (bounds: per-thread maxima, then a per-wave shuffle reduction into LDS;
+  // LDS atomics here became 64-iteration readlane loops per wave)
+  float tb[W + 1];
+#pragma unroll
+  for (int k = 0; k <= W; ++k) tb[k] = 0.f;
   for (int m = tid; m < mp; m += NT) {
     float e[W];
     const bool mv = m < M;
@@ -1019,8 +1023,8 @@ vq_assign_filter_kernel(const float* __restrict__ X, int64_t ldx,
       sl[3 * W + 1] = h2;
       sl[3 * W + 2] = f2bf(r1 - bf2f(h2));
 #pragma unroll
-      for (int k = 0; k < W; ++k) atomicMax(reinterpret_cast<unsigned*>(bnd) + k, __float_as_uint(fabsf(e[k])));
-      atomicMax(reinterpret_cast<unsigned*>(bnd) + W, __float_as_uint(s2));
+      for (int k = 0; k < W; ++k) tb[k] = fmaxf(tb[k], fabsf(e[k]));
+      tb[W] = fmaxf(tb[W], s2);
     } else {
       sl[3 * W] = 0x7F80;   // +inf: never the best score
     }
@@ -1033,6 +1037,13 @@ vq_assign_filter_kernel(const float* __restrict__ X, int64_t ldx,
       v.w = (unsigned)sl[8 * pq + 6] | ((unsigned)sl[8 * pq + 7] << 16);
       *reinterpret_cast<uint4*>(fpl + ((size_t)pq * mp + m) * 16) = v;
     }
+  }
+#pragma unroll
+  for (int k = 0; k <= W; ++k) {
+    float v = tb[k];
+#pragma unroll
+    for (int sft = 32; sft >= 1; sft >>= 1) v = fmaxf(v, __shfl_xor(v, sft));
+    if (lane == 0) bnd[wave * 16 + k] = v;
   }
 
   // k-slot kc*4 + q of this lane: column, normalisation coefficients (as the
@@ -1085,8 +1096,15 @@ vq_assign_filter_kernel(const float* __restrict__ X, int64_t ldx,
   __syncthreads();
   float bound_e[W];
 #pragma unroll
-  for (int k = 0; k < W; ++k) bound_e[k] = bnd[k];
-  const float bound_ee = bnd[W];
+  for (int k = 0; k < W; ++k) {
+    float v = bnd[k];
+#pragma unroll
+    for (int w = 1; w < WV; ++w) v = fmaxf(v, bnd[w * 16 + k]);
+    bound_e[k] = v;
+  }
+  float bound_ee = bnd[W];
+#pragma unroll
+  for (int w = 1; w < WV; ++w) bound_ee = fmaxf(bound_ee, bnd[w * 16 + W]);
   const uint32_t aoff = (uint32_t)(q * mp + j) * 16u;   // plane q, codeword j of tile 0
 
   for (int it = 0; it < n_iters; ++it) {
@@ -1672,6 +1690,10 @@ static int launch_assign(const float* X, int64_t ldx, const float* G, int64_t ld
     return VQGNN_ERR_UNSUPPORTED;
   }
   const int wgs = g.parts * nb;
+  // the list pass handles the few undecided rows (~0.4%): a short grid, so
+  // fewer workgroups stage the codebook for a handful of rows each
+  static const int list_parts = env_int_vq("VQGNN_LIST_PARTS", 4);
+  const int wgs_list = std::max(1, std::min(g.parts, list_parts)) * nb;
   const int wm = slot_mode(KC, W, D);
   if (want_ema && !ema_zeroed)
     (void)hipMemsetAsync(parts, 0, (size_t)nb * M * (W + 1) * sizeof(unsigned long long), s);
@@ -1719,7 +1741,8 @@ static int launch_assign(const float* X, int64_t ldx, const float* G, int64_t ld
     hipEvent_t ev0 = nullptr, ev1 = nullptr;                                                  \
     if (!LI) timing_events(&ev0, &ev1);                                                       \
     else ev1 = tev1;                                                                          \
-    hipExtLaunchKernelGGL((vq_assign_kernel<KC, FU, WMV, LI>), dim3(wgs), dim3(kAsgWaves * 64),\
+    hipExtLaunchKernelGGL((vq_assign_kernel<KC, FU, WMV, LI>), dim3(LI ? wgs_list : wgs),      \
+                          dim3(kAsgWaves * 64),                                               \
                           (uint32_t)lds, s, ev0, ev1, 0, X, ldx, G, ldg, B, nb, D, M, W, coef, \
                           grad_scale, emb, ldw, emb_bstride, idx_out, codes, ldc, batch_idx,   \
                           idx32, parts, g.rows_per_part, g.chunk, sh.f, sh.g, rlist, rcnt,    \
