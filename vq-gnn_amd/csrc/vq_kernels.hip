@@ -607,6 +607,18 @@ vq_assign_kernel(const float* __restrict__ X, int64_t ldx,
   const bool vec_rows = WM != 0 && (ldw & 3) == 0 && (emb_bstride & 3) == 0 &&
                         (reinterpret_cast<uintptr_t>(emb) & 15) == 0;
 
+  // rlist (the exact pass behind vq_assign_filter_kernel): this branch's rows
+  // are rlist[b*B + i], i < rcnt[b], at least 64 per part (the undecided
+  // rows are few and skewed across branches: the grid covers the worst
+  // branch, and parts past the count leave before staging the codebook)
+  int b_rows = B, rpp = rows_per_part;
+  if constexpr (LIST) {
+    b_rows = rcnt[b];
+    const int nparts = (int)gridDim.x / nb;
+    rpp = max((b_rows + nparts - 1) / nparts, 64);
+    if (part * rpp >= b_rows) return;   // whole workgroup: no barrier reached
+  }
+
   if constexpr (FUSED) {
     for (int i = tid; i < M * (W + 1); i += NT) acc[i] = 0ull;
   }
@@ -630,14 +642,6 @@ vq_assign_kernel(const float* __restrict__ X, int64_t ldx,
     be[kc] = kval[kc] ? coef[(isg[kc] ? 3 * F : F) + c] : 0.f;
   }
 
-  // rlist (the exact pass behind vq_assign_filter_kernel): this branch's rows
-  // are rlist[b*B + i], i < rcnt[b], split over the parts in-kernel
-  int b_rows = B, rpp = rows_per_part;
-  if constexpr (LIST) {
-    b_rows = rcnt[b];
-    const int nparts = (int)gridDim.x / nb;
-    rpp = (b_rows + nparts - 1) / nparts;
-  }
   auto act = [&](int r) {
     if constexpr (LIST) return rlist[(int64_t)b * B + r];
     else return r;
@@ -1690,9 +1694,9 @@ static int launch_assign(const float* X, int64_t ldx, const float* G, int64_t ld
     return VQGNN_ERR_UNSUPPORTED;
   }
   const int wgs = g.parts * nb;
-  // the list pass handles the few undecided rows (~0.4%): a short grid, so
-  // fewer workgroups stage the codebook for a handful of rows each
-  static const int list_parts = env_int_vq("VQGNN_LIST_PARTS", 4);
+  // the list pass handles the undecided rows (0.4-2%, up to ~10% in one
+  // branch): up to 32 parts per branch of >= 64 rows, empty parts exit early
+  static const int list_parts = env_int_vq("VQGNN_LIST_PARTS", 32);
   const int wgs_list = std::max(1, std::min(g.parts, list_parts)) * nb;
   const int wm = slot_mode(KC, W, D);
   if (want_ema && !ema_zeroed)
