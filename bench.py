@@ -283,7 +283,8 @@ def main():
     # filter kernel plus the exact kernel's pass over the undecided rows
     mp = (M + 15) // 16 * 16 + 48
     filt = (os.environ.get("VQGNN_ASSIGN_FILTER", "0") == "1" and D == 4 and W in (4, 8)
-            and (4 * mp * 16 + 4 * mp + 8 * 64 + 7) // 8 * 8 + M * (W + 1) * 8 <= 160 * 1024)
+            and (4 * mp * 16 + 4 * mp + 8 * 64 + 16 + 2048 * 4 + 7) // 8 * 8 + M * (W + 1) * 8
+            <= 160 * 1024)
     vq_name = "vq_assign_filter_kernel+vq_assign_kernel(list)" if filt else "vq_assign_kernel"
     rl_vq = dict(kernel=vq_name, bound="mfma",
                  achieved=vq_flops / (assign_ms * 1e-3) / 1e12, peak=157.3, unit="TFLOP/s",

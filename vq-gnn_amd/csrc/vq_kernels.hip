@@ -339,6 +339,7 @@ constexpr size_t kLdsBudget = 160 * 1024;
 // tile pair ahead without a bound check (staged as e = 0, |e|^2 = +inf)
 constexpr int kSweepSlack = 32;
 constexpr int kFilterSlack = 48;   // the filter sweep reads 64 codewords a step
+constexpr int kLocalList = 2048;   // undecided rows a filter workgroup lists in LDS
 
 struct AssignGeom {
   int parts;          // row parts per branch (= EMA partial slabs)
@@ -955,7 +956,8 @@ __device__ __forceinline__ float vmin_after(float a, float b, float after) {
 // the bound constants, the fused EMA accumulators
 static size_t filter_lds_bytes(int M, int W, bool fused) {
   const int mp = (M + 15) / 16 * 16 + kFilterSlack;
-  size_t b = (size_t)4 * mp * 16 + (size_t)mp * 4 + kAsgWaves * 16 * 4;
+  size_t b = (size_t)4 * mp * 16 + (size_t)mp * 4 + kAsgWaves * 16 * 4 + 16 +
+             (size_t)kLocalList * 4;
   if (fused) b = align_up(b, 8) + (size_t)M * (W + 1) * sizeof(unsigned long long);
   return b;
 }
@@ -982,13 +984,17 @@ vq_assign_filter_kernel(const float* __restrict__ X, int64_t ldx,
   char* fpl = reinterpret_cast<char*>(smem);             // [4][mp][16 B]
   float* se = reinterpret_cast<float*>(fpl + (size_t)4 * mp * 16);   // [mp]
   float* bnd = se + mp;              // [wave][16]: per-wave max|e_k| (W), max|e|^2
+  int* lcnt = reinterpret_cast<int*>(bnd + WV * 16);    // undecided rows listed here
+  int* llist = lcnt + 4;                                // [kLocalList]
   unsigned long long* acc = reinterpret_cast<unsigned long long*>(
-      fpl + (((size_t)4 * mp * 16 + (size_t)mp * 4 + WV * 64 + 7) / 8) * 8);
+      fpl + (((size_t)4 * mp * 16 + (size_t)mp * 4 + WV * 64 + 16 + (size_t)kLocalList * 4 + 7) /
+             8) * 8);
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int q = lane >> 4, j = lane & 15;
   const float* E = emb + (int64_t)b * emb_bstride;
 
+  if (tid == 0) *lcnt = 0;
   if constexpr (FUSED) {
     for (int i = tid; i < M * (W + 1); i += NT) acc[i] = 0ull;
   }
@@ -1279,9 +1285,14 @@ vq_assign_filter_kernel(const float* __restrict__ X, int64_t ldx,
         if (okq) {
           if (idx_out) idx_out[(int64_t)b * B + row] = (int64_t)m;
           if (codes) codes[cur_bi * ldc + b] = (int16_t)m;
-        } else {
-          const int slot = atomicAdd(rcnt + b, 1);
-          rlist[(int64_t)b * B + slot] = row;
+        } else {   // listed in LDS (global atomics only past kLocalList)
+          const int slot = atomicAdd(lcnt, 1);
+          if (slot < kLocalList) {
+            llist[slot] = row;
+          } else {
+            const int gs = atomicAdd(rcnt + b, 1);
+            rlist[(int64_t)b * B + gs] = row;
+          }
         }
       }
     }
@@ -1297,6 +1308,16 @@ vq_assign_filter_kernel(const float* __restrict__ X, int64_t ldx,
         }
       }
     }
+  }
+  // this workgroup's listed rows: one global reservation, then a copy
+  __syncthreads();
+  const int nl = min(*lcnt, kLocalList);
+  if (nl > 0) {
+    __syncthreads();          // every lane has read lcnt before it is reused
+    if (tid == 0) *lcnt = atomicAdd(rcnt + b, nl);
+    __syncthreads();
+    const int base = *lcnt;
+    for (int i = tid; i < nl; i += NT) rlist[(int64_t)b * B + base + i] = llist[i];
   }
   if constexpr (FUSED) {
     __syncthreads();
