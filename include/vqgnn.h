@@ -63,38 +63,62 @@ int vqgnn_bn_stats(const float* X, int64_t ldx, const float* G, int64_t ldg,
                    int32_t B, int32_t F, int32_t with_grad,
                    double* sums, void* workspace, vqgnn_stream_t stream);
 
-/* 2. BatchNorm finalize: batch mean/var -> per-column affine normalisation
- *    coefficients (alpha = invstd, beta = -mean*invstd, as ATen's CPU
- *    batch_norm computes them) and the running-stat EMA update.
+/* 2. BatchNorm finalize: batch statistics -> per-column normalisation
+ *    coefficients and the running-stat EMA update.
  *    Replaces BatchNorm1d.forward's stat update (vq.py:162, :223) and the
  *    first-call running-stat initialisation of update() (vq.py:216-221).
  *    mode: 0 = eval (coefficients from running stats, no update)
  *          1 = train (batch stats, running stats updated with momentum)
  *          2 = train + init_from_batch (vq.py:216-221, then as 1)
  *          3 = eval  + init_from_batch (vq.py:216-221, then as 0)
- *    count = rows over all ranks.  coef[4][F]: alpha_f, beta_f, alpha_g, beta_g.
+ *    arith_x / arith_g: the arithmetic of the feature / gradient columns,
+ *    i.e. which of ATen's CPU BatchNorm paths the reference takes for that
+ *    input (oracle/bn_ref.py restates both):
+ *      VQGNN_BN_FP64    fp64 sums; deterministic and independent of the
+ *                       number of ranks (the multi-GPU path, whose sums are
+ *                       all-reduced)
+ *      VQGNN_BN_STRIDED ATen on a non-contiguous [B, D] input: the reference
+ *                       layers' x[:, D*i:D*(i+1)] slices (models.py:162-165)
+ *      VQGNN_BN_CONTIG  ATen on a contiguous [B, D] input with ref_threads
+ *                       CPU threads (its row chunks depend on them)
+ *    vqgnn_bn_finalize takes fp64 sums, so its batch modes use FP64; arith
+ *    only picks the form of the eval coefficients.
+ *    count = rows over all ranks.  momenta and eps are the reference's
+ *    Python floats (double).
+ *    coef[6][F]: alpha_f, beta_f, alpha_g, beta_g, shift_f, shift_g; every
+ *    consumer normalises x as fma(x - shift, alpha, beta), which is ATen's
+ *    expression on either path ((x - mean) * invstd, or
+ *    fma(x, invstd, -mean * invstd)).
  *    batch_out[4][F] (optional, may be NULL): mean_f, std_f, mean_g, std_g with
- *    std = sqrt(unbiased var + eps_std) (vq.py:208-211 logging stash).
+ *    mean = torch.mean and std = sqrt(torch.var + eps_std) (vq.py:208-211
+ *    logging stash).
  *    nbt_f / nbt_g (optional, [F / nbt_d] int64): BatchNorm1d's
- *    num_batches_tracked of each branch (nbt_d columns per branch) += 1 —
- *    pass them in training modes only.                                        */
+ *    num_batches_tracked of each branch (nbt_d columns per branch) += 1 in
+ *    the training modes.                                                      */
+#define VQGNN_BN_FP64 0
+#define VQGNN_BN_STRIDED 1
+#define VQGNN_BN_CONTIG 2
 int vqgnn_bn_finalize(const double* sums, int64_t count, int32_t F, int32_t with_grad,
-                      int32_t mode, float momentum_f, float eps_f,
-                      float momentum_g, float eps_g, float eps_std,
-                      float* rm_f, float* rv_f, float* rm_g, float* rv_g,
+                      int32_t mode, int32_t arith_x, int32_t arith_g,
+                      double momentum_f, double eps_f, double momentum_g, double eps_g,
+                      double eps_std, float* rm_f, float* rv_f, float* rm_g, float* rv_g,
                       float* coef, float* batch_out,
                       int64_t* nbt_f, int64_t* nbt_g, int32_t nbt_d,
                       vqgnn_stream_t stream);
 
-/* 2b. Single-process shortcut: vqgnn_bn_stats + vqgnn_bn_finalize in two
- *     kernels (the reduce and the finalize fused: one wave per data column,
- *     same summation order, same bits).  mode must be a batch-statistics mode
- *     (1..3); count = B.  sums (optional) receives the fp64 sums.  Multi-GPU
- *     callers all-reduce the sums between the two calls instead. */
+/* 2b. Single-process statistics + finalize (count = B), any arithmetic.
+ *     FP64: the vqgnn_bn_stats partials with the reduce and the finalize
+ *     fused (same summation order and bits as the two calls); sums
+ *     (optional) receives the fp64 sums.  STRIDED / CONTIG: the cascade-sum
+ *     and row-chunk statistics of ATen's paths (sums must be NULL);
+ *     ref_threads (1..1024) is the reference's torch.get_num_threads(), used
+ *     by CONTIG columns only.  B <= 2^23.  Multi-GPU callers use FP64 and
+ *     all-reduce the sums between vqgnn_bn_stats and vqgnn_bn_finalize. */
 int vqgnn_bn_stats_finalize(const float* X, int64_t ldx, const float* G, int64_t ldg,
                             int32_t B, int32_t F, int32_t with_grad, double* sums, int32_t mode,
-                            float momentum_f, float eps_f, float momentum_g, float eps_g,
-                            float eps_std, float* rm_f, float* rv_f, float* rm_g, float* rv_g,
+                            int32_t arith_x, int32_t arith_g, int32_t ref_threads,
+                            double momentum_f, double eps_f, double momentum_g, double eps_g,
+                            double eps_std, float* rm_f, float* rv_f, float* rm_g, float* rv_g,
                             float* coef, float* batch_out, int64_t* nbt_f, int64_t* nbt_g,
                             int32_t nbt_d, void* workspace, vqgnn_stream_t stream);
 

@@ -93,6 +93,7 @@ def update(st, X_B, grad, training=True):
                     _bn(grad, st["rm_g"], st["rv_g"], training, st["momentum"], eps)], dim=1)  # :223
     xn[:, D:2 * D] *= st["grad_scale"][0]                                        # :224
     d = distances(xn, st["embedding"])                                           # :230-232
+    logs["distances"] = d          # (oracle extra: what argmin ran on, for diagnostics)
     idx = torch.argmin(d, dim=1).unsqueeze(1)                                    # :236
     enc = torch.zeros(idx.shape[0], M)                                           # :237
     enc.scatter_(1, idx, 1)                                                      # :238

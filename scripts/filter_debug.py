@@ -20,7 +20,7 @@ F = nb * D
 X = torch.randn(B, F, device=dev)
 G = torch.randn(B, F, device=dev) * 1e-3
 emb = torch.randn(nb, M, 2 * D, device=dev)
-coef = torch.zeros(4, F, device=dev)
+coef = torch.zeros(6, F, device=dev)
 coef[0] = 1.0
 coef[2] = 1.0
 L = lib()

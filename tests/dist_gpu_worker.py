@@ -51,6 +51,7 @@ def main(out_dir):
     res["codes"] = codes.cpu().numpy()
     if rank == 0:                                  # single-process union batch
         ref = fresh_bank()
+        ref.bn_arith = "fp64"       # the multi-rank statistics' arithmetic
         rc = codes0.to(dev)
         Xu, Gu, nu = X.to(dev), G.to(dev), node.to(dev)
         ref.feature_update(Xu, 0, nb, True, codes=rc, batch_idx=nu)

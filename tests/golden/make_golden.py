@@ -33,7 +33,7 @@ def state_of(m):
 
 def make_case(vq, name, M, D, B, op, training=True, warm_up=True, grad_scale=(1.0, 1.0),
               momentum=0.1, calls=1, tie=False, seed=0, xscale=1.0, gscale=1e-3,
-              cs_init=None):
+              cs_init=None, strided=False):
     torch.manual_seed(seed)
     m = vq.VectorQuantizerEMA(M, D, grad_normalize_scale=list(grad_scale),
                               warm_up_flag=warm_up, momentum=momentum)
@@ -45,8 +45,12 @@ def make_case(vq, name, M, D, B, op, training=True, warm_up=True, grad_scale=(1.
     rec = {}
     for call in range(calls):
         pre = state_of(m)
-        X = (torch.randn(B, D) * xscale + 0.3).float()
-        G = (torch.randn(B, D) * gscale).float()
+        if strided:   # branch slices of wider activations, as the layers pass them
+            X = (torch.randn(B, 3 * D) * xscale + 0.3).float()[:, D:2 * D]
+            G = (torch.randn(B, 3 * D) * gscale).float()[:, 2 * D:3 * D]
+        else:
+            X = (torch.randn(B, D) * xscale + 0.3).float()
+            G = (torch.randn(B, D) * gscale).float()
         err = ""
         idx = torch.full((B, 1), -1, dtype=torch.long)
         logs = {}
@@ -63,8 +67,8 @@ def make_case(vq, name, M, D, B, op, training=True, warm_up=True, grad_scale=(1.
             err = str(e)
         post = state_of(m)
         p = f"c{call}_"
-        rec[p + "X"] = X.numpy()
-        rec[p + "G"] = G.numpy()
+        rec[p + "X"] = X.contiguous().numpy()
+        rec[p + "G"] = G.contiguous().numpy()
         rec[p + "idx"] = idx.numpy()[:, 0]
         rec[p + "error"] = np.array(err)
         rec[p + "bn_inited_pre"] = np.array(pre_bn_inited)
@@ -77,7 +81,8 @@ def make_case(vq, name, M, D, B, op, training=True, warm_up=True, grad_scale=(1.
         if err:
             break
     meta = dict(M=M, D=D, B=B, op=op, training=training, warm_up=warm_up,
-                grad_scale=list(grad_scale), momentum=momentum, calls=calls)
+                grad_scale=list(grad_scale), momentum=momentum, calls=calls,
+                strided=strided, threads=torch.get_num_threads())
     rec["meta"] = np.array(repr(meta))
     np.savez_compressed(os.path.join(OUT, f"vq_{name}.npz"), **rec)
     print(name, {k: v.shape for k, v in rec.items() if k.endswith("idx")},
@@ -102,6 +107,17 @@ def main():
     make_case(vq, "up_tie", 64, 4, 600, "update", tie=True, seed=11)
     make_case(vq, "up_m4096", 4096, 4, 2500, "update", seed=12)
     make_case(vq, "up_nowarm", 32, 4, 3000, "update", warm_up=False, cs_init=1.0, seed=13)
+    # strided inputs: ATen's non-contiguous BatchNorm path (cascade-sum mean)
+    make_case(vq, "fu_strided", 256, 4, 5000, "feature_update", calls=2, seed=14, strided=True)
+    make_case(vq, "fu_strided_eval", 128, 4, 1200, "feature_update", training=False, seed=15,
+              strided=True)
+    make_case(vq, "up_strided", 256, 4, 4500, "update", calls=2, seed=16, strided=True)
+    make_case(vq, "up_strided_m1024", 1024, 4, 10000, "update", seed=17, strided=True,
+              xscale=2.0)
+    make_case(vq, "up_strided_scale", 128, 4, 1500, "update", grad_scale=(0.5, 1.0),
+              momentum=0.2, calls=2, seed=18, strided=True)
+    make_case(vq, "up_strided_eval", 128, 4, 1000, "update", training=False, seed=19,
+              strided=True)
 
 
 if __name__ == "__main__":

@@ -58,3 +58,31 @@ def tie_aware_mismatch(idx_a, idx_b, dist, rel=1e-5):
     scale = 1.0 + dist[bad].abs().max(dim=1).values.double()
     unexplained = int(((da - db).abs() > rel * scale).sum())
     return int(bad.numel()), unexplained
+
+
+def as_layout(t, strided, device=None):
+    """``t`` [B, D] as the reference received it: a column slice of a wider
+    row-major matrix when ``strided`` (ATen's non-contiguous BatchNorm path,
+    as the layers' x[:, D*i:D*(i+1)]), else a contiguous tensor."""
+    t = t.to(device) if device is not None else t
+    if not strided:
+        return t.contiguous()
+    B, D = t.shape
+    wide = torch.zeros(B, 3 * D, dtype=t.dtype, device=t.device)
+    wide[:, D:2 * D] = t
+    return wide[:, D:2 * D]
+
+
+class torch_threads:
+    """Context manager: torch.set_num_threads(n), restored on exit (the
+    reference's contiguous-input BatchNorm depends on the thread count)."""
+
+    def __init__(self, n):
+        self.n = n
+
+    def __enter__(self):
+        self.old = torch.get_num_threads()
+        torch.set_num_threads(self.n)
+
+    def __exit__(self, *a):
+        torch.set_num_threads(self.old)

@@ -48,7 +48,7 @@ def test_filter_equals_exact_kernel(B, M, W, stats, near):
         emb[:, h:2 * h] = emb[:, :h]
         emb[:, h:2 * h:3] = torch.nextafter(emb[:, h:2 * h:3], torch.tensor(10.0))
     emb = emb.to(DEV)
-    coef = torch.zeros(4, nb * D)
+    coef = torch.zeros(6, nb * D)
     coef[0], coef[1] = 1.1, -0.05
     coef[2], coef[3] = 0.9, 0.01
     coef = coef.to(DEV)

@@ -3,7 +3,8 @@ golden vectors produced by running vq_gnn_v2/vq.py (tests/golden/make_golden.py)
 import pytest
 import torch
 
-from helpers import golden_cases, load_case, oracle_state_from, tie_aware_mismatch, STATE_KEYS
+from helpers import (STATE_KEYS, as_layout, golden_cases, load_case, oracle_state_from,
+                     tie_aware_mismatch, torch_threads)
 from oracle import vq_ref
 
 
@@ -17,24 +18,27 @@ def test_oracle_matches_reference_golden(name):
         for k in STATE_KEYS:  # chained calls start from the previous post-state
             torch.testing.assert_close(st[k], rec["pre"][k], rtol=0, atol=0)
         err = ""
+        strided = meta.get("strided", False)
+        X, G = as_layout(rec["X"], strided), as_layout(rec["G"], strided)
         try:
-            if meta["op"] == "feature_update":
-                idx = vq_ref.feature_update(st, rec["X"], meta["training"])
-            else:
-                idx, enc, logs = vq_ref.update(st, rec["X"], rec["G"], meta["training"])
-                torch.testing.assert_close(logs["mean"], rec["logs"]["mean"], rtol=1e-6, atol=1e-7)
-                torch.testing.assert_close(logs["std"], rec["logs"]["std"], rtol=1e-6, atol=1e-7)
-                assert enc.sum().item() == rec["X"].shape[0]
+            # the reference's layout and thread count -> the same ATen path
+            with torch_threads(meta.get("threads", 8)):
+                if meta["op"] == "feature_update":
+                    idx = vq_ref.feature_update(st, X, meta["training"])
+                else:
+                    idx, enc, logs = vq_ref.update(st, X, G, meta["training"])
+                    torch.testing.assert_close(logs["mean"], rec["logs"]["mean"], rtol=0, atol=0)
+                    torch.testing.assert_close(logs["std"], rec["logs"]["std"], rtol=0, atol=0)
+                    assert enc.sum().item() == rec["X"].shape[0]
         except ValueError as e:
             err = str(e)
         assert err == rec["error"]
         if err:
             break
-        # same ops as the reference -> identical up to BN-stat threading order
-        n_mis = int((idx[:, 0] != rec["idx"]).sum())
-        assert n_mis <= 1, f"{name} call {c}: {n_mis} index mismatches"
+        # the same ops as the reference on the same layout: bit-identical
+        assert torch.equal(idx[:, 0], rec["idx"]), f"{name} call {c}: index mismatch"
         for k in STATE_KEYS:
-            torch.testing.assert_close(st[k], rec["post"][k], rtol=2e-6, atol=1e-6,
+            torch.testing.assert_close(st[k], rec["post"][k], rtol=0, atol=0,
                                        msg=lambda m: f"{name} call {c} {k}: {m}")
         # continue chained calls from the reference's exact post-state
         for k in STATE_KEYS:

@@ -21,6 +21,7 @@ _c_void_p = ctypes.c_void_p
 _i32 = ctypes.c_int32
 _i64 = ctypes.c_int64
 _f32 = ctypes.c_float
+_f64 = ctypes.c_double
 _size = ctypes.c_size_t
 
 # name -> (restype, argtypes); mirrors include/vqgnn.h one to one.
@@ -30,10 +31,10 @@ SIGNATURES = {
     "vqgnn_bn_stats_workspace": (_size, [_i32, _i32]),
     "vqgnn_bn_stats": (ctypes.c_int, [_c_void_p, _i64, _c_void_p, _i64, _i32, _i32, _i32,
                                       _c_void_p, _c_void_p, _c_void_p]),
-    "vqgnn_bn_finalize": (ctypes.c_int, [_c_void_p, _i64, _i32, _i32, _i32, _f32, _f32, _f32,
-                                         _f32, _f32, _c_void_p, _c_void_p, _c_void_p,
+    "vqgnn_bn_finalize": (ctypes.c_int, [_c_void_p, _i64, _i32, _i32, _i32, _i32, _i32, _f64,
+                                         _f64, _f64, _f64, _f64, _c_void_p, _c_void_p,
                                          _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
-                                         _i32, _c_void_p]),
+                                         _c_void_p, _i32, _c_void_p]),
     "vqgnn_vq_stat_shifts": (None, [_i64, _f32, _c_void_p, _c_void_p]),
     "vqgnn_vq_ema_parts": (_i32, [_i32, _i32, _i32, _i32]),
     "vqgnn_vq_assign_workspace": (_size, [_i32, _i32, _i32, _i32]),
@@ -90,10 +91,11 @@ SIGNATURES = {
                                            _c_void_p, _c_void_p, _c_void_p, _c_void_p, _f32,
                                            _c_void_p, _c_void_p, _c_void_p, _c_void_p]),
     "vqgnn_bn_stats_finalize": (ctypes.c_int, [_c_void_p, _i64, _c_void_p, _i64, _i32, _i32, _i32,
-                                               _c_void_p, _i32, _f32, _f32, _f32, _f32, _f32,
+                                               _c_void_p, _i32, _i32, _i32, _i32, _f64, _f64,
+                                               _f64, _f64, _f64, _c_void_p, _c_void_p,
                                                _c_void_p, _c_void_p, _c_void_p, _c_void_p,
-                                               _c_void_p, _c_void_p, _c_void_p, _c_void_p,
-                                               _i32, _c_void_p, _c_void_p]),
+                                               _c_void_p, _c_void_p, _i32, _c_void_p,
+                                               _c_void_p]),
     # §9 mini-batch construction
     "vqgnn_khop_workspace": (_size, [_i64]),
     "vqgnn_khop_subset": (ctypes.c_int, [_c_void_p, _c_void_p, _i64, _c_void_p, _i32, _i32, _i32,

@@ -16,6 +16,7 @@
 
 #include <hip/hip_ext.h>
 
+#include <algorithm>
 #include <vector>
 #include <atomic>
 
@@ -179,100 +180,163 @@ bn_stats_reduce_kernel(const double* __restrict__ part, int chunks, int F, int C
 }
 
 // ---------------------------------------------------------------------------
-// 2. BatchNorm finalize (one thread per column)
-//    ATen batch_norm_cpu_update_stats_template: mean/var in double
-//    (acc_type<float, CPU> = double), invstd = 1/sqrt(var_biased + eps),
-//    running = momentum*batch + (1-momentum)*running  (double, stored float),
-//    running_var uses the unbiased variance.  Eval: invstd = 1/sqrtf(rv+eps)
-//    in float (opmath).  beta = -(mean*alpha) in float.
+// 2. BatchNorm finalize
+//
+// Coefficients: coef[6][F] = alpha_f, beta_f, alpha_g, beta_g, shift_f,
+// shift_g; every consumer normalises as fma(x - shift, alpha, beta)
+// (bn_apply), which is each ATen path's exact expression:
+//   strided input (the reference layers' x[:, D*i:D*(i+1)] slices):
+//       ((x - mean) * invstd) * 1 + 0          -> shift = mean, beta = 0
+//   contiguous input / fp64 sums:
+//       fma(x, invstd, -(mean * invstd))       -> shift = 0
+// Arithmetic per column (include/vqgnn.h VQGNN_BN_*; oracle/bn_ref.py):
+//   FP64     mean and variance from fp64 sums (deterministic and independent
+//            of the number of ranks: the multi-GPU path all-reduces them)
+//   STRIDED  batch_norm_cpu_update_stats_template, non-contiguous branch:
+//            mean = float cascade sum / B (at::mean), var_sum = sum (x-mean)^2
+//            in double, invstd = 1/sqrt(var_sum/B + eps) in double, running
+//            stats in double
+//   CONTIG   batch_norm_cpu_collect_stats_channels_last_impl: fp32 per-thread
+//            row chunks folded in double, var_sum stored as float, running
+//            stats in float (momentum_ is float)
+// Eval (every arithmetic): invstd = 1/sqrtf(rv + (float)eps) in float.
+// Init (update()'s first call, vq.py:216-221): rm = torch.mean (cascade sum
+// / B), rv = torch.var (unbiased, double then float).
 // ---------------------------------------------------------------------------
-// have: the batch sums are available (always in the training modes; in eval
-// mode for update(), whose batch mean / std stash runs in every mode,
-// vq.py:208-211)
-__device__ __forceinline__ void bn_column(double s, double s2, bool have, int64_t n, int mode,
-                                          float momentum, float eps, float eps_std,
+enum : int { kBnFp64 = 0, kBnStrided = 1, kBnContig = 2 };
+
+struct BnCol {            // batch statistics of one column
+  float mean;             // the arithmetic's batch mean
+  double var_sum;         // sum (x - mean)^2 (FP64 / STRIDED: double; CONTIG: float value)
+  float tmean;            // torch.mean (init, logging)
+  double var_u;           // unbiased variance about the exact mean (torch.var)
+};
+
+__device__ __forceinline__ void bn_column(const BnCol& st, bool have, int64_t n, int mode,
+                                          int arith, double mom, double eps, double eps_std,
                                           float* rm, float* rv, float* alpha, float* beta,
-                                          float* mean_out, float* std_out) {
+                                          float* shift, float* mean_out, float* std_out) {
   const bool train = (mode == 1 || mode == 2);
   const bool init = mode >= 2;
   const double nd = (double)n;
-  double mean = 0.0, var_b = 0.0, var_u = 0.0;
   if (have) {
-    mean = s / nd;
-    double m2 = s2 - s * mean;            // sum (x - mean)^2
-    if (m2 < 0.0) m2 = 0.0;
-    var_b = m2 / nd;
-    var_u = (n > 1) ? m2 / (nd - 1.0) : NAN;
-    if (mean_out) *mean_out = (float)mean;
-    if (std_out) *std_out = sqrtf(__fadd_rn((float)var_u, eps_std));
+    if (mean_out) *mean_out = st.tmean;
+    if (std_out) *std_out = sqrtf(__fadd_rn((float)st.var_u, (float)eps_std));
   }
   if (init) {  // vq.py:216-221: running stats <- torch.mean / torch.var(unbiased)
-    *rm = (float)mean;
-    *rv = (float)var_u;
+    *rm = st.tmean;
+    *rv = (float)st.var_u;
   }
   if (!train) {  // BatchNorm1d eval: float invstd from the running stats
-    const float invstd = 1.0f / sqrtf(__fadd_rn(*rv, eps));
+    const float invstd = 1.0f / sqrtf(__fadd_rn(*rv, (float)eps));
     *alpha = invstd;
-    *beta = -__fmul_rn(*rm, invstd);
+    if (arith == kBnStrided) {
+      *shift = *rm;
+      *beta = 0.f;
+    } else {
+      *shift = 0.f;
+      *beta = -__fmul_rn(*rm, invstd);
+    }
     return;
   }
-  const double mom = (double)momentum;
-  *rm = (float)(mom * mean + (1.0 - mom) * (double)(*rm));
-  *rv = (float)(mom * var_u + (1.0 - mom) * (double)(*rv));
-  const float invstd = (float)(1.0 / sqrt(var_b + (double)eps));
-  const float mean32 = (float)mean;
+  if (arith == kBnContig) {
+    const float momf = (float)mom, vs = (float)st.var_sum;
+    const float one_m = __fsub_rn(1.0f, momf);
+    *rm = __fadd_rn(__fmul_rn(momf, st.mean), __fmul_rn(one_m, *rm));
+    const float vu = __fdiv_rn(vs, (float)(n - 1));
+    *rv = (float)((double)momf * (double)vu + (double)__fmul_rn(one_m, *rv));
+    const float invstd = (float)(1.0 / sqrt((double)__fdiv_rn(vs, (float)n) + eps));
+    *alpha = invstd;
+    *beta = -__fmul_rn(st.mean, invstd);
+    *shift = 0.f;
+    return;
+  }
+  const double md = (double)st.mean;
+  *rm = (float)(mom * md + (1.0 - mom) * (double)(*rm));
+  const double vu = n > 1 ? st.var_sum / (nd - 1.0) : NAN;
+  *rv = (float)(mom * vu + (1.0 - mom) * (double)(*rv));
+  const float invstd = (float)(1.0 / sqrt(st.var_sum / nd + eps));
   *alpha = invstd;
-  *beta = -__fmul_rn(mean32, invstd);
+  if (arith == kBnStrided) {
+    *shift = st.mean;
+    *beta = 0.f;
+  } else {
+    *shift = 0.f;
+    *beta = -__fmul_rn(st.mean, invstd);
+  }
 }
 
-__global__ void bn_finalize_kernel(const double* __restrict__ sums, int64_t n, int F, int with_grad,
-                                   int mode, float mom_f, float eps_f, float mom_g, float eps_g,
-                                   float eps_std, float* rm_f, float* rv_f, float* rm_g,
-                                   float* rv_g, float* __restrict__ coef,
-                                   float* __restrict__ batch_out, long long* __restrict__ nbt_f,
-                                   long long* __restrict__ nbt_g, int D) {
+// FP64 statistics from the sums: mean = s / n, var_sum = s2 - s*mean.
+__device__ __forceinline__ BnCol bn_from_sums(double s, double s2, int64_t n) {
+  BnCol st;
+  const double nd = (double)n;
+  const double mean = s / nd;
+  double m2 = s2 - s * mean;
+  if (m2 < 0.0) m2 = 0.0;
+  st.mean = (float)mean;
+  st.tmean = (float)mean;
+  st.var_sum = m2;
+  st.var_u = n > 1 ? m2 / (nd - 1.0) : NAN;
+  return st;
+}
+
+struct BnArgs {           // per-call BatchNorm parameters (feature / gradient half)
+  int mode, arith_x, arith_g;
+  double mom_f, eps_f, mom_g, eps_g, eps_std;
+  float *rm_f, *rv_f, *rm_g, *rv_g;
+  float* coef;            // [6][F]
+  float* batch_out;       // [4][F] or null
+  long long *nbt_f, *nbt_g;
+  int D;
+};
+
+// column k of half g (0: features, 1: gradients) of F columns
+__device__ __forceinline__ void bn_emit(const BnArgs& a, int F, int g, int k, const BnCol& st,
+                                        bool have, int64_t n) {
+  if (a.D > 0 && k % a.D == 0 && (a.mode == 1 || a.mode == 2)) {
+    long long* nbt = g ? a.nbt_g : a.nbt_f;   // BatchNorm1d.num_batches_tracked += 1
+    if (nbt) nbt[k / a.D] += 1;
+  }
+  const int o = g ? 2 * F : 0;
+  bn_column(st, have, n, a.mode, g ? a.arith_g : a.arith_x, g ? a.mom_g : a.mom_f,
+            g ? a.eps_g : a.eps_f, a.eps_std, (g ? a.rm_g : a.rm_f) + k,
+            (g ? a.rv_g : a.rv_f) + k, a.coef + o + k, a.coef + o + F + k,
+            a.coef + (g ? 5 * F : 4 * F) + k,
+            a.batch_out ? a.batch_out + o + k : nullptr,
+            a.batch_out ? a.batch_out + o + F + k : nullptr);
+}
+
+__global__ void bn_finalize_kernel(const double* __restrict__ sums, int64_t n, int F,
+                                   int with_grad, BnArgs a) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= F) return;
-  if (D > 0 && c % D == 0) {   // BatchNorm1d.num_batches_tracked += 1 (train)
-    if (nbt_f) nbt_f[c / D] += 1;
-    if (nbt_g && with_grad) nbt_g[c / D] += 1;
-  }
   const bool have = sums != nullptr;
-  bn_column(have ? sums[c] : 0.0, have ? sums[F + c] : 0.0, have, n, mode, mom_f, eps_f, eps_std,
-            rm_f + c, rv_f + c, coef + c, coef + F + c, batch_out ? batch_out + c : nullptr,
-            batch_out ? batch_out + F + c : nullptr);
-  if (with_grad) {
-    bn_column(have ? sums[2 * F + c] : 0.0, have ? sums[3 * F + c] : 0.0, have, n, mode, mom_g,
-              eps_g, eps_std, rm_g + c,
-              rv_g + c, coef + 2 * F + c, coef + 3 * F + c,
-              batch_out ? batch_out + 2 * F + c : nullptr,
-              batch_out ? batch_out + 3 * F + c : nullptr);
-  }
+  bn_emit(a, F, 0, c, have ? bn_from_sums(sums[c], sums[F + c], n) : BnCol{}, have, n);
+  if (with_grad)
+    bn_emit(a, F, 1, c, have ? bn_from_sums(sums[2 * F + c], sums[3 * F + c], n) : BnCol{},
+            have, n);
 }
 
-// Single-process fusion of bn_stats_reduce + bn_finalize.  Block = 32 data
-// columns; lane l of every wave reads value column (l / 32 ? sum of squares :
-// sum) of data column 32*block + l % 32, so a half-wave reads 256 contiguous
-// bytes of a chunk row; wave w sums its slice of the chunks in order, the 16
-// slices are folded in order in LDS (deterministic), then one thread per data
-// column runs its BatchNorm update.  No all-reduce can sit between the two
-// here, so multi-GPU callers keep vqgnn_bn_stats + vqgnn_bn_finalize.
+// Single-process fusion of bn_stats_reduce + bn_finalize (FP64 arithmetic).
+// Block = 32 data columns; lane l of every wave reads value column (l / 32 ?
+// sum of squares : sum) of data column 32*block + l % 32, so a half-wave
+// reads 256 contiguous bytes of a chunk row; wave w sums its slice of the
+// chunks in order, the 16 slices are folded in order in LDS (deterministic),
+// then one thread per data column runs its BatchNorm update.  No all-reduce
+// can sit between the two here, so multi-GPU callers keep vqgnn_bn_stats +
+// vqgnn_bn_finalize.
 constexpr int kRfThreads = 1024;
 constexpr int kRfWaves = kRfThreads / 64;
 __global__ void __launch_bounds__(kRfThreads)
 bn_reduce_finalize_kernel(const double* __restrict__ part, int chunks, int F, int C,
-                          double* __restrict__ sums, int64_t n, int mode, float mom_f,
-                          float eps_f, float mom_g, float eps_g, float eps_std, float* rm_f,
-                          float* rv_f, float* rm_g, float* rv_g, float* __restrict__ coef,
-                          float* __restrict__ batch_out, long long* __restrict__ nbt_f,
-                          long long* __restrict__ nbt_g, int D) {
+                          double* __restrict__ sums, int64_t n, BnArgs a) {
   __shared__ double red[kRfWaves][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int c = blockIdx.x * 32 + (lane & 31);            // data column
   const int h = lane >> 5;                                // 0: sum, 1: sum of squares
   const int per = (chunks + kRfWaves - 1) / kRfWaves;
   const int p0 = wave * per, p1 = min(chunks, p0 + per);
-  double a = 0.0;
+  double acc = 0.0;
   if (c < C) {
     // all of a slice's loads in flight before the in-order adds (the
     // partials come from every XCD: each round trip is an L2 miss)
@@ -283,10 +347,10 @@ bn_reduce_finalize_kernel(const double* __restrict__ part, int chunks, int F, in
       for (int u = 0; u < 32; ++u) t[u] = p + u < p1 ? col[(int64_t)(p + u) * 2 * C] : 0.0;
 #pragma unroll
       for (int u = 0; u < 32; ++u)
-        if (p + u < p1) a += t[u];
+        if (p + u < p1) acc += t[u];
     }
   }
-  red[wave][lane] = a;
+  red[wave][lane] = acc;
   __syncthreads();
   if (threadIdx.x >= 32) return;
   const int t = threadIdx.x;
@@ -303,14 +367,185 @@ bn_reduce_finalize_kernel(const double* __restrict__ part, int chunks, int F, in
     sums[(g ? 2 * F : 0) + k] = sm;
     sums[(g ? 3 * F : F) + k] = sq;
   }
-  if (D > 0 && k % D == 0) {   // BatchNorm1d.num_batches_tracked += 1 (train)
-    long long* nbt = g ? nbt_g : nbt_f;
-    if (nbt) nbt[k / D] += 1;
+  bn_emit(a, F, g, k, bn_from_sums(sm, sq, n), true, n);
+}
+
+// ---------------------------------------------------------------------------
+// 2b. ATen-arithmetic statistics (STRIDED / CONTIG columns)
+//
+// at::mean's float cascade sum (SumKernel.cpp multi_row_sum, 4 levels):
+// level 0 sums blocks of step = 2^lp rows sequentially, level 1 sums `step`
+// blocks (a superblock), level 2 `step` superblocks (a group), level 3 the
+// groups; the tail rows and the unfinished levels are added last as
+// ((tail + acc1) + acc2) + acc3.  lp = max(4, ceil_log2(B) / 4).
+// bn_cascade_partial_kernel: one wave per (superblock, 64-column tile) — the
+// lane of column c sums its superblock's blocks in the reference's order and
+// also accumulates P = sum (x - x0), Q = sum (x - x0)^2 in double about the
+// column's first value x0 (the variance terms, cancellation-free).
+// bn_contig_chunk_kernel: the channels-last per-thread row chunks (CONTIG
+// columns only; a serial fp32 chain per chunk, as the CPU thread runs it).
+// bn_aten_finalize_kernel: one wave per column folds the partials and runs
+// the BatchNorm update of its arithmetic.
+// ---------------------------------------------------------------------------
+constexpr int kCasWaves = 4;
+
+__device__ __forceinline__ const float* bn_col_base(const float* X, int64_t ldx, const float* G,
+                                                    int64_t ldg, int F, int c, int64_t* ld) {
+  *ld = c < F ? ldx : ldg;
+  return c < F ? X + c : G + (c - F);
+}
+
+__global__ void __launch_bounds__(kCasWaves * 64)
+bn_cascade_partial_kernel(const float* __restrict__ X, int64_t ldx,
+                          const float* __restrict__ G, int64_t ldg, int B, int F, int C,
+                          int lp, int nsb, int ntiles, float* __restrict__ sb_sum,
+                          double* __restrict__ sb_p, double* __restrict__ sb_q,
+                          float* __restrict__ tail) {
+  const int w = blockIdx.x * kCasWaves + (threadIdx.x >> 6);
+  if (w >= nsb * ntiles) return;
+  const int sb = w / ntiles, tile = w % ntiles;
+  const int c = tile * 64 + (threadIdx.x & 63);
+  if (c >= C) return;
+  int64_t ld;
+  const float* base = bn_col_base(X, ldx, G, ldg, F, c, &ld);
+  const double x0 = (double)base[0];
+  const int step = 1 << lp;
+  const int nblk_all = B >> lp;
+  const int nblk = min(step, nblk_all - (sb << lp));     // complete blocks in this superblock
+  const int64_t r0 = (int64_t)sb << (2 * lp);
+  float acc1 = 0.f;
+  double p = 0.0, q = 0.0;
+  for (int k = 0; k < nblk; ++k) {
+    const float* rp = base + (r0 + ((int64_t)k << lp)) * ld;
+    float bs = 0.f;
+    for (int i0 = 0; i0 < step; i0 += 16) {
+      float v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v[u] = rp[(int64_t)(i0 + u) * ld];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        bs = __fadd_rn(bs, v[u]);
+        const double d = (double)v[u] - x0;
+        p += d;
+        q = fma(d, d, q);
+      }
+    }
+    acc1 = __fadd_rn(acc1, bs);
   }
-  const int o = g ? 2 * F : 0;
-  bn_column(sm, sq, true, n, mode, g ? mom_g : mom_f, g ? eps_g : eps_f, eps_std,
-            (g ? rm_g : rm_f) + k, (g ? rv_g : rv_f) + k, coef + o + k, coef + o + F + k,
-            batch_out ? batch_out + o + k : nullptr, batch_out ? batch_out + o + F + k : nullptr);
+  if (sb == nsb - 1) {        // the tail rows (B mod step) follow the last complete block
+    float ts = 0.f;
+    for (int64_t r = (int64_t)nblk_all << lp; r < B; ++r) {
+      const float v = base[r * ld];
+      ts = __fadd_rn(ts, v);
+      const double d = (double)v - x0;
+      p += d;
+      q = fma(d, d, q);
+    }
+    tail[c] = ts;
+  }
+  const int64_t o = (int64_t)c * nsb + sb;
+  sb_sum[o] = acc1;
+  sb_p[o] = p;
+  sb_q[o] = q;
+}
+
+// pass 0: buf[t][c] = fp32 sum of chunk t; pass 1: fp32 fma chain of
+// (x - mean)^2 with mean = (float)(sum_t buf0[t][c] / B)  (CONTIG columns)
+__global__ void __launch_bounds__(256)
+bn_contig_chunk_kernel(const float* __restrict__ X, int64_t ldx, const float* __restrict__ G,
+                       int64_t ldg, int B, int F, int C, int arith_x, int arith_g, int T,
+                       int chunk, int pass, const float* __restrict__ buf0,
+                       float* __restrict__ buf) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  const int t = blockIdx.y;
+  if (c >= C || (c < F ? arith_x : arith_g) != kBnContig) return;
+  int64_t ld;
+  const float* base = bn_col_base(X, ldx, G, ldg, F, c, &ld);
+  const int64_t r0 = (int64_t)t * chunk, r1 = min((int64_t)B, r0 + chunk);
+  float s = 0.f;
+  if (pass == 0) {
+    for (int64_t r = r0; r < r1; ++r) s = __fadd_rn(s, base[r * ld]);
+  } else {
+    double m = 0.0;
+    for (int u = 0; u < T; ++u) m += (double)buf0[(int64_t)u * C + c];
+    const float mean = (float)(m / (double)B);
+    for (int64_t r = r0; r < r1; ++r) {
+      const float d = __fsub_rn(base[r * ld], mean);
+      s = fmaf(d, d, s);
+    }
+  }
+  buf[(int64_t)t * C + c] = s;
+}
+
+__global__ void __launch_bounds__(64)
+bn_aten_finalize_kernel(const float* __restrict__ X, int64_t ldx, const float* __restrict__ G,
+                        int64_t ldg, int B, int F, int C, int lp, int nsb,
+                        const float* __restrict__ sb_sum, const double* __restrict__ sb_p,
+                        const double* __restrict__ sb_q, const float* __restrict__ tail,
+                        int T, const float* __restrict__ cbuf0, const float* __restrict__ cbuf1,
+                        BnArgs a) {
+  extern __shared__ float sbs[];          // [nsb] superblock sums of this column, then
+                                          // [nsb >> lp] level-2 group sums
+  const int c = blockIdx.x, lane = threadIdx.x;
+  const int64_t o = (int64_t)c * nsb;
+  double p = 0.0, q = 0.0;
+  for (int i = lane; i < nsb; i += 64) {
+    sbs[i] = sb_sum[o + i];
+    p += sb_p[o + i];
+    q += sb_q[o + i];
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {   // fixed butterfly: deterministic
+    p += __shfl_xor(p, off);
+    q += __shfl_xor(q, off);
+  }
+  __syncthreads();
+  const int step = 1 << lp;
+  const int nblk = B >> lp, nsb_full = nblk >> lp, ngr = nsb_full >> lp;
+  float* grp = sbs + nsb;                 // [ngr] level-2 group sums, one lane each
+  for (int gi = lane; gi < ngr; gi += 64) {
+    float acc2 = 0.f;
+    for (int k = 0; k < step; ++k) acc2 = __fadd_rn(acc2, sbs[gi * step + k]);
+    grp[gi] = acc2;
+  }
+  __syncthreads();
+  if (lane != 0) return;
+  float acc3 = 0.f;
+  for (int gi = 0; gi < ngr; ++gi) acc3 = __fadd_rn(acc3, grp[gi]);
+  float acc2 = 0.f;
+  for (int k = ngr * step; k < nsb_full; ++k) acc2 = __fadd_rn(acc2, sbs[k]);
+  const float acc1 = nsb_full < nsb ? sbs[nsb_full] : 0.f;
+  const float total = __fadd_rn(__fadd_rn(__fadd_rn(tail[c], acc1), acc2), acc3);
+  const bool g = c >= F;
+  const int k = g ? c - F : c;
+  const int arith = g ? a.arith_g : a.arith_x;
+  int64_t ld;
+  const double x0 = (double)bn_col_base(X, ldx, G, ldg, F, c, &ld)[0];
+  const double nd = (double)B;
+  BnCol st;
+  st.tmean = __fdiv_rn(total, (float)B);
+  double vs_exact = q - p * (p / nd);       // sum (x - exact mean)^2
+  if (vs_exact < 0.0) vs_exact = 0.0;
+  st.var_u = B > 1 ? vs_exact / (nd - 1.0) : NAN;
+  if (arith == kBnContig) {
+    double s = 0.0, v = 0.0;
+    for (int u = 0; u < T; ++u) {
+      s += (double)cbuf0[(int64_t)u * C + c];
+      v += (double)cbuf1[(int64_t)u * C + c];
+    }
+    st.mean = (float)(s / nd);
+    st.var_sum = (double)(float)v;
+  } else if (arith == kBnStrided) {
+    st.mean = st.tmean;
+    const double dm = (double)st.mean - x0;
+    double vs = q - dm * (2.0 * p - nd * dm);  // sum (x - mean)^2 about the float mean
+    st.var_sum = vs < 0.0 ? 0.0 : vs;
+  } else {
+    const double md = x0 + p / nd;
+    st.mean = (float)md;
+    st.var_sum = vs_exact;
+  }
+  bn_emit(a, F, g, k, st, true, (int64_t)B);
 }
 
 // ---------------------------------------------------------------------------
@@ -626,7 +861,7 @@ vq_assign_kernel(const float* __restrict__ X, int64_t ldx,
   if (nchunks == 1) stage_chunk<KC, NT>(E, ldw, W, 0, M, chunk, qs, cb, se, tid);
 
   // k-slot k = kc*4 + q of this lane: column, normalisation coefficients
-  float al[KC], be[KC];
+  float al[KC], be[KC], sh[KC];
   bool isg[KC], kval[KC];
   int colx[KC];
 #pragma unroll
@@ -641,6 +876,7 @@ vq_assign_kernel(const float* __restrict__ X, int64_t ldx,
     colx[kc] = c;
     al[kc] = kval[kc] ? coef[(isg[kc] ? 2 * F : 0) + c] : 0.f;
     be[kc] = kval[kc] ? coef[(isg[kc] ? 3 * F : F) + c] : 0.f;
+    sh[kc] = kval[kc] ? coef[(isg[kc] ? 5 * F : 4 * F) + c] : 0.f;
   }
 
   auto act = [&](int r) {
@@ -707,7 +943,7 @@ vq_assign_kernel(const float* __restrict__ X, int64_t ldx,
     for (int g = 0; g < NG; ++g) {
 #pragma unroll
       for (int kc = 0; kc < KC; ++kc) {
-        float v = fmaf(nxt[g][kc], al[kc], be[kc]);       // BatchNorm1d (ATen: fma)
+        float v = fmaf(__fsub_rn(nxt[g][kc], sh[kc]), al[kc], be[kc]);   // BatchNorm1d (bn_apply)
         if (isg[kc]) v = __fmul_rn(v, grad_scale);        // vq.py:224
         xk[g][kc] = kval[kc] ? v : 0.f;                   // padded k-slots are 0
       }
@@ -1058,7 +1294,7 @@ vq_assign_filter_kernel(const float* __restrict__ X, int64_t ldx,
 
   // k-slot kc*4 + q of this lane: column, normalisation coefficients (as the
   // exact kernel, WM == 2 for W = 8: features then gradients)
-  float al[KC], be[KC];
+  float al[KC], be[KC], sh[KC];
   bool isg[KC];
   int colx[KC];
 #pragma unroll
@@ -1070,6 +1306,7 @@ vq_assign_filter_kernel(const float* __restrict__ X, int64_t ldx,
     colx[kc] = c;
     al[kc] = coef[(isg[kc] ? 2 * F : 0) + c];
     be[kc] = coef[(isg[kc] ? 3 * F : F) + c];
+    sh[kc] = coef[(isg[kc] ? 5 * F : 4 * F) + c];
   }
   const int part_begin = part * rows_per_part;
   const int part_end = min(B, part_begin + rows_per_part);
@@ -1124,7 +1361,7 @@ vq_assign_filter_kernel(const float* __restrict__ X, int64_t ldx,
     for (int g = 0; g < NG; ++g) {
 #pragma unroll
       for (int kc = 0; kc < KC; ++kc) {
-        float v = fmaf(nxt[g][kc], al[kc], be[kc]);       // BatchNorm1d (ATen: fma)
+        float v = fmaf(__fsub_rn(nxt[g][kc], sh[kc]), al[kc], be[kc]);   // BatchNorm1d (bn_apply)
         if (isg[kc]) v = __fmul_rn(v, grad_scale);        // vq.py:224
         xk[g][kc] = v;
       }
@@ -1365,7 +1602,8 @@ vq_ema_partial_kernel(const float* __restrict__ X, int64_t ldx,
         const bool g = k >= D;
         const int c = g ? b * D + (k - D) : b * D + k;
         const float raw = g ? Gr[(int64_t)r * ldg + c] : X[(int64_t)r * ldx + c];
-        float v = fmaf(raw, coef[(g ? 2 * F : 0) + c], coef[(g ? 3 * F : F) + c]);
+        float v = fmaf(__fsub_rn(raw, coef[(g ? 5 * F : 4 * F) + c]), coef[(g ? 2 * F : 0) + c],
+                       coef[(g ? 3 * F : F) + c]);
         if (g) v = __fmul_rn(v, grad_scale);
         atomicAdd(a + k1, to_fixed(v, g ? shift_g : shift_f));
       }
@@ -1505,9 +1743,43 @@ vq_ema_finalize_kernel(long long* __restrict__ stats, int nparts, int64_t part_s
 // ===========================================================================
 using namespace vqgnn;
 
-extern "C" size_t vqgnn_bn_stats_workspace(int32_t B, int32_t F) {
+// ATen-arithmetic workspace layout (after the FP64 partials): superblock
+// sums [C][nsb] f32, P and Q [C][nsb] f64, tail [C] f32, CONTIG chunk
+// buffers 2 x [T][C] f32.
+constexpr int kMaxRefThreads = 1024;
+
+struct CascadeGeom {
+  int lp, nsb;
+};
+
+static CascadeGeom cascade_geom(int B) {
+  int cl = 0;
+  while ((int64_t(1) << cl) < (int64_t)B) ++cl;     // CeilLog2
+  CascadeGeom g;
+  g.lp = std::max(4, cl / 4);
+  const int64_t sbrows = int64_t(1) << (2 * g.lp);
+  g.nsb = (int)(((int64_t)B + sbrows - 1) / sbrows);
+  if (g.nsb < 1) g.nsb = 1;
+  return g;
+}
+
+static size_t fp64_ws_bytes(int B, int F) {
   const int C4 = (2 * F + 3) / 4;  // worst case with grads
   return align_up((size_t)stats_chunks(B, C4) * 2 * C4 * 4 * sizeof(double), 256);
+}
+
+static size_t aten_ws_bytes(int B, int F) {
+  const int C = 2 * F;
+  const CascadeGeom g = cascade_geom(B);
+  size_t s = align_up((size_t)C * g.nsb * sizeof(float), 256);
+  s += 2 * align_up((size_t)C * g.nsb * sizeof(double), 256);
+  s += align_up((size_t)C * sizeof(float), 256);
+  s += 2 * align_up((size_t)kMaxRefThreads * C * sizeof(float), 256);
+  return s;
+}
+
+extern "C" size_t vqgnn_bn_stats_workspace(int32_t B, int32_t F) {
+  return std::max(fp64_ws_bytes(B, F), aten_ws_bytes(B, F));
 }
 
 extern "C" int vqgnn_bn_stats(const float* X, int64_t ldx, const float* G, int64_t ldg,
@@ -1539,56 +1811,132 @@ extern "C" int vqgnn_bn_stats(const float* X, int64_t ldx, const float* G, int64
   return check_launch("bn_stats");
 }
 
+static BnArgs bn_args(int mode, int arith_x, int arith_g, double mom_f, double eps_f,
+                      double mom_g, double eps_g, double eps_std, float* rm_f, float* rv_f,
+                      float* rm_g, float* rv_g, float* coef, float* batch_out, int64_t* nbt_f,
+                      int64_t* nbt_g, int nbt_d) {
+  BnArgs a;
+  a.mode = mode;
+  a.arith_x = arith_x;
+  a.arith_g = arith_g;
+  a.mom_f = mom_f;
+  a.eps_f = eps_f;
+  a.mom_g = mom_g;
+  a.eps_g = eps_g;
+  a.eps_std = eps_std;
+  a.rm_f = rm_f;
+  a.rv_f = rv_f;
+  a.rm_g = rm_g;
+  a.rv_g = rv_g;
+  a.coef = coef;
+  a.batch_out = batch_out;
+  a.nbt_f = reinterpret_cast<long long*>(nbt_f);
+  a.nbt_g = reinterpret_cast<long long*>(nbt_g);
+  a.D = nbt_d;
+  return a;
+}
+
+static bool arith_ok(int a) { return a == kBnFp64 || a == kBnStrided || a == kBnContig; }
+
 extern "C" int vqgnn_bn_finalize(const double* sums, int64_t count, int32_t F, int32_t with_grad,
-                                 int32_t mode, float momentum_f, float eps_f, float momentum_g,
-                                 float eps_g, float eps_std, float* rm_f, float* rv_f,
+                                 int32_t mode, int32_t arith_x, int32_t arith_g,
+                                 double momentum_f, double eps_f, double momentum_g,
+                                 double eps_g, double eps_std, float* rm_f, float* rv_f,
                                  float* rm_g, float* rv_g, float* coef, float* batch_out,
                                  int64_t* nbt_f, int64_t* nbt_g, int32_t nbt_d,
                                  vqgnn_stream_t stream) {
   clear_error();
   VQGNN_REQUIRE(F > 0 && coef && rm_f && rv_f, "bn_finalize: bad arguments");
   VQGNN_REQUIRE(mode >= 0 && mode <= 3, "bn_finalize: mode must be 0..3");
+  VQGNN_REQUIRE(arith_ok(arith_x) && arith_ok(arith_g), "bn_finalize: bad arithmetic code");
   VQGNN_REQUIRE(mode == 0 || (sums && count > 0), "bn_finalize: sums/count required");
   VQGNN_REQUIRE(!with_grad || (rm_g && rv_g), "bn_finalize: grad running stats required");
+  // batch statistics from fp64 sums follow the FP64 arithmetic; the eval
+  // coefficients take the form of the requested path
+  const bool batch = mode != 0;
+  const BnArgs a = bn_args(mode, batch ? kBnFp64 : arith_x, batch ? kBnFp64 : arith_g,
+                           momentum_f, eps_f, momentum_g, eps_g, eps_std, rm_f, rv_f, rm_g,
+                           rv_g, coef, batch_out, nbt_f, nbt_g, nbt_d);
   hipLaunchKernelGGL(bn_finalize_kernel, dim3((F + 255) / 256), dim3(256), 0, as_stream(stream),
-                     sums, count, F, with_grad, mode, momentum_f, eps_f, momentum_g, eps_g,
-                     eps_std, rm_f, rv_f, rm_g, rv_g, coef, batch_out,
-                     reinterpret_cast<long long*>(nbt_f), reinterpret_cast<long long*>(nbt_g),
-                     nbt_d);
+                     sums, count, F, with_grad, a);
   return check_launch("bn_finalize");
 }
 
 extern "C" int vqgnn_bn_stats_finalize(const float* X, int64_t ldx, const float* G, int64_t ldg,
                                        int32_t B, int32_t F, int32_t with_grad, double* sums,
-                                       int32_t mode, float momentum_f, float eps_f,
-                                       float momentum_g, float eps_g, float eps_std, float* rm_f,
-                                       float* rv_f, float* rm_g, float* rv_g, float* coef,
-                                       float* batch_out, int64_t* nbt_f, int64_t* nbt_g,
-                                       int32_t nbt_d, void* workspace, vqgnn_stream_t stream) {
+                                       int32_t mode, int32_t arith_x, int32_t arith_g,
+                                       int32_t ref_threads, double momentum_f, double eps_f,
+                                       double momentum_g, double eps_g, double eps_std,
+                                       float* rm_f, float* rv_f, float* rm_g, float* rv_g,
+                                       float* coef, float* batch_out, int64_t* nbt_f,
+                                       int64_t* nbt_g, int32_t nbt_d, void* workspace,
+                                       vqgnn_stream_t stream) {
   clear_error();
   VQGNN_REQUIRE(X && coef && rm_f && rv_f && workspace, "bn_stats_finalize: null pointer");
   VQGNN_REQUIRE(B > 0 && F > 0 && ldx >= F, "bn_stats_finalize: bad shape B=%d F=%d", B, F);
-  VQGNN_REQUIRE(mode >= 1 && mode <= 3, "bn_stats_finalize: mode must use batch statistics");
+  VQGNN_REQUIRE(B <= (1 << 23), "bn_stats_finalize: B=%d rows exceed 2^23", B);
+  VQGNN_REQUIRE(mode >= 0 && mode <= 3, "bn_stats_finalize: mode must be 0..3");
   VQGNN_REQUIRE(!with_grad || (G && ldg >= F && rm_g && rv_g), "bn_stats_finalize: grads required");
-  const bool vec = F % 4 == 0 && ldx % 4 == 0 && ((uintptr_t)X & 15) == 0 &&
-                   (!with_grad || (ldg % 4 == 0 && ((uintptr_t)G & 15) == 0));
+  VQGNN_REQUIRE(arith_ok(arith_x) && arith_ok(arith_g), "bn_stats_finalize: bad arithmetic code");
+  const bool contig = arith_x == kBnContig || (with_grad && arith_g == kBnContig);
+  VQGNN_REQUIRE(!contig || (ref_threads >= 1 && ref_threads <= kMaxRefThreads),
+                "bn_stats_finalize: ref_threads=%d outside 1..%d", ref_threads, kMaxRefThreads);
   const int C = with_grad ? 2 * F : F;
-  const int C4 = (C + 3) / 4;
-  const int chunks = stats_chunks(B, C4);
-  const int rpc = (B + chunks - 1) / chunks;
-  double* part = reinterpret_cast<double*>(workspace);
+  const BnArgs a = bn_args(mode, arith_x, with_grad ? arith_g : kBnFp64, momentum_f, eps_f,
+                           momentum_g, eps_g, eps_std, rm_f, rv_f, rm_g, rv_g, coef, batch_out,
+                           nbt_f, nbt_g, nbt_d);
   hipStream_t s = as_stream(stream);
-  if (vec) {
-    hipLaunchKernelGGL(bn_stats_partial_kernel, dim3(chunks), dim3(kStatsThreads), 0, s, X, ldx,
-                       G, ldg, B, F / 4, C4, rpc, part);
-  } else {
-    hipLaunchKernelGGL(bn_stats_partial_scalar_kernel, dim3(chunks), dim3(kStatsThreads), 0, s,
-                       X, ldx, G, ldg, B, F, C, rpc, part);
+  if (arith_x == kBnFp64 && (!with_grad || arith_g == kBnFp64)) {
+    const bool vec = F % 4 == 0 && ldx % 4 == 0 && ((uintptr_t)X & 15) == 0 &&
+                     (!with_grad || (ldg % 4 == 0 && ((uintptr_t)G & 15) == 0));
+    const int C4 = (C + 3) / 4;
+    const int chunks = stats_chunks(B, C4);
+    const int rpc = (B + chunks - 1) / chunks;
+    double* part = reinterpret_cast<double*>(workspace);
+    if (vec) {
+      hipLaunchKernelGGL(bn_stats_partial_kernel, dim3(chunks), dim3(kStatsThreads), 0, s, X,
+                         ldx, G, ldg, B, F / 4, C4, rpc, part);
+    } else {
+      hipLaunchKernelGGL(bn_stats_partial_scalar_kernel, dim3(chunks), dim3(kStatsThreads), 0,
+                         s, X, ldx, G, ldg, B, F, C, rpc, part);
+    }
+    hipLaunchKernelGGL(bn_reduce_finalize_kernel, dim3((C + 31) / 32), dim3(kRfThreads), 0, s,
+                       part, chunks, F, C, sums, (int64_t)B, a);
+    return check_launch("bn_stats_finalize");
   }
-  hipLaunchKernelGGL(bn_reduce_finalize_kernel, dim3((C + 31) / 32), dim3(kRfThreads), 0, s, part, chunks, F, C, sums, (int64_t)B, mode,
-                     momentum_f, eps_f, momentum_g, eps_g, eps_std, rm_f, rv_f, rm_g, rv_g, coef,
-                     batch_out, reinterpret_cast<long long*>(nbt_f),
-                     reinterpret_cast<long long*>(nbt_g), nbt_d);
+  VQGNN_REQUIRE(sums == nullptr, "bn_stats_finalize: fp64 sums exist only for the FP64 arithmetic");
+  const CascadeGeom g = cascade_geom(B);
+  char* w = reinterpret_cast<char*>(workspace);
+  float* sb_sum = reinterpret_cast<float*>(w);
+  w += align_up((size_t)C * g.nsb * sizeof(float), 256);
+  double* sb_p = reinterpret_cast<double*>(w);
+  w += align_up((size_t)C * g.nsb * sizeof(double), 256);
+  double* sb_q = reinterpret_cast<double*>(w);
+  w += align_up((size_t)C * g.nsb * sizeof(double), 256);
+  float* tail = reinterpret_cast<float*>(w);
+  w += align_up((size_t)C * sizeof(float), 256);
+  float* cb0 = reinterpret_cast<float*>(w);
+  w += align_up((size_t)kMaxRefThreads * C * sizeof(float), 256);
+  float* cb1 = reinterpret_cast<float*>(w);
+  const int ntiles = (C + 63) / 64;
+  const int waves = g.nsb * ntiles;
+  hipLaunchKernelGGL(bn_cascade_partial_kernel, dim3((waves + kCasWaves - 1) / kCasWaves),
+                     dim3(kCasWaves * 64), 0, s, X, ldx, G, ldg, B, F, C, g.lp, g.nsb, ntiles,
+                     sb_sum, sb_p, sb_q, tail);
+  int T = 1;
+  if (contig) {
+    // at::parallel_for(0, B, 1): min(T, B) threads of ceil(B / threads) rows
+    T = std::min(ref_threads, B);
+    const int chunk = (B + T - 1) / T;
+    const dim3 grid((C + 255) / 256, T);
+    hipLaunchKernelGGL(bn_contig_chunk_kernel, grid, dim3(256), 0, s, X, ldx, G, ldg, B, F, C,
+                       arith_x, with_grad ? arith_g : kBnFp64, T, chunk, 0, nullptr, cb0);
+    hipLaunchKernelGGL(bn_contig_chunk_kernel, grid, dim3(256), 0, s, X, ldx, G, ldg, B, F, C,
+                       arith_x, with_grad ? arith_g : kBnFp64, T, chunk, 1, cb0, cb1);
+  }
+  const size_t fin_lds = (size_t)(g.nsb + (g.nsb >> g.lp) + 1) * sizeof(float);
+  hipLaunchKernelGGL(bn_aten_finalize_kernel, dim3(C), dim3(64), fin_lds, s, X,
+                     ldx, G, ldg, B, F, C, g.lp, g.nsb, sb_sum, sb_p, sb_q, tail, T, cb0, cb1, a);
   return check_launch("bn_stats_finalize");
 }
 

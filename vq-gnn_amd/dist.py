@@ -37,6 +37,11 @@ class CodebookSync:
         wait() orders the current stream after the collective)."""
         return dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=async_op)
 
+    def allreduce_stats_(self, sums: torch.Tensor, B: int) -> int:
+        """All-reduce the fp64 BatchNorm sums in place -> global row count."""
+        self.allreduce_(sums)
+        return self.global_count(B)
+
     def global_count(self, B: int) -> int:
         if B in self._count_cache:
             return self._count_cache[B]

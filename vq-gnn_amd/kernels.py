@@ -14,6 +14,8 @@ from ._lib import check, lib, ptr, require_gpu, stream_ptr, workspace
 
 # bn_finalize modes (include/vqgnn.h §2)
 BN_EVAL, BN_TRAIN, BN_TRAIN_INIT, BN_EVAL_INIT = 0, 1, 2, 3
+# BatchNorm arithmetic of an input (include/vqgnn.h §2, oracle/bn_ref.py)
+BN_FP64, BN_STRIDED, BN_CONTIG = 0, 1, 2
 
 
 def _ld(t: torch.Tensor) -> int:
@@ -21,6 +23,13 @@ def _ld(t: torch.Tensor) -> int:
         raise ValueError(f"expected a row-major 2-D view, got shape {tuple(t.shape)} "
                          f"strides {t.stride()}")
     return t.stride(0)
+
+
+def bn_arith_of(t: torch.Tensor, D: int) -> int:
+    """The ATen BatchNorm path the reference takes for each D-column branch
+    slice of ``t`` [B, nb*D]: contiguous iff the slice is (row stride D, or
+    one row), else strided (models.py:162-165 slices x[:, D*i:D*(i+1)])."""
+    return BN_CONTIG if (_ld(t) == D or t.shape[0] <= 1) else BN_STRIDED
 
 
 def bn_stats(X: torch.Tensor, G: torch.Tensor | None, F: int) -> torch.Tensor:
@@ -37,17 +46,26 @@ def bn_stats(X: torch.Tensor, G: torch.Tensor | None, F: int) -> torch.Tensor:
     return sums
 
 
+def _coef(F, with_grad, dev):
+    coef = torch.empty(6, F, dtype=torch.float32, device=dev)
+    if not with_grad:
+        coef[2:4].zero_()
+        coef[5].zero_()
+    return coef
+
+
 def bn_finalize(sums, count, F, with_grad, mode, mom_f, eps_f, mom_g, eps_g, eps_std,
                 rm_f, rv_f, rm_g=None, rv_g=None, want_batch=False, nbt_f=None, nbt_g=None,
-                D=0):
-    """-> (coef [4, F], batch_out [4, F] or None); updates running stats in place
-    and, when given, num_batches_tracked (nbt_f / nbt_g [F // D] int64) += 1."""
+                D=0, arith_x=BN_FP64, arith_g=BN_FP64):
+    """-> (coef [6, F], batch_out [4, F] or None); updates running stats in place
+    and, when given, num_batches_tracked (nbt_f / nbt_g [F // D] int64) += 1.
+    Batch statistics come from the fp64 sums (FP64 arithmetic); arith_x /
+    arith_g choose the form of the eval coefficients."""
     dev = rm_f.device
-    coef = torch.empty(4, F, dtype=torch.float32, device=dev)
-    if not with_grad:
-        coef[2:].zero_()
+    coef = _coef(F, with_grad, dev)
     batch = torch.empty(4, F, dtype=torch.float32, device=dev) if want_batch else None
     check(lib().vqgnn_bn_finalize(ptr(sums), int(count), F, int(with_grad), int(mode),
+                                  int(arith_x), int(arith_g),
                                   float(mom_f), float(eps_f), float(mom_g), float(eps_g),
                                   float(eps_std), ptr(rm_f), ptr(rv_f), ptr(rm_g), ptr(rv_g),
                                   ptr(coef), ptr(batch), ptr(nbt_f), ptr(nbt_g), int(D),
@@ -57,22 +75,22 @@ def bn_finalize(sums, count, F, with_grad, mode, mom_f, eps_f, mom_g, eps_g, eps
 
 def bn_stats_finalize(X, G, F, mode, mom_f, eps_f, mom_g, eps_g, eps_std, rm_f, rv_f,
                       rm_g=None, rv_g=None, want_batch=False, nbt_f=None, nbt_g=None, D=0,
-                      want_sums=False):
-    """bn_stats + bn_finalize for a single process (count = B): the reduce and
-    the finalize run as one kernel.  -> (coef, batch_out or None, sums or None)."""
+                      want_sums=False, arith_x=BN_FP64, arith_g=BN_FP64, ref_threads=1):
+    """Batch statistics + finalize for a single process (count = B) in the
+    given arithmetic (BN_FP64 / BN_STRIDED / BN_CONTIG per half).
+    -> (coef [6, F], batch_out or None, sums or None); sums only for FP64."""
     require_gpu(X, "bn_stats_finalize")
     B = X.shape[0]
     dev = X.device
     with_grad = G is not None
     L = lib()
     ws = workspace(L.vqgnn_bn_stats_workspace(B, F), dev)
-    coef = torch.empty(4, F, dtype=torch.float32, device=dev)
-    if not with_grad:
-        coef[2:].zero_()
+    coef = _coef(F, with_grad, dev)
     batch = torch.empty(4, F, dtype=torch.float32, device=dev) if want_batch else None
     sums = torch.zeros(4, F, dtype=torch.float64, device=dev) if want_sums else None
     check(L.vqgnn_bn_stats_finalize(ptr(X), _ld(X), ptr(G), _ld(G) if with_grad else 0, B, F,
-                                    int(with_grad), ptr(sums), int(mode), float(mom_f),
+                                    int(with_grad), ptr(sums), int(mode), int(arith_x),
+                                    int(arith_g), int(ref_threads), float(mom_f),
                                     float(eps_f), float(mom_g), float(eps_g), float(eps_std),
                                     ptr(rm_f), ptr(rv_f), ptr(rm_g), ptr(rv_g), ptr(coef),
                                     ptr(batch), ptr(nbt_f), ptr(nbt_g), int(D), ptr(ws),

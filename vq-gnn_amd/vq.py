@@ -10,11 +10,18 @@ views of its slice under the reference's buffer names (``_embedding``,
 ``batch_norm_feat.running_mean`` ...), and ``state_dict()`` /
 ``load_state_dict()`` use the reference's keys.
 
-Numerics.  BatchNorm statistics are fp64 sums on the GPU; the normalisation,
-distance and argmin follow ATen's CPU arithmetic exactly (see
-csrc/vq_kernels.hip), so codeword indices equal the reference's for equal
-normalisation coefficients; EMA sums are fp32 with a different summation
-order than MKL's one-hot sgemm (tolerance-tested).
+Numerics.  BatchNorm follows the ATen CPU path the reference takes for the
+same input layout (``bn_arith = "aten"``, the default on one process): the
+cascade-sum statistics of a strided branch slice, or the per-thread row
+chunks of a contiguous [B, D] input with ``ref_threads`` threads (see
+include/vqgnn.h §2 and oracle/bn_ref.py).  With multi-GPU statistics
+(``comm`` set) or ``bn_arith = "fp64"`` the batch statistics are fp64 sums,
+identical for any number of ranks.  The normalisation, distance and argmin
+follow ATen's CPU arithmetic exactly (csrc/vq_kernels.hip), so codeword
+indices are bit-exact.  The EMA statistics (counts and encodingsᵀ·x_norm)
+are int64 fixed-point sums, exact and order-free, rounded to fp32 once
+(DESIGN §2.2); the reference's MKL sgemm sums them in fp32 in an order of
+its own, so EMA state matches within the documented bound.
 """
 from __future__ import annotations
 
@@ -24,7 +31,8 @@ import torch
 from torch import nn
 
 from . import kernels
-from .kernels import BN_EVAL, BN_EVAL_INIT, BN_TRAIN, BN_TRAIN_INIT
+from .kernels import (BN_EVAL, BN_EVAL_INIT, BN_FP64, BN_TRAIN, BN_TRAIN_INIT,
+                      bn_arith_of)
 
 # 'Bad Init!' (vq.py:188) is a device flag.  The reference checks it with a
 # host sync on every call; VQGNN_DEFER_BAD_INIT=1 defers the check to
@@ -85,6 +93,13 @@ class VQBank(nn.Module):
         # last batched call's logging stash (vq.py:208-214, :276-277)
         self.last_batch = None       # [4, nb*D] mean_f, std_f, mean_g, std_g
         self.last_inputs = None      # (X, G) of the last update()
+        # BatchNorm arithmetic: "aten" reproduces the reference's ATen CPU
+        # path for the input layout; "fp64" = rank-count-invariant fp64 sums
+        # (always used with multi-GPU statistics).  ref_threads: the
+        # reference's torch.get_num_threads() for contiguous inputs (None:
+        # VQGNN_REF_THREADS, else this process's torch.get_num_threads()).
+        self.bn_arith = "aten"
+        self.ref_threads = None
 
     def init_branch(self, b):
         """Per-branch random init in the reference's RNG order (vq.py:73-98)."""
@@ -158,6 +173,19 @@ class VQBank(nn.Module):
     def _sel(self, b0, nbr):
         return slice(b0, b0 + nbr)
 
+    def _threads(self):
+        if self.ref_threads is not None:
+            return int(self.ref_threads)
+        env = os.environ.get("VQGNN_REF_THREADS")
+        return int(env) if env else torch.get_num_threads()
+
+    def _arith(self, t, comm):
+        """(arith for batch statistics, arith for the eval form) of input t."""
+        layout = bn_arith_of(t, self.D)
+        if comm is not None or self.bn_arith == "fp64":
+            return BN_FP64, layout
+        return layout, layout
+
     def feature_update(self, X, b0, nbr, training, idx_out=None, codes=None, batch_idx=None):
         """vq.py:160-202 for branches [b0, b0+nbr): X is [B, nbr*D] (a row-major view)."""
         self.finish_update()
@@ -168,22 +196,23 @@ class VQBank(nn.Module):
         if training and B <= 1:
             raise ValueError("Expected more than 1 value per channel when training")
         comm = self.comm if training else None
-        if training and comm is None:      # one process: reduce + finalize fused
+        ax, ax_eval = self._arith(X, comm)
+        if training and comm is None:      # one process: statistics + finalize
             count = B
             coef, _, _ = kernels.bn_stats_finalize(X, None, F, BN_TRAIN, 0.1, 1e-5, 0.0, 0.0,
                                                    0.0, self.rm_f[sl], self.rv_f[sl],
-                                                   nbt_f=self.nbt_f[sl], D=D)
+                                                   nbt_f=self.nbt_f[sl], D=D, arith_x=ax,
+                                                   ref_threads=self._threads())
         elif training:
             sums = kernels.bn_stats(X, None, F)
-            comm.allreduce_(sums)
-            count = comm.global_count(B)
+            count = comm.allreduce_stats_(sums, B)
             coef, _ = kernels.bn_finalize(sums, count, F, False, BN_TRAIN, 0.1, 1e-5, 0.0, 0.0,
                                           0.0, self.rm_f[sl], self.rv_f[sl], nbt_f=self.nbt_f[sl],
                                           D=D)
         else:
             count = B
             coef, _ = kernels.bn_finalize(None, B, F, False, BN_EVAL, 0.1, 1e-5, 0.0, 0.0, 0.0,
-                                          self.rm_f[sl], self.rv_f[sl])
+                                          self.rm_f[sl], self.rv_f[sl], arith_x=ax_eval)
         slab = self._slab(D, b0, nbr) if training else None
         local = None
         if comm is not None and codes is not None:
@@ -251,14 +280,17 @@ class VQBank(nn.Module):
                    self.rv_f[sl], self.rm_g[sl], self.rv_g[sl])
         bn_kw = dict(want_batch=True, nbt_f=self.nbt_f[sl] if training else None,
                      nbt_g=self.nbt_g[sl] if training else None, D=D)
-        if comm is None and mode != BN_EVAL:   # one process: reduce + finalize fused
-            coef, batch, _ = kernels.bn_stats_finalize(X, G, F, *bn_args, **bn_kw)
+        ax, ax_eval = self._arith(X, comm)
+        ag, ag_eval = self._arith(G, comm)
+        if comm is None:   # one process: statistics + finalize (the stash in every mode)
+            coef, batch, _ = kernels.bn_stats_finalize(X, G, F, *bn_args, **bn_kw, arith_x=ax,
+                                                       arith_g=ag,
+                                                       ref_threads=self._threads())
         else:
             sums = kernels.bn_stats(X, G, F)
-            if comm is not None:
-                comm.allreduce_(sums)
-                count = comm.global_count(B)
-            coef, batch = kernels.bn_finalize(sums, count, F, True, *bn_args, **bn_kw)
+            count = comm.allreduce_stats_(sums, B)
+            coef, batch = kernels.bn_finalize(sums, count, F, True, *bn_args, **bn_kw,
+                                              arith_x=ax_eval, arith_g=ag_eval)
         for b in range(b0, b0 + nbr):
             self.bn_inited[b] = True
         self.last_batch = batch
