@@ -279,6 +279,32 @@ int vqgnn_spmm_pair(const int32_t* rowptr, const int32_t* col, const float* val,
                     int32_t F, float* out, int64_t ldo, const int32_t* plan,
                     const int32_t* chunk_plan, void* workspace, vqgnn_stream_t stream);
 
+/* 6e. Task-split SpMM (the default aggregation): out = A * xin as in 6, for
+ *     any F that is a multiple of 4 (column tiles of 128).  The nnz range is
+ *     cut into tasks of K edges; 8 lanes walk one task (a wave: 8 tasks in
+ *     lock-step, balanced whatever the row lengths), gathering each source
+ *     row as 128-byte lines (dwordx4) and accumulating with fma; rows that
+ *     span tasks are finished by a fix-up in task order, empty rows written
+ *     as zeros.  Each row is a sequential fma chain over its edges in CSR
+ *     order: deterministic, within 1e-5 relative of the fp64 sum (north_star
+ *     tolerance; not spmm_sum's separate multiply/add bit pattern).
+ *     Plan (once per batch adjacency, any F): vqgnn_spmm_task_plan fills
+ *     task_row [vqgnn_spmm_task_size(nnz, K)] int32 and records [nnz] int64
+ *     (source column, row-end flag, weight) from the CSR; K = 64 (multiple of
+ *     4 in [8, 4096]).  A call may cover the first n_rows rows of the planned
+ *     CSR (edges [0, rowptr[n_rows])), e.g. the backward's batch rows.
+ *     n_cols < 2^26.  Workspace: vqgnn_spmm_task_workspace(nnz, K, F) bytes.
+ *     Replaces convs.py:95 -> torch_sparse spmm_sum like 6.                  */
+int32_t vqgnn_spmm_task_size(int64_t nnz, int32_t K);
+int vqgnn_spmm_task_plan(const int32_t* rowptr, const int32_t* col, const float* val,
+                         int32_t n_rows, int64_t nnz, int32_t K, int32_t* task_row,
+                         int64_t* records, vqgnn_stream_t stream);
+size_t vqgnn_spmm_task_workspace(int64_t nnz, int32_t K, int32_t F);
+int vqgnn_spmm_task(const int32_t* rowptr, int32_t n_rows, int32_t n_cols, int64_t nnz,
+                    int32_t B, const float* X, int64_t ldx, const float* X2, int64_t ldx2,
+                    int32_t F, float* out, int64_t ldo, const int32_t* task_row,
+                    const int64_t* records, int32_t K, void* workspace, vqgnn_stream_t stream);
+
 /* 7. CSR transpose (structure + values) for the backward product
  *    dX = A^T dOut (torch_sparse matmul autograd, convs.py:95).  Output CSR of
  *    A^T with rows sorted by column of A; within a row, entries ordered by

@@ -1,0 +1,153 @@
+"""GPU parity of the task-split SpMM (include/vqgnn.h §6e, the default
+aggregation kernel) against the fp64 sum: every row within 1e-5 of
+sum |w| |x| (north_star: fp32 messages within 1e-5 relative), on ragged,
+empty, hub and two-source inputs; deterministic across calls."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import conv_ref
+from vq_gnn_amd import graph, kernels
+from vq_gnn_amd.sparse import CSR
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+
+def _dev_csr(rowptr, col, val, n_rows, n_cols):
+    return CSR(torch.as_tensor(np.asarray(rowptr)), torch.as_tensor(np.asarray(col)),
+               torch.as_tensor(np.asarray(val, dtype=np.float32)), (n_rows, n_cols)).to(DEV)
+
+
+def _csr_from_deg(deg, n_cols, rng):
+    rowptr = np.zeros(deg.size + 1, np.int64)
+    rowptr[1:] = np.cumsum(deg)
+    col = np.concatenate([np.sort(rng.choice(n_cols, size=d, replace=d > n_cols))
+                          for d in deg]) if rowptr[-1] else np.zeros(0, np.int64)
+    val = rng.standard_normal(col.shape[0]).astype(np.float32)
+    return rowptr, col.astype(np.int64), val
+
+
+def _check(out, rowptr, col, val, xin, n_rows=None):
+    n = rowptr.size - 1 if n_rows is None else n_rows
+    rp = rowptr[: n + 1]
+    ref = conv_ref.spmm_fp64(rp, col[: rp[-1]], val[: rp[-1]], xin)
+    scale = conv_ref.spmm_fp64(rp, col[: rp[-1]], np.abs(val[: rp[-1]]), np.abs(xin))
+    o = out.cpu().numpy().astype(np.float64)
+    err = np.abs(o - ref)
+    assert (err <= 1e-5 * scale + 1e-30).all(), f"max rel err {(err / (scale + 1e-30)).max():.3e}"
+    empty = np.diff(rp) == 0
+    assert np.all(o[empty] == 0)
+
+
+def _run(a, X, F, X2=None, B=None, n_rows=None, K=None):
+    plan = kernels.spmm_task_plan(a.rowptr, a.col, a.value, a.size(0), a.nnz(), K)
+    nr = a.size(0) if n_rows is None else n_rows
+    return kernels.spmm(a.rowptr, a.col, a.value, nr, a.nnz(), X, F, X2=X2, B=B, plan=plan)
+
+
+@pytest.mark.parametrize("F", [4, 8, 16, 32, 64, 124, 128, 132, 256, 604])
+@pytest.mark.parametrize("K", [8, 64, 256])
+def test_task_spmm_ragged_vs_fp64(F, K):
+    rng = np.random.default_rng(F * 31 + K)
+    deg = rng.integers(0, 24, size=900)
+    deg[rng.random(900) < 0.1] = 0
+    deg[[3, 450, 899]] = [700, 1300, 257]          # rows spanning many tasks
+    rowptr, col, val = _csr_from_deg(deg, 1100, rng)
+    x = rng.standard_normal((1100, F)).astype(np.float32)
+    a = _dev_csr(rowptr, col, val, 900, 1100)
+    xd = torch.from_numpy(x).to(DEV)
+    out = _run(a, xd, F, K=K)
+    _check(out, rowptr, col, val, x)
+    again = _run(a, xd, F, K=K)
+    assert torch.equal(out, again)                 # deterministic
+
+
+def test_task_spmm_two_sources_and_strides():
+    rng = np.random.default_rng(5)
+    B, n2, F = 700, 500, 128
+    deg = rng.integers(1, 40, size=B + n2)
+    rowptr, col, val = _csr_from_deg(deg, B + n2, rng)
+    X = torch.randn(B, F + 12, device=DEV)[:, 4:4 + F]       # ld = F + 12
+    X2 = torch.randn(n2, F, device=DEV)
+    out = torch.full((B + n2, F + 8), 7.0, device=DEV)[:, :F]  # ldo = F + 8
+    a = _dev_csr(rowptr, col, val, B + n2, B + n2)
+    plan = kernels.spmm_task_plan(a.rowptr, a.col, a.value, B + n2, a.nnz())
+    kernels.spmm(a.rowptr, a.col, a.value, B + n2, a.nnz(), X, F, X2=X2, B=B, out=out, plan=plan)
+    xin = torch.cat([X, X2]).cpu().numpy()
+    _check(out, rowptr, col, val, xin)
+
+
+def test_task_spmm_far_path_matches_near():
+    rng = np.random.default_rng(6)
+    B, n2, F = 600, 400, 64
+    rowptr, col, val = _csr_from_deg(rng.integers(0, 30, size=B + n2), B + n2, rng)
+    a = _dev_csr(rowptr, col, val, B + n2, B + n2)
+    X, X2 = torch.randn(B, F, device=DEV), torch.randn(n2, F, device=DEV)
+    near = _run(a, X, F, X2=X2, B=B)
+    os.environ["VQGNN_SPMM_FAR"] = "1"
+    try:
+        far = _run(a, X, F, X2=X2, B=B)
+    finally:
+        del os.environ["VQGNN_SPMM_FAR"]
+    assert torch.equal(near, far)
+
+
+def test_task_spmm_empty_runs_and_degenerate():
+    rng = np.random.default_rng(7)
+    deg = rng.integers(1, 9, size=400)
+    deg[50:120] = 0            # 70 consecutive empty rows: the skip-count escape
+    deg[200:230] = 0           # 30: below the escape
+    deg[-40:] = 0              # trailing empty rows (eval adjacency)
+    deg[:3] = 0                # leading
+    rowptr, col, val = _csr_from_deg(deg, 300, rng)
+    x = rng.standard_normal((300, 32)).astype(np.float32)
+    a = _dev_csr(rowptr, col, val, 400, 300)
+    _check(_run(a, torch.from_numpy(x).to(DEV), 32, K=8), rowptr, col, val, x)
+    z = _dev_csr([0, 0, 0, 0], [], [], 3, 10)
+    out = _run(z, torch.randn(10, 8, device=DEV), 8)
+    assert torch.count_nonzero(out) == 0
+    one = _dev_csr([0, 1], [2], [3.0], 1, 5)
+    xx = torch.randn(5, 4, device=DEV)
+    assert torch.equal(_run(one, xx, 4)[0], 3.0 * xx[2])
+
+
+def test_task_spmm_leading_rows_of_planned_csr():
+    """A call over the first n_rows rows (the backward's batch rows of A^T)
+    uses the plan of the whole CSR and writes only those rows."""
+    rng = np.random.default_rng(8)
+    rowptr, col, val = _csr_from_deg(rng.integers(0, 50, size=1000), 800, rng)
+    a = _dev_csr(rowptr, col, val, 1000, 800)
+    x = rng.standard_normal((800, 128)).astype(np.float32)
+    plan = kernels.spmm_task_plan(a.rowptr, a.col, a.value, 1000, a.nnz())
+    out = torch.full((600, 128), 5.0, device=DEV)
+    kernels.spmm(a.rowptr, a.col, a.value, 600, a.nnz(), torch.from_numpy(x).to(DEV), 128,
+                 out=out, plan=plan)
+    _check(out, rowptr, col, val, x, n_rows=600)
+
+
+def test_task_spmm_arxiv_batch_vs_fp64_and_chunk_kernel():
+    cfg = dict(graph.CONFIGS["arxiv_gcn"])
+    g, _, b = graph.make_batch(cfg)
+    F = 128
+    bidx, subset, adj = graph.batch_to_device(b, DEV)
+    X = torch.randn(b.B, F, device=DEV)
+    X2 = torch.randn(b.n - b.B, F, device=DEV)
+    task = kernels.spmm(adj.rowptr, adj.col, adj.value, b.n, b.nnz, X, F, X2=X2, B=b.B,
+                        plan=adj.plan(F, B=b.B))
+    chunk = kernels.spmm(adj.rowptr, adj.col, adj.value, b.n, b.nnz, X, F, X2=X2, B=b.B,
+                         plan=adj.plan(F, B=b.B, kind="chunk"))
+    xin = torch.cat([X, X2]).cpu().numpy()
+    _check(task, b.rowptr, b.col, b.val, xin)
+    scale = conv_ref.spmm_fp64(b.rowptr, b.col, np.abs(b.val), np.abs(xin))
+    assert (np.abs(task.cpu().numpy() - chunk.cpu().numpy()) <= 2e-5 * scale + 1e-30).all()
+
+
+def test_task_plan_rejects_other_values():
+    a = _dev_csr([0, 2, 3], [0, 1, 1], [1.0, 2.0, 3.0], 2, 2)
+    plan = a.plan(4)
+    with pytest.raises(ValueError, match="other values"):
+        kernels.spmm(a.rowptr, a.col, a.value * 2, 2, 3, torch.randn(2, 4, device=DEV), 4,
+                     plan=plan)

@@ -51,7 +51,8 @@ class GATFunction(torch.autograd.Function):
                                      slope)
         out = kernels.spmm(adj.rowptr, adj.col, coef, n, nnz, xc, F, X2=x_first,
                            B=B if x_first is not None else None,
-                           plan=adj.plan(F, B=B if x_first is not None else None))
+                           plan=adj.plan(F, B=B if x_first is not None else None,
+                                         kind="chunk"))
         if normalize:
             kernels.gat_normalize(out, B, F, den, 1e-16)
         ctx.save_for_backward(xc, x_first if x_first is not None else xc, att_l, att_r, al, ar,
@@ -114,7 +115,7 @@ class GATFunction(torch.autograd.Function):
             t = adj.transposed()
             tcoef = coef[adj.t_perm.long()]
             # rows [0, B) of A_coef^T dy (the merge kernel bounds the walk by nnz)
-            dx = kernels.spmm(t.rowptr, t.col, tcoef, B, nnz, dy, F, plan=t.plan(F, n_rows=B))
+            dx = kernels.spmm(t.rowptr, t.col, tcoef, B, nnz, dy, F, plan=t.plan(F, n_rows=B, kind="chunk"))
             dx += dal[:B, None] * att_l.view(-1)[:F] + dar[:B, None] * att_r.view(-1)[:F]
         return dx, None, d_att_l, d_att_r, None, None, None, None, None, None, None
 

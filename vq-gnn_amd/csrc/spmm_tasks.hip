@@ -1,0 +1,412 @@
+// Task-split CSR SpMM for gfx950 (MI355X): out = A * xin with
+// xin = [X (rows < B) ; X2 (rows >= B)] — LowRankGNNLayer's aggregation
+// (vq_gnn_v2/models.py:174 + convs.py:95: torch_sparse.matmul(adj, x_input,
+// reduce='add')) without materialising the torch.cat.
+//
+// Work split (merge-based SpMM).  The nnz range is cut into tasks of K
+// consecutive edges.  A group of 8 lanes walks one task edge by edge; a wave
+// holds 8 groups, i.e. 8 tasks in lock-step — every group runs exactly K
+// steps, so the wave is balanced whatever the row lengths (arxiv: median 7,
+// max 1,460 edges).  Per step a lane gathers NC float4 pieces of the edge's
+// source row (piece i of lane k is float4 column 8i + k: each gather
+// wave-instruction reads one contiguous 128-byte line per group, 1 KiB per
+// instruction), multiplies by the weight and accumulates with fma.  When the
+// edge ends its row the group stores the row (or, for a row that began in an
+// earlier task, its head partial) and resets; a row still open at the task's
+// end leaves a tail partial.  spmm_task_fixup_kernel adds, for every row
+// that spans tasks, tail[first task] + ... + tail[last-1] + head[last] in
+// task order, and writes zeros to empty rows.
+//
+// Per-batch plan (vqgnn_spmm_task_plan): one 8-byte record per edge — source
+// column (bits 0-25), "row ends here" (bit 31) and the number of empty rows
+// that follow (bits 26-30, 31 = look it up), and the weight — plus the row
+// containing each task's first edge.  The kernel reads no rowptr / col / val.
+//
+// Numerics: each row is a sequential fma chain over its edges in CSR order
+// (rows split across tasks: the task partials added in task order).
+// Deterministic and independent of the launch geometry; within 1e-5 relative
+// of the fp64 sum (north_star tolerance), not the bit pattern of spmm_sum's
+// separate multiply and add.
+
+#include "common.h"
+
+namespace vqgnn {
+
+constexpr int kTaskThreads = 256;             // 4 waves
+constexpr uint32_t kColMask = (1u << 26) - 1;
+constexpr uint32_t kEndBit = 1u << 31;
+constexpr int kSkipShift = 26;
+constexpr uint32_t kSkipEsc = 31;
+
+struct TaskArgs {
+  const int2* rec;          // [nnz] (col | skip << 26 | end << 31, weight bits)
+  const int32_t* task_row;  // [ntasks]
+  const int32_t* rowptr;    // [n_rows + 1] (fixup, skip escapes)
+  int n_rows, nnz, K, ntasks;
+  int B;                    // columns < B read X, >= B read X2 (row j - B)
+  const float* X;
+  int64_t ldx;              // floats
+  const float* X2;
+  int64_t ldx2;
+  int F;                    // columns (multiple of 4)
+  float* out;
+  int64_t ldo;
+  float* carry;             // [ntasks][2][F]: head partial, tail partial
+  // near path: X and X2 as one 32-bit buffer range from ubase
+  const char* ubase;
+  uint32_t span, offx, ldxb, offx2, ldx2b;
+  int dbg;                  // experiments: 1 = no row stores (results invalid)
+};
+
+__device__ __forceinline__ int upper_bound_i32(const int32_t* __restrict__ a, int n, int key) {
+  // first i in [0, n] with a[i] > key  (a non-decreasing, n + 1 entries read)
+  int lo = 0, hi = n + 1;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (a[mid] <= key) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+// ---- plan ----------------------------------------------------------------
+__global__ void task_records_kernel(const int32_t* __restrict__ col, const float* __restrict__ val,
+                                    int nnz, int2* __restrict__ rec) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= nnz) return;
+  rec[e] = make_int2(col[e] & (int)kColMask, val ? __float_as_int(val[e]) : __float_as_int(1.f));
+}
+
+__global__ void task_row_ends_kernel(const int32_t* __restrict__ rowptr, int n_rows,
+                                     int2* __restrict__ rec) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n_rows) return;
+  const int e1 = rowptr[r + 1];
+  if (e1 == rowptr[r]) return;             // empty row: no edge to mark
+  uint32_t skip = 0;
+  for (int k = r + 1; k < n_rows && skip < kSkipEsc && rowptr[k + 1] == rowptr[k]; ++k) ++skip;
+  int2 v = rec[e1 - 1];
+  v.x = (int)(((uint32_t)v.x & kColMask) | (skip << kSkipShift) | kEndBit);
+  rec[e1 - 1] = v;
+}
+
+__global__ void task_first_row_kernel(const int32_t* __restrict__ rowptr, int n_rows, int K,
+                                      int ntasks, int32_t* __restrict__ task_row) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= ntasks) return;
+  // the row whose edge range holds edge t*K: last r with rowptr[r] <= t*K
+  task_row[t] = upper_bound_i32(rowptr, n_rows, t * K) - 1;
+}
+
+// ---- main kernel ---------------------------------------------------------
+template <bool FAR>
+__device__ __forceinline__ void row_src(const TaskArgs& a, uint32_t j, uint32_t lane_off,
+                                        uint32_t* off, const char** p) {
+  if constexpr (FAR) {
+    const float* row = (int)j < a.B ? a.X + (int64_t)j * a.ldx : a.X2 + (int64_t)((int)j - a.B) * a.ldx2;
+    *p = reinterpret_cast<const char*>(row) + lane_off;
+  } else {
+    *off = ((int)j < a.B ? a.offx + j * a.ldxb : a.offx2 + (j - (uint32_t)a.B) * a.ldx2b) + lane_off;
+  }
+}
+
+// G lanes per task (64 / G tasks per wave), NC float4 pieces per lane (piece
+// i of lane k is float4 column G*i + k: a column tile of 4*G*NC floats), U
+// edges per block
+template <int G, int NC, int U, bool FAR>
+__global__ void __launch_bounds__(kTaskThreads)
+spmm_task_kernel(TaskArgs a) {
+  constexpr int TPW = 64 / G;
+  const int lane = threadIdx.x & 63;
+  const int g = lane / G, k = lane % G;
+  const int nwaves = (int)gridDim.x * (kTaskThreads / 64);
+  const int wv = xcd_remap(blockIdx.x, gridDim.x) * (kTaskThreads / 64) + (threadIdx.x >> 6);
+  const int t = wv * TPW + g;
+  // a call over the first n_rows rows of a larger CSR (the backward's
+  // transpose restricted to batch rows) covers edges [0, rowptr[n_rows])
+  const int nnz = min(a.nnz, a.rowptr[a.n_rows]);
+  if (wv >= nwaves || wv * TPW * a.K >= nnz) return;
+  const int e0 = t * a.K;
+  const bool valid = e0 < nnz;
+  const int e1 = valid ? min(nnz, e0 + a.K) : e0;
+  const int F4 = a.F >> 2;
+  const int c4base = (int)blockIdx.y * NC * G + k;   // this lane's first float4 column
+  bool pv[NC];
+#pragma unroll
+  for (int i = 0; i < NC; ++i) pv[i] = c4base + G * i < F4;
+  const uint32_t lane_off = (uint32_t)c4base * 16u;
+
+  int r = valid ? a.task_row[t] : 0;
+  bool head = valid && a.rowptr[r] < e0;    // first row began in an earlier task
+  bool open = false;                        // acc holds a partial row
+
+  const __amdgpu_buffer_rsrc_t rsx =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.ubase, 0, FAR ? 0 : (int)a.span, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.rec, 0, (int)(uint32_t)min((int64_t)a.nnz * 8, (int64_t)0x7FFFFFFF), 0x00020000);
+
+  float4 acc[NC];
+#pragma unroll
+  for (int i = 0; i < NC; ++i) acc[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+
+  // records of a U-edge block; past e1 the buffer range or the weight-0
+  // dummy keeps the loads in bounds and the sums unchanged
+  auto load_recs = [&](int e, int2 (&rv)[U]) {
+#pragma unroll
+    for (int u = 0; u < U; u += 2) {
+      const int eu = e + u;
+      const int4 q = __builtin_bit_cast(
+          int4, __builtin_amdgcn_raw_buffer_load_b128(rsr, (uint32_t)eu * 8u, 0, 0));
+      rv[u] = eu < e1 ? make_int2(q.x, q.y) : make_int2(0, 0);
+      rv[u + 1] = eu + 1 < e1 ? make_int2(q.z, q.w) : make_int2(0, 0);
+    }
+  };
+
+  int2 rcur[U];
+  load_recs(e0, rcur);
+  const int nblk = (a.K + U - 1) / U;
+  for (int bi = 0; bi < nblk; ++bi) {
+    const int e = e0 + bi * U;
+    int2 rnxt[U];
+    if (bi + 1 < nblk) load_recs(e + U, rnxt);
+    float4 v[U][NC];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t j = (uint32_t)rcur[u].x & kColMask;
+      uint32_t off = 0;
+      const char* p = nullptr;
+      row_src<FAR>(a, j, lane_off, &off, &p);
+#pragma unroll
+      for (int i = 0; i < NC; ++i) {
+        if constexpr (FAR) {
+          v[u][i] = pv[i] ? *reinterpret_cast<const float4*>(p + 16 * G * i)
+                          : make_float4(0.f, 0.f, 0.f, 0.f);
+        } else {   // pieces past F read the next row (or 0 past the range): never stored
+          v[u][i] = __builtin_bit_cast(
+              float4, __builtin_amdgcn_raw_buffer_load_b128(rsx, off + 16u * G * i, 0, 0));
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const float w = __int_as_float(rcur[u].y);
+      const uint32_t x = (uint32_t)rcur[u].x;
+      const bool real = e + u < e1;
+#pragma unroll
+      for (int i = 0; i < NC; ++i) {
+        acc[i].x = fmaf(w, v[u][i].x, acc[i].x);
+        acc[i].y = fmaf(w, v[u][i].y, acc[i].y);
+        acc[i].z = fmaf(w, v[u][i].z, acc[i].z);
+        acc[i].w = fmaf(w, v[u][i].w, acc[i].w);
+      }
+      open = open || real;
+      if (x & kEndBit) {                   // the row ends at this edge
+        float* dst = head ? a.carry + (int64_t)t * 2 * a.F : a.out + (int64_t)r * a.ldo;
+#pragma unroll
+        for (int i = 0; i < NC; ++i) {
+          if (pv[i] && !(a.dbg & 1))
+            *reinterpret_cast<float4*>(dst + 4 * (c4base + G * i)) = acc[i];
+          acc[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        const uint32_t skip = (x >> kSkipShift) & kSkipEsc;
+        r = skip == kSkipEsc ? upper_bound_i32(a.rowptr, a.n_rows, e + u + 1) - 1
+                             : r + 1 + (int)skip;
+        head = false;
+        open = false;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) rcur[u] = rnxt[u];
+  }
+  if (open) {                              // the last row continues in the next task
+    float* dst = a.carry + ((int64_t)t * 2 + 1) * a.F;
+#pragma unroll
+    for (int i = 0; i < NC; ++i)
+      if (pv[i]) *reinterpret_cast<float4*>(dst + 4 * (c4base + G * i)) = acc[i];
+  }
+}
+
+// One 64-lane group per index x: (1) task x — if its first row began in an
+// earlier task and ends in this one, out[row] = tails of the earlier tasks +
+// this task's head, in task order; (2) row x — zeros if it is empty.
+__global__ void __launch_bounds__(256)
+spmm_task_fixup_kernel(TaskArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int x = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int F4 = a.F >> 2;
+  const int nnz = min(a.nnz, a.rowptr[a.n_rows]);
+  if (x < a.ntasks && x * a.K < nnz) {
+    const int e0 = x * a.K;
+    const int r = a.task_row[x];
+    const int rs = a.rowptr[r], re = a.rowptr[r + 1];
+    if (rs < e0 && re <= min(nnz, e0 + a.K)) {
+      const int ts = rs / a.K;
+      const float4* c4 = reinterpret_cast<const float4*>(a.carry);
+      for (int c = lane; c < F4; c += 64) {
+        float4 s = c4[((int64_t)ts * 2 + 1) * F4 + c];
+        for (int u = ts + 1; u < x; ++u) {
+          const float4 q = c4[((int64_t)u * 2 + 1) * F4 + c];
+          s.x = __fadd_rn(s.x, q.x);
+          s.y = __fadd_rn(s.y, q.y);
+          s.z = __fadd_rn(s.z, q.z);
+          s.w = __fadd_rn(s.w, q.w);
+        }
+        const float4 h = c4[(int64_t)x * 2 * F4 + c];
+        s.x = __fadd_rn(s.x, h.x);
+        s.y = __fadd_rn(s.y, h.y);
+        s.z = __fadd_rn(s.z, h.z);
+        s.w = __fadd_rn(s.w, h.w);
+        reinterpret_cast<float4*>(a.out + (int64_t)r * a.ldo)[c] = s;
+      }
+    }
+  }
+  if (x < a.n_rows && a.rowptr[x + 1] == a.rowptr[x]) {
+    float4* o = reinterpret_cast<float4*>(a.out + (int64_t)x * a.ldo);
+    for (int c = lane; c < F4; c += 64) o[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
+template <int G, int NC, int U, bool FAR>
+static void launch_task(const TaskArgs& a, int tiles, hipStream_t s) {
+  const int waves = (a.ntasks + 64 / G - 1) / (64 / G);
+  const int blocks = (waves + 3) / 4;
+  hipLaunchKernelGGL((spmm_task_kernel<G, NC, U, FAR>), dim3(blocks, tiles), dim3(kTaskThreads), 0,
+                     s, a);
+}
+
+static int task_env(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v ? atoi(v) : dflt;
+}
+
+}  // namespace vqgnn
+
+using namespace vqgnn;
+
+extern "C" int32_t vqgnn_spmm_task_size(int64_t nnz, int32_t K) {
+  if (K <= 0) K = 64;
+  return (int32_t)((nnz + K - 1) / K);
+}
+
+extern "C" int vqgnn_spmm_task_plan(const int32_t* rowptr, const int32_t* col, const float* val,
+                                    int32_t n_rows, int64_t nnz, int32_t K, int32_t* task_row,
+                                    int64_t* records, vqgnn_stream_t stream) {
+  clear_error();
+  VQGNN_REQUIRE(rowptr && n_rows >= 0 && nnz >= 0 && nnz < (int64_t)1 << 31,
+                "spmm_task_plan: bad arguments");
+  VQGNN_REQUIRE(K >= 8 && K % 4 == 0 && K <= 4096, "spmm_task_plan: K=%d must be a multiple of 4 in [8, 4096]", K);
+  VQGNN_REQUIRE(nnz == 0 || (col && task_row && records), "spmm_task_plan: null pointer");
+  if (nnz == 0) return VQGNN_OK;
+  hipStream_t s = as_stream(stream);
+  int2* rec = reinterpret_cast<int2*>(records);
+  const int ntasks = vqgnn_spmm_task_size(nnz, K);
+  hipLaunchKernelGGL(task_records_kernel, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s, col,
+                     val, (int)nnz, rec);
+  if (n_rows > 0)
+    hipLaunchKernelGGL(task_row_ends_kernel, dim3((n_rows + 255) / 256), dim3(256), 0, s, rowptr,
+                       n_rows, rec);
+  hipLaunchKernelGGL(task_first_row_kernel, dim3((ntasks + 255) / 256), dim3(256), 0, s, rowptr,
+                     n_rows, K, ntasks, task_row);
+  return check_launch("spmm_task_plan");
+}
+
+extern "C" size_t vqgnn_spmm_task_workspace(int64_t nnz, int32_t K, int32_t F) {
+  return align_up((size_t)vqgnn_spmm_task_size(nnz, K) * 2 * F * sizeof(float), 256) + 256;
+}
+
+extern "C" int vqgnn_spmm_task(const int32_t* rowptr, int32_t n_rows, int32_t n_cols, int64_t nnz,
+                               int32_t B, const float* X, int64_t ldx, const float* X2,
+                               int64_t ldx2, int32_t F, float* out, int64_t ldo,
+                               const int32_t* task_row, const int64_t* records, int32_t K,
+                               void* workspace, vqgnn_stream_t stream) {
+  clear_error();
+  VQGNN_REQUIRE(rowptr && out && (nnz == 0 || (X && task_row && records && workspace)),
+                "spmm_task: null pointer");
+  VQGNN_REQUIRE(F > 0 && F % 4 == 0, "spmm_task: F=%d must be a positive multiple of 4", F);
+  VQGNN_REQUIRE(ldx % 4 == 0 && ldo % 4 == 0 && (!X2 || ldx2 % 4 == 0) &&
+                    ((uintptr_t)X & 15) == 0 && ((uintptr_t)out & 15) == 0 &&
+                    ((uintptr_t)X2 & 15) == 0,
+                "spmm_task: rows must be 16-byte aligned");
+  VQGNN_REQUIRE(ldx >= F && ldo >= F && (!X2 || ldx2 >= F), "spmm_task: leading dimension < F");
+  VQGNN_REQUIRE(n_cols <= (int32_t)kColMask, "spmm_task: %d columns exceed 2^26", n_cols);
+  VQGNN_REQUIRE(B >= 0 && (X2 || B == 0), "spmm_task: B=%d without X2", B);
+  VQGNN_REQUIRE(K >= 8 && K % 4 == 0, "spmm_task: K=%d", K);
+  hipStream_t s = as_stream(stream);
+  TaskArgs a{};
+  a.rec = reinterpret_cast<const int2*>(records);
+  a.task_row = task_row;
+  a.rowptr = rowptr;
+  a.n_rows = n_rows;
+  a.nnz = (int)nnz;
+  a.K = K;
+  a.ntasks = vqgnn_spmm_task_size(nnz, K);
+  a.B = X2 ? B : n_cols;
+  a.X = X;
+  a.ldx = ldx;
+  a.X2 = X2 ? X2 : X;
+  a.ldx2 = X2 ? ldx2 : ldx;
+  a.F = F;
+  a.out = out;
+  a.ldo = ldo;
+  a.carry = reinterpret_cast<float*>(workspace);
+  // near path: both sources inside one 32-bit byte range
+  const int nx = a.B, nx2 = X2 ? n_cols - B : 0;
+  const uintptr_t x0 = (uintptr_t)X, x1 = x0 + (uintptr_t)((int64_t)(nx > 0 ? nx - 1 : 0) * ldx + F) * 4;
+  uintptr_t lo = x0, hi = x1;
+  uintptr_t y0 = 0, y1 = 0;
+  if (nx2 > 0) {
+    y0 = (uintptr_t)X2;
+    y1 = y0 + (uintptr_t)((int64_t)(nx2 - 1) * ldx2 + F) * 4;
+    lo = lo < y0 ? lo : y0;
+    hi = hi > y1 ? hi : y1;
+  }
+  const bool near = hi - lo < 0x7FFFFFF0ull && (int64_t)ldx * 4 < 0x7FFFFFFF &&
+                    (int64_t)a.ldx2 * 4 < 0x7FFFFFFF && !task_env("VQGNN_SPMM_FAR", 0);
+  if (near) {
+    a.ubase = reinterpret_cast<const char*>(lo);
+    a.span = (uint32_t)(hi - lo);
+    a.offx = (uint32_t)(x0 - lo);
+    a.ldxb = (uint32_t)(ldx * 4);
+    a.offx2 = nx2 > 0 ? (uint32_t)(y0 - lo) : 0;
+    a.ldx2b = (uint32_t)(a.ldx2 * 4);
+  }
+  if (nnz > 0) {
+    const int F4 = F / 4;
+    // lanes per task: VQGNN_TASK_G (8, 16 or 32; default 32); pieces per lane
+    // so that one column tile covers min(F, 128) floats
+    int G = task_env("VQGNN_TASK_G", 32);
+    G = G >= 32 ? 32 : (G >= 16 ? 16 : 8);
+    int nc = 1;
+    while (nc * G < F4 && nc * G * 4 < 128) nc *= 2;      // 4*G*nc floats <= 128
+    const int tiles = (F4 + nc * G - 1) / (nc * G);
+    const int Ue = task_env("VQGNN_TASK_U", 8);
+    const int U = Ue >= 16 ? 16 : (Ue >= 8 ? 8 : (Ue >= 4 ? 4 : 2));
+    a.dbg = task_env("VQGNN_TASK_DBG", 0);
+#define VQGNN_TASK_LAUNCH(G_, NC_)                                  \
+  if (near) {                                                       \
+    if (U == 16) launch_task<G_, NC_, 16, false>(a, tiles, s);      \
+    else if (U == 8) launch_task<G_, NC_, 8, false>(a, tiles, s);   \
+    else if (U == 4) launch_task<G_, NC_, 4, false>(a, tiles, s);   \
+    else launch_task<G_, NC_, 2, false>(a, tiles, s);               \
+  } else {                                                          \
+    if (U == 16) launch_task<G_, NC_, 16, true>(a, tiles, s);       \
+    else if (U == 8) launch_task<G_, NC_, 8, true>(a, tiles, s);    \
+    else if (U == 4) launch_task<G_, NC_, 4, true>(a, tiles, s);    \
+    else launch_task<G_, NC_, 2, true>(a, tiles, s);                \
+  }
+    if (G == 8) {
+      if (nc == 1) { VQGNN_TASK_LAUNCH(8, 1) }
+      else if (nc == 2) { VQGNN_TASK_LAUNCH(8, 2) }
+      else { VQGNN_TASK_LAUNCH(8, 4) }
+    } else if (G == 16) {
+      if (nc == 1) { VQGNN_TASK_LAUNCH(16, 1) }
+      else { VQGNN_TASK_LAUNCH(16, 2) }
+    } else {
+      VQGNN_TASK_LAUNCH(32, 1)
+    }
+#undef VQGNN_TASK_LAUNCH
+  }
+  const int nfix = a.ntasks > n_rows ? a.ntasks : n_rows;
+  if (nfix > 0)
+    hipLaunchKernelGGL(spmm_task_fixup_kernel, dim3((nfix + 3) / 4), dim3(256), 0, s, a);
+  return check_launch("spmm_task");
+}

@@ -270,6 +270,32 @@ def spmm_pair_plan(rowptr, n_rows, nnz, F, B, chunk=None):
     return PairPlan(buf, int(F), int(B), int(n_rows), chunk)
 
 
+class TaskPlan:
+    """Task plan of a CSR for vqgnn_spmm_task (include/vqgnn.h §6e): per-edge
+    records (column, row-end flag, weight) and each task's first row; built
+    once per batch adjacency, valid for any F and any leading row count."""
+
+    def __init__(self, task_row, records, K, nnz, n_rows, val):
+        self.task_row, self.records, self.K = task_row, records, K
+        self.nnz, self.n_rows = nnz, n_rows
+        self.val_ptr = val.data_ptr() if val is not None else 0
+
+
+TASK_K = 64
+
+
+def spmm_task_plan(rowptr, col, val, n_rows, nnz, K=None):
+    L = lib()
+    K = int(K or TASK_K)
+    dev = rowptr.device
+    nt = L.vqgnn_spmm_task_size(int(nnz), K)
+    task_row = torch.empty(max(nt, 1), dtype=torch.int32, device=dev)
+    records = torch.empty(max(int(nnz), 1), dtype=torch.int64, device=dev)
+    check(L.vqgnn_spmm_task_plan(ptr(rowptr), ptr(col), ptr(val), int(n_rows), int(nnz), K,
+                                 ptr(task_row), ptr(records), stream_ptr()), "spmm_task_plan")
+    return TaskPlan(task_row, records, K, int(nnz), int(n_rows), val)
+
+
 def spmm(rowptr, col, val, n_rows, nnz, X, F, X2=None, B=None, out=None, plan=None):
     """out[i] = sum_e val[e] * xin[col[e]]; xin = X rows (< B), X2 rows (>= B).
     Every column index must be < the rows of xin (X rows, or B + X2 rows)."""
@@ -278,11 +304,23 @@ def spmm(rowptr, col, val, n_rows, nnz, X, F, X2=None, B=None, out=None, plan=No
     if out is None:
         out = torch.empty(n_rows, F, dtype=torch.float32, device=dev)
     L = lib()
-    ws = workspace(L.vqgnn_spmm_workspace(n_rows, nnz, F), dev)
     Bv = int(B) if X2 is not None else 0
     n_cols = Bv + X2.shape[0] if X2 is not None else X.shape[0]
     if X2 is not None and X.shape[0] < Bv:
         raise ValueError(f"spmm: X has {X.shape[0]} rows < B={Bv}")
+    if isinstance(plan, TaskPlan):
+        if (val.data_ptr() if val is not None else 0) != plan.val_ptr:
+            raise ValueError("spmm: the task plan's records hold other values than val")
+        if plan.nnz != int(nnz) or int(n_rows) > plan.n_rows:
+            raise ValueError(f"spmm: task plan for nnz={plan.nnz}, rows={plan.n_rows}; called "
+                             f"with nnz={nnz}, n_rows={n_rows}")
+        ws = workspace(L.vqgnn_spmm_task_workspace(int(nnz), plan.K, F), dev)
+        check(L.vqgnn_spmm_task(ptr(rowptr), int(n_rows), int(n_cols), int(nnz), Bv, ptr(X),
+                                _ld(X), ptr(X2), _ld(X2) if X2 is not None else 0, F, ptr(out),
+                                _ld(out), ptr(plan.task_row), ptr(plan.records), plan.K,
+                                ptr(ws), stream_ptr()), "spmm_task")
+        return out
+    ws = workspace(L.vqgnn_spmm_workspace(n_rows, nnz, F), dev)
     if isinstance(plan, PairPlan):
         if plan.F != F or plan.n_rows != int(n_rows):
             raise ValueError(f"spmm: pair plan built for F={plan.F}, n_rows={plan.n_rows}; "

@@ -118,9 +118,12 @@ class CSR:
             self._t = t
         return self._t
 
-    def plan(self, F, B=None, n_rows=None):
+    def plan(self, F, B=None, n_rows=None, kind=None):
         """SpMM plan for feature width F, cached like torch_sparse's storage
-        caches: the chunk plan (include/vqgnn.h §6b), or with
+        caches: by default the task plan (include/vqgnn.h §6e, any F);
+        the task records hold this CSR's values, so products with other
+        values (GAT coefficients) ask for ``kind="chunk"``;
+        ``VQGNN_SPMM=chunk`` selects the chunk plan (§6b), or with
         ``VQGNN_SPMM_PAIR=1`` the segment-pair plan (§6d) where it applies
         (F = 128; bit-identical output, measured within +-8% of the chunk
         kernel across boxes, so not the default).  The pair plan covers rows
@@ -128,6 +131,14 @@ class CSR:
         from out-of-batch rows."""
         import os
         from . import kernels
+        mode = kind or os.environ.get("VQGNN_SPMM", "task")
+        if mode == "task" and os.environ.get("VQGNN_SPMM_PAIR", "0") != "1":
+            p = self._plans.get("task")
+            if p is None:
+                p = kernels.spmm_task_plan(self.rowptr, self.col, self.value, self._sizes[0],
+                                           self._host_nnz)
+                self._plans["task"] = p
+            return p
         chunk = self._plans.get(F)
         if chunk is None:
             chunk = kernels.spmm_plan(self.rowptr, self._sizes[0], self._host_nnz, F)
