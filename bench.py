@@ -121,8 +121,9 @@ def main():
         gat = OurGATConv(F + 1, F + 1, bias=False, add_self_loops=False).to(dev)
     # per-batch adjacency preparation (like the reference's SparseTensor build
     # in the data loader): the SpMM chunk plan, computed once per batch
-    spmm_plan = adj.plan(F, B=B)
     fused = gat is None and args.spmm_source == "codes" and kernels.spmm_codes_supported(F, nb, M, D)
+    spmm_plan = adj.plan(F, B=B, kind="chunk" if fused else None)
+    task = isinstance(spmm_plan, kernels.TaskPlan)
     if args.spmm_source == "codes" and not fused:
         raise SystemExit(f"--spmm-source codes: F={F} M={M} does not fit the LDS codebook path")
     # codebook state = one feature_update warm pass
@@ -252,7 +253,7 @@ def main():
 
     # Algorithmic work per launch:
     #  vq_assign_kernel: 2*B*M*W flops per branch (the distance contraction);
-    #  SpMM (spmm_wave_kernel + spmm_fixup_kernel): rowptr + (col, val) + every
+    #  SpMM (spmm_task_kernel + spmm_task_fixup_kernel): rowptr + (col, val) + every
     #  input row once (x and x_first_order) + the output rows.
     #  fused (spmm_codes_kernel): X rows once, the B' code records and the
     #  codebooks' feature halves instead of x_first_order.
@@ -272,11 +273,14 @@ def main():
             pmc = {}
     agg_name = ("gat aggregation (alpha+coef+spmm+normalize)" if gat is not None
                 else "spmm_codes_kernel+spmm_fixup_kernel" if fused
+                else "spmm_task_kernel+spmm_task_fixup_kernel" if task
                 else "spmm_wave_kernel+spmm_fixup_kernel")
+    agg_pmc = ("spmm_codes_kernel" if fused else "spmm_task_kernel" if task
+               else "spmm_wave_kernel")
     rl_spmm = dict(kernel=agg_name, bound="hbm",
                    achieved=spmm_bytes / (spmm_ms * 1e-3) / 1e9, peak=8000.0, unit="GB/s",
                    bytes_per_launch=spmm_bytes, ms_per_launch=spmm_ms,
-                   traffic=pmc.get("spmm_codes_kernel" if fused else "spmm_wave_kernel"))
+                   traffic=pmc.get(agg_pmc))
     rl_spmm["frac"] = rl_spmm["achieved"] / rl_spmm["peak"]
     # the filtered assign (vq_kernels.hip: D = 4, W in {4, 8}, codebook planes +
     # fused accumulators within 160 KiB of LDS) is one timed span: the bf16

@@ -289,21 +289,27 @@ int vqgnn_spmm_pair(const int32_t* rowptr, const int32_t* col, const float* val,
  *     order: deterministic, within 1e-5 relative of the fp64 sum (north_star
  *     tolerance; not spmm_sum's separate multiply/add bit pattern).
  *     Plan (once per batch adjacency, any F): vqgnn_spmm_task_plan fills
- *     task_row [vqgnn_spmm_task_size(nnz, K)] int32 and records [nnz] int64
- *     (source column, row-end flag, weight) from the CSR; K = 64 (multiple of
- *     4 in [8, 4096]).  A call may cover the first n_rows rows of the planned
- *     CSR (edges [0, rowptr[n_rows])), e.g. the backward's batch rows.
- *     n_cols < 2^26.  Workspace: vqgnn_spmm_task_workspace(nnz, K, F) bytes.
+ *     plan [vqgnn_spmm_task_size(nnz, K, n_rows)] int32 (each task's first
+ *     edge and row — a row of at most K/2 edges is never cut, so tasks hold
+ *     K/2..3K/2 edges — then the fix-up jobs: cut rows and empty rows),
+ *     records [nnz] int64 (source column, row-end flag, weight) and
+ *     counts[2] (device int32: cut rows, empty rows), which the caller reads
+ *     once per plan and passes to every vqgnn_spmm_task call as n_jobs /
+ *     n_empty.  K = 64 (multiple of 4 in [8, 4096]).  A call may cover the
+ *     first n_rows rows of the planned CSR (edges [0, rowptr[n_rows])), e.g.
+ *     the backward's batch rows.  n_cols < 2^26.  Workspace:
+ *     vqgnn_spmm_task_workspace(nnz, K, F) bytes.
  *     Replaces convs.py:95 -> torch_sparse spmm_sum like 6.                  */
-int32_t vqgnn_spmm_task_size(int64_t nnz, int32_t K);
+int64_t vqgnn_spmm_task_size(int64_t nnz, int32_t K, int32_t n_rows);
 int vqgnn_spmm_task_plan(const int32_t* rowptr, const int32_t* col, const float* val,
-                         int32_t n_rows, int64_t nnz, int32_t K, int32_t* task_row,
-                         int64_t* records, vqgnn_stream_t stream);
+                         int32_t n_rows, int64_t nnz, int32_t K, int32_t* plan,
+                         int64_t* records, int32_t* counts, vqgnn_stream_t stream);
 size_t vqgnn_spmm_task_workspace(int64_t nnz, int32_t K, int32_t F);
 int vqgnn_spmm_task(const int32_t* rowptr, int32_t n_rows, int32_t n_cols, int64_t nnz,
                     int32_t B, const float* X, int64_t ldx, const float* X2, int64_t ldx2,
-                    int32_t F, float* out, int64_t ldo, const int32_t* task_row,
-                    const int64_t* records, int32_t K, void* workspace, vqgnn_stream_t stream);
+                    int32_t F, float* out, int64_t ldo, const int32_t* plan,
+                    const int64_t* records, int32_t K, int32_t n_jobs, int32_t n_empty,
+                    void* workspace, vqgnn_stream_t stream);
 
 /* 7. CSR transpose (structure + values) for the backward product
  *    dX = A^T dOut (torch_sparse matmul autograd, convs.py:95).  Output CSR of

@@ -51,10 +51,14 @@ def run(name, F=None):
     chunk = adj.plan(F, B=b.B, kind="chunk")
     plans = {K: kernels.spmm_task_plan(adj.rowptr, adj.col, adj.value, b.n, b.nnz, K)
              for K in (32, 64, 128)}
+    os.environ["VQGNN_TASK_SNAP"] = "0"     # fixed K-edge tasks (rows cut anywhere)
+    plans.update({-K: kernels.spmm_task_plan(adj.rowptr, adj.col, adj.value, b.n, b.nnz, K)
+                  for K in (64, 128)})
+    del os.environ["VQGNN_TASK_SNAP"]
     variants = [("chunk kernel", None, None, None)] + [
-        (f"task K={K} G={G} U={U}", K, G, U)
-        for (K, G, U) in ((64, 32, 8), (64, 32, 16), (32, 32, 8), (32, 32, 16),
-                          (128, 32, 16), (64, 16, 8), (64, 8, 8))]
+        (f"task K={K} G={G} U={U}" + (" fixed" if K < 0 else ""), K, G, U)
+        for (K, G, U) in ((64, 32, 8), (-64, 32, 8), (64, 32, 4), (-64, 32, 4), (128, 32, 8),
+                          (-128, 32, 8), (32, 32, 8), (64, 16, 8))]
     res = {v[0]: [] for v in variants}
     for rep in range(3):              # interleaved repeats: box drift hits every variant alike
         for tag, K, G, U in variants:

@@ -222,7 +222,7 @@ def test_spmm_codes_vs_two_source(F, D, M):
     xd = torch.from_numpy(X).to(DEV)
     xt, lcodes = kernels.gather_codewords(subset, b.B, codes_d, emb_d, D, want_codes=True)
     two = kernels.spmm(adj.rowptr, adj.col, adj.value, b.n, b.nnz, xd, F, X2=xt, B=b.B)
-    plan = adj.plan(F)
+    plan = adj.plan(F, kind="chunk")
     fused = kernels.spmm_codes(adj.rowptr, adj.col, adj.value, b.n, b.nnz, xd, F, lcodes, emb_d,
                                D, b.B, plan=plan)
     assert torch.equal(fused, two)

@@ -30,6 +30,8 @@
 
 #include "common.h"
 
+#include <utility>
+
 namespace vqgnn {
 
 constexpr int kTaskThreads = 256;             // 4 waves
@@ -40,7 +42,11 @@ constexpr uint32_t kSkipEsc = 31;
 
 struct TaskArgs {
   const int2* rec;          // [nnz] (col | skip << 26 | end << 31, weight bits)
-  const int32_t* task_row;  // [ntasks]
+  const int32_t* task_start;  // [ntasks + 1] first edge of each task (row-aligned unless split)
+  const int32_t* task_row;    // [ntasks] row containing the task's first edge
+  const int32_t* jobs;        // fixup: [ntasks][3] slots, n_jobs used (row, first task,
+                              // last task), then [n_rows] slots, n_empty used (empty rows)
+  int n_jobs, n_empty;
   const int32_t* rowptr;    // [n_rows + 1] (fixup, skip escapes)
   int n_rows, nnz, K, ntasks;
   int B;                    // columns < B read X, >= B read X2 (row j - B)
@@ -89,12 +95,47 @@ __global__ void task_row_ends_kernel(const int32_t* __restrict__ rowptr, int n_r
   rec[e1 - 1] = v;
 }
 
-__global__ void task_first_row_kernel(const int32_t* __restrict__ rowptr, int n_rows, int K,
-                                      int ntasks, int32_t* __restrict__ task_row) {
+// Task t nominally starts at edge t*K.  A row of at most K/2 edges that holds
+// the nominal start is not split: the task starts at the next row instead
+// (the previous task takes the whole row), so tasks hold K/2..3K/2 edges and
+// only rows longer than K/2 are cut (their partials summed by the fixup).
+__global__ void task_first_row_kernel(const int32_t* __restrict__ rowptr, int n_rows, int nnz,
+                                      int K, int snap, int ntasks, int32_t* __restrict__ task_start,
+                                      int32_t* __restrict__ task_row) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= ntasks) return;
-  // the row whose edge range holds edge t*K: last r with rowptr[r] <= t*K
-  task_row[t] = upper_bound_i32(rowptr, n_rows, t * K) - 1;
+  if (t > ntasks) return;
+  int st = t == ntasks ? nnz : t * K;
+  if (t > 0 && t < ntasks) {
+    const int r = upper_bound_i32(rowptr, n_rows, st) - 1;   // row containing edge st
+    const int rs = rowptr[r], re = rowptr[r + 1];
+    if (rs < st && re - rs <= snap) st = re;
+  }
+  task_start[t] = st;
+  if (t < ntasks) task_row[t] = st < nnz ? upper_bound_i32(rowptr, n_rows, st) - 1 : n_rows - 1;
+}
+
+// Fix-up jobs: a row cut by task boundaries (its first edge in task ts, its
+// last in task t > ts) -> (row, ts, t); an empty row -> its index.  Appended
+// with atomics (the order does not matter: every job writes its own row).
+__global__ void task_jobs_kernel(const int32_t* __restrict__ rowptr, int n_rows, int ntasks,
+                                 const int32_t* __restrict__ task_start,
+                                 const int32_t* __restrict__ task_row, int32_t* __restrict__ jobs,
+                                 int32_t* __restrict__ empties, int32_t* __restrict__ counts) {
+  const int x = blockIdx.x * blockDim.x + threadIdx.x;
+  const int nnz = task_start[ntasks];
+  if (x < ntasks && task_start[x] < nnz) {
+    const int e0 = task_start[x];
+    const int r = task_row[x];
+    const int rs = rowptr[r], re = rowptr[r + 1];
+    if (rs < e0 && re <= task_start[x + 1]) {
+      const int ts = upper_bound_i32(task_start, ntasks, rs) - 1;
+      const int j = atomicAdd(counts, 1);
+      jobs[3 * j] = r;
+      jobs[3 * j + 1] = ts;
+      jobs[3 * j + 2] = x;
+    }
+  }
+  if (x < n_rows && rowptr[x + 1] == rowptr[x]) empties[atomicAdd(counts + 1, 1)] = x;
 }
 
 // ---- main kernel ---------------------------------------------------------
@@ -107,6 +148,14 @@ __device__ __forceinline__ void row_src(const TaskArgs& a, uint32_t j, uint32_t 
   } else {
     *off = ((int)j < a.B ? a.offx + j * a.ldxb : a.offx2 + (j - (uint32_t)a.B) * a.ldx2b) + lane_off;
   }
+}
+
+// out[u] = x of lane u of this lane's group (ds_swizzle bit mode inside each
+// 32-lane half: lane id -> (id & AND) | u); the pattern must be an immediate
+template <int AND, int... Us>
+__device__ __forceinline__ void group_bcast(int x, int (&out)[sizeof...(Us)],
+                                            std::integer_sequence<int, Us...>) {
+  ((out[Us] = __builtin_amdgcn_ds_swizzle(x, AND | (Us << 5))), ...);
 }
 
 // G lanes per task (64 / G tasks per wave), NC float4 pieces per lane (piece
@@ -124,10 +173,12 @@ spmm_task_kernel(TaskArgs a) {
   // a call over the first n_rows rows of a larger CSR (the backward's
   // transpose restricted to batch rows) covers edges [0, rowptr[n_rows])
   const int nnz = min(a.nnz, a.rowptr[a.n_rows]);
-  if (wv >= nwaves || wv * TPW * a.K >= nnz) return;
-  const int e0 = t * a.K;
+  if (wv >= nwaves || wv * TPW >= a.ntasks || a.task_start[wv * TPW] >= nnz) return;
+  const bool tv = t < a.ntasks;
+  const int e0 = tv ? min(a.task_start[t], nnz) : nnz;
   const bool valid = e0 < nnz;
-  const int e1 = valid ? min(nnz, e0 + a.K) : e0;
+  const int e1 = valid ? min(nnz, a.task_start[t + 1]) : e0;
+
   const int F4 = a.F >> 2;
   const int c4base = (int)blockIdx.y * NC * G + k;   // this lane's first float4 column
   bool pv[NC];
@@ -148,30 +199,38 @@ spmm_task_kernel(TaskArgs a) {
 #pragma unroll
   for (int i = 0; i < NC; ++i) acc[i] = make_float4(0.f, 0.f, 0.f, 0.f);
 
-  // records of a U-edge block; past e1 the buffer range or the weight-0
-  // dummy keeps the loads in bounds and the sums unchanged
-  auto load_recs = [&](int e, int2 (&rv)[U]) {
-#pragma unroll
-    for (int u = 0; u < U; u += 2) {
-      const int eu = e + u;
-      const int4 q = __builtin_bit_cast(
-          int4, __builtin_amdgcn_raw_buffer_load_b128(rsr, (uint32_t)eu * 8u, 0, 0));
-      rv[u] = eu < e1 ? make_int2(q.x, q.y) : make_int2(0, 0);
-      rv[u + 1] = eu + 1 < e1 ? make_int2(q.z, q.w) : make_int2(0, 0);
-    }
+  // Records: lane k < U of a group holds the record of edge e + k of the
+  // current block (one coalesced 8-byte load per lane); step u reads edge
+  // e + u's record from lane u of its group by a ds_swizzle broadcast.
+  // Records outside [e0, e1) read as weight 0 without a row end.
+  static_assert(U <= G, "records of a block live in the group's first U lanes");
+  constexpr int kAnd = 0x1F & ~(G - 1);               // keep the group bits (32-lane swizzle)
+  auto load_rec = [&](int e) -> int2 {
+    const int eu = e + k;
+    const int2 q = __builtin_bit_cast(
+        int2, __builtin_amdgcn_raw_buffer_load_b64(rsr, (uint32_t)eu * 8u, 0, 0));
+    return (k < U && eu >= e0 && eu < e1) ? q : make_int2(0, 0);
   };
 
-  int2 rcur[U];
-  load_recs(e0, rcur);
-  const int nblk = (a.K + U - 1) / U;
+  // the wave runs as many U-edge blocks as its longest task needs
+  int len = e1 - e0;
+#pragma unroll
+  for (int o = G; o < 64; o <<= 1) len = max(len, __shfl_xor(len, o));
+
+  int2 rcur = load_rec(e0);
+  // wave-uniform (every lane holds the max): an SGPR loop, not an exec-masked one
+  const int nblk = __builtin_amdgcn_readfirstlane((len + U - 1) / U);
   for (int bi = 0; bi < nblk; ++bi) {
     const int e = e0 + bi * U;
-    int2 rnxt[U];
-    if (bi + 1 < nblk) load_recs(e + U, rnxt);
+    int2 rnxt = make_int2(0, 0);
+    if (bi + 1 < nblk) rnxt = load_rec(e + U);
+    int cx[U], cw[U];
+    group_bcast<kAnd>(rcur.x, cx, std::make_integer_sequence<int, U>{});
+    group_bcast<kAnd>(rcur.y, cw, std::make_integer_sequence<int, U>{});
     float4 v[U][NC];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const uint32_t j = (uint32_t)rcur[u].x & kColMask;
+      const uint32_t j = (uint32_t)cx[u] & kColMask;
       uint32_t off = 0;
       const char* p = nullptr;
       row_src<FAR>(a, j, lane_off, &off, &p);
@@ -188,9 +247,9 @@ spmm_task_kernel(TaskArgs a) {
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const float w = __int_as_float(rcur[u].y);
-      const uint32_t x = (uint32_t)rcur[u].x;
-      const bool real = e + u < e1;
+      const float w = __int_as_float(cw[u]);
+      const uint32_t x = (uint32_t)cx[u];
+      const bool real = e + u >= e0 && e + u < e1;
 #pragma unroll
       for (int i = 0; i < NC; ++i) {
         acc[i].x = fmaf(w, v[u][i].x, acc[i].x);
@@ -214,8 +273,7 @@ spmm_task_kernel(TaskArgs a) {
         open = false;
       }
     }
-#pragma unroll
-    for (int u = 0; u < U; ++u) rcur[u] = rnxt[u];
+    rcur = rnxt;
   }
   if (open) {                              // the last row continues in the next task
     float* dst = a.carry + ((int64_t)t * 2 + 1) * a.F;
@@ -225,42 +283,41 @@ spmm_task_kernel(TaskArgs a) {
   }
 }
 
-// One 64-lane group per index x: (1) task x — if its first row began in an
-// earlier task and ends in this one, out[row] = tails of the earlier tasks +
-// this task's head, in task order; (2) row x — zeros if it is empty.
+// One wave per fix-up job.  A cut row: out[row] = tail[ts] + ... + tail[t-1]
+// + head[t], in task order (loads 8 tasks ahead of the in-order adds).  An
+// empty row: zeros.  Rows at or past n_rows (a call over leading rows) are
+// skipped.
 __global__ void __launch_bounds__(256)
 spmm_task_fixup_kernel(TaskArgs a) {
   const int lane = threadIdx.x & 63;
-  const int x = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int w = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int F4 = a.F >> 2;
-  const int nnz = min(a.nnz, a.rowptr[a.n_rows]);
-  if (x < a.ntasks && x * a.K < nnz) {
-    const int e0 = x * a.K;
-    const int r = a.task_row[x];
-    const int rs = a.rowptr[r], re = a.rowptr[r + 1];
-    if (rs < e0 && re <= min(nnz, e0 + a.K)) {
-      const int ts = rs / a.K;
-      const float4* c4 = reinterpret_cast<const float4*>(a.carry);
-      for (int c = lane; c < F4; c += 64) {
-        float4 s = c4[((int64_t)ts * 2 + 1) * F4 + c];
-        for (int u = ts + 1; u < x; ++u) {
-          const float4 q = c4[((int64_t)u * 2 + 1) * F4 + c];
-          s.x = __fadd_rn(s.x, q.x);
-          s.y = __fadd_rn(s.y, q.y);
-          s.z = __fadd_rn(s.z, q.z);
-          s.w = __fadd_rn(s.w, q.w);
-        }
-        const float4 h = c4[(int64_t)x * 2 * F4 + c];
-        s.x = __fadd_rn(s.x, h.x);
-        s.y = __fadd_rn(s.y, h.y);
-        s.z = __fadd_rn(s.z, h.z);
-        s.w = __fadd_rn(s.w, h.w);
-        reinterpret_cast<float4*>(a.out + (int64_t)r * a.ldo)[c] = s;
+  if (w < a.n_jobs) {
+    const int r = a.jobs[3 * w], ts = a.jobs[3 * w + 1], t = a.jobs[3 * w + 2];
+    if (r < 0 || r >= a.n_rows) return;
+    const float4* c4 = reinterpret_cast<const float4*>(a.carry);
+    auto add4 = [](float4 x, float4 y) {
+      return make_float4(__fadd_rn(x.x, y.x), __fadd_rn(x.y, y.y), __fadd_rn(x.z, y.z),
+                         __fadd_rn(x.w, y.w));
+    };
+    for (int c = lane; c < F4; c += 64) {
+      float4 sum = c4[((int64_t)ts * 2 + 1) * F4 + c];
+      int u = ts + 1;
+      for (; u + 8 <= t; u += 8) {
+        float4 q[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) q[i] = c4[((int64_t)(u + i) * 2 + 1) * F4 + c];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) sum = add4(sum, q[i]);
       }
+      for (; u < t; ++u) sum = add4(sum, c4[((int64_t)u * 2 + 1) * F4 + c]);
+      sum = add4(sum, c4[(int64_t)t * 2 * F4 + c]);
+      reinterpret_cast<float4*>(a.out + (int64_t)r * a.ldo)[c] = sum;
     }
-  }
-  if (x < a.n_rows && a.rowptr[x + 1] == a.rowptr[x]) {
-    float4* o = reinterpret_cast<float4*>(a.out + (int64_t)x * a.ldo);
+  } else if (w < a.n_jobs + a.n_empty) {
+    const int r = a.jobs[3 * a.ntasks + (w - a.n_jobs)];    // the empty-row list
+    if (r < 0 || r >= a.n_rows) return;
+    float4* o = reinterpret_cast<float4*>(a.out + (int64_t)r * a.ldo);
     for (int c = lane; c < F4; c += 64) o[c] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
 }
@@ -273,6 +330,26 @@ static void launch_task(const TaskArgs& a, int tiles, hipStream_t s) {
                      s, a);
 }
 
+// U edges per block, at most G (a block's records live in the group's lanes)
+template <int G, int NC>
+static void launch_task_u(const TaskArgs& a, int tiles, int U, bool near, hipStream_t s) {
+  if (U > G) U = G;
+  if (near) {
+    if constexpr (G >= 16) {
+      if (U == 16) return launch_task<G, NC, 16, false>(a, tiles, s);
+    }
+    if (U == 8) return launch_task<G, NC, 8, false>(a, tiles, s);
+    if (U == 4) return launch_task<G, NC, 4, false>(a, tiles, s);
+    return launch_task<G, NC, 2, false>(a, tiles, s);
+  }
+  if constexpr (G >= 16) {
+    if (U == 16) return launch_task<G, NC, 16, true>(a, tiles, s);
+  }
+  if (U == 8) return launch_task<G, NC, 8, true>(a, tiles, s);
+  if (U == 4) return launch_task<G, NC, 4, true>(a, tiles, s);
+  return launch_task<G, NC, 2, true>(a, tiles, s);
+}
+
 static int task_env(const char* name, int dflt) {
   const char* v = getenv(name);
   return v ? atoi(v) : dflt;
@@ -282,45 +359,63 @@ static int task_env(const char* name, int dflt) {
 
 using namespace vqgnn;
 
-extern "C" int32_t vqgnn_spmm_task_size(int64_t nnz, int32_t K) {
+static int task_count(int64_t nnz, int K) { return (int)((nnz + K - 1) / K); }
+
+extern "C" int64_t vqgnn_spmm_task_size(int64_t nnz, int32_t K, int32_t n_rows) {
   if (K <= 0) K = 64;
-  return (int32_t)((nnz + K - 1) / K);
+  // starts [ntasks + 1], first rows [ntasks], jobs [ntasks][3], empty rows [n_rows]
+  return 5 * (int64_t)task_count(nnz, K) + 1 + (n_rows > 0 ? n_rows : 0);
 }
 
 extern "C" int vqgnn_spmm_task_plan(const int32_t* rowptr, const int32_t* col, const float* val,
-                                    int32_t n_rows, int64_t nnz, int32_t K, int32_t* task_row,
-                                    int64_t* records, vqgnn_stream_t stream) {
+                                    int32_t n_rows, int64_t nnz, int32_t K, int32_t* plan,
+                                    int64_t* records, int32_t* counts, vqgnn_stream_t stream) {
   clear_error();
-  VQGNN_REQUIRE(rowptr && n_rows >= 0 && nnz >= 0 && nnz < (int64_t)1 << 31,
+  VQGNN_REQUIRE(rowptr && plan && counts && n_rows >= 0 && nnz >= 0 && nnz < (int64_t)1 << 31,
                 "spmm_task_plan: bad arguments");
-  VQGNN_REQUIRE(K >= 8 && K % 4 == 0 && K <= 4096, "spmm_task_plan: K=%d must be a multiple of 4 in [8, 4096]", K);
-  VQGNN_REQUIRE(nnz == 0 || (col && task_row && records), "spmm_task_plan: null pointer");
-  if (nnz == 0) return VQGNN_OK;
+  VQGNN_REQUIRE(K >= 8 && K % 4 == 0 && K <= 4096,
+                "spmm_task_plan: K=%d must be a multiple of 4 in [8, 4096]", K);
+  VQGNN_REQUIRE(nnz == 0 || (col && records), "spmm_task_plan: null pointer");
   hipStream_t s = as_stream(stream);
+  const int ntasks = task_count(nnz, K);
+  int32_t* task_start = plan;
+  int32_t* task_row = plan + ntasks + 1;
+  int32_t* jobs = task_row + ntasks;
+  int32_t* empties = jobs + 3 * ntasks;
+  if (hipMemsetAsync(counts, 0, 2 * sizeof(int32_t), s) != hipSuccess)
+    return check_launch("spmm_task_plan memset");
   int2* rec = reinterpret_cast<int2*>(records);
-  const int ntasks = vqgnn_spmm_task_size(nnz, K);
-  hipLaunchKernelGGL(task_records_kernel, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s, col,
-                     val, (int)nnz, rec);
-  if (n_rows > 0)
-    hipLaunchKernelGGL(task_row_ends_kernel, dim3((n_rows + 255) / 256), dim3(256), 0, s, rowptr,
-                       n_rows, rec);
-  hipLaunchKernelGGL(task_first_row_kernel, dim3((ntasks + 255) / 256), dim3(256), 0, s, rowptr,
-                     n_rows, K, ntasks, task_row);
+  if (nnz > 0) {
+    hipLaunchKernelGGL(task_records_kernel, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s,
+                       col, val, (int)nnz, rec);
+    if (n_rows > 0)
+      hipLaunchKernelGGL(task_row_ends_kernel, dim3((n_rows + 255) / 256), dim3(256), 0, s,
+                         rowptr, n_rows, rec);
+  }
+  hipLaunchKernelGGL(task_first_row_kernel, dim3((ntasks + 256) / 256), dim3(256), 0, s, rowptr,
+                     n_rows, (int)nnz, K, task_env("VQGNN_TASK_SNAP", 1) ? K / 2 : 0, ntasks,
+                     task_start, task_row);
+  const int nx = ntasks > n_rows ? ntasks : n_rows;
+  if (nx > 0)
+    hipLaunchKernelGGL(task_jobs_kernel, dim3((nx + 255) / 256), dim3(256), 0, s, rowptr, n_rows,
+                       ntasks, task_start, task_row, jobs, empties, counts);
   return check_launch("spmm_task_plan");
 }
 
 extern "C" size_t vqgnn_spmm_task_workspace(int64_t nnz, int32_t K, int32_t F) {
-  return align_up((size_t)vqgnn_spmm_task_size(nnz, K) * 2 * F * sizeof(float), 256) + 256;
+  return align_up((size_t)task_count(nnz, K > 0 ? K : 64) * 2 * F * sizeof(float), 256) + 256;
 }
 
 extern "C" int vqgnn_spmm_task(const int32_t* rowptr, int32_t n_rows, int32_t n_cols, int64_t nnz,
                                int32_t B, const float* X, int64_t ldx, const float* X2,
                                int64_t ldx2, int32_t F, float* out, int64_t ldo,
-                               const int32_t* task_row, const int64_t* records, int32_t K,
-                               void* workspace, vqgnn_stream_t stream) {
+                               const int32_t* plan, const int64_t* records, int32_t K,
+                               int32_t n_jobs, int32_t n_empty, void* workspace,
+                               vqgnn_stream_t stream) {
   clear_error();
-  VQGNN_REQUIRE(rowptr && out && (nnz == 0 || (X && task_row && records && workspace)),
+  VQGNN_REQUIRE(rowptr && out && plan && (nnz == 0 || (X && records && workspace)),
                 "spmm_task: null pointer");
+  VQGNN_REQUIRE(n_jobs >= 0 && n_empty >= 0, "spmm_task: bad job counts");
   VQGNN_REQUIRE(F > 0 && F % 4 == 0, "spmm_task: F=%d must be a positive multiple of 4", F);
   VQGNN_REQUIRE(ldx % 4 == 0 && ldo % 4 == 0 && (!X2 || ldx2 % 4 == 0) &&
                     ((uintptr_t)X & 15) == 0 && ((uintptr_t)out & 15) == 0 &&
@@ -333,12 +428,16 @@ extern "C" int vqgnn_spmm_task(const int32_t* rowptr, int32_t n_rows, int32_t n_
   hipStream_t s = as_stream(stream);
   TaskArgs a{};
   a.rec = reinterpret_cast<const int2*>(records);
-  a.task_row = task_row;
+  a.ntasks = task_count(nnz, K);
+  a.task_start = plan;
+  a.task_row = plan + a.ntasks + 1;
+  a.jobs = a.task_row + a.ntasks;
+  a.n_jobs = n_jobs;
+  a.n_empty = n_empty;
   a.rowptr = rowptr;
   a.n_rows = n_rows;
   a.nnz = (int)nnz;
   a.K = K;
-  a.ntasks = vqgnn_spmm_task_size(nnz, K);
   a.B = X2 ? B : n_cols;
   a.X = X;
   a.ldx = ldx;
@@ -381,31 +480,18 @@ extern "C" int vqgnn_spmm_task(const int32_t* rowptr, int32_t n_rows, int32_t n_
     const int Ue = task_env("VQGNN_TASK_U", 8);
     const int U = Ue >= 16 ? 16 : (Ue >= 8 ? 8 : (Ue >= 4 ? 4 : 2));
     a.dbg = task_env("VQGNN_TASK_DBG", 0);
-#define VQGNN_TASK_LAUNCH(G_, NC_)                                  \
-  if (near) {                                                       \
-    if (U == 16) launch_task<G_, NC_, 16, false>(a, tiles, s);      \
-    else if (U == 8) launch_task<G_, NC_, 8, false>(a, tiles, s);   \
-    else if (U == 4) launch_task<G_, NC_, 4, false>(a, tiles, s);   \
-    else launch_task<G_, NC_, 2, false>(a, tiles, s);               \
-  } else {                                                          \
-    if (U == 16) launch_task<G_, NC_, 16, true>(a, tiles, s);       \
-    else if (U == 8) launch_task<G_, NC_, 8, true>(a, tiles, s);    \
-    else if (U == 4) launch_task<G_, NC_, 4, true>(a, tiles, s);    \
-    else launch_task<G_, NC_, 2, true>(a, tiles, s);                \
-  }
     if (G == 8) {
-      if (nc == 1) { VQGNN_TASK_LAUNCH(8, 1) }
-      else if (nc == 2) { VQGNN_TASK_LAUNCH(8, 2) }
-      else { VQGNN_TASK_LAUNCH(8, 4) }
+      if (nc == 1) launch_task_u<8, 1>(a, tiles, U, near, s);
+      else if (nc == 2) launch_task_u<8, 2>(a, tiles, U, near, s);
+      else launch_task_u<8, 4>(a, tiles, U, near, s);
     } else if (G == 16) {
-      if (nc == 1) { VQGNN_TASK_LAUNCH(16, 1) }
-      else { VQGNN_TASK_LAUNCH(16, 2) }
+      if (nc == 1) launch_task_u<16, 1>(a, tiles, U, near, s);
+      else launch_task_u<16, 2>(a, tiles, U, near, s);
     } else {
-      VQGNN_TASK_LAUNCH(32, 1)
+      launch_task_u<32, 1>(a, tiles, U, near, s);
     }
-#undef VQGNN_TASK_LAUNCH
   }
-  const int nfix = a.ntasks > n_rows ? a.ntasks : n_rows;
+  const int nfix = n_jobs + n_empty;
   if (nfix > 0)
     hipLaunchKernelGGL(spmm_task_fixup_kernel, dim3((nfix + 3) / 4), dim3(256), 0, s, a);
   return check_launch("spmm_task");

@@ -272,13 +272,16 @@ def spmm_pair_plan(rowptr, n_rows, nnz, F, B, chunk=None):
 
 class TaskPlan:
     """Task plan of a CSR for vqgnn_spmm_task (include/vqgnn.h §6e): per-edge
-    records (column, row-end flag, weight) and each task's first row; built
-    once per batch adjacency, valid for any F and any leading row count."""
+    records (column, row-end flag, weight), the tasks' first edges and rows,
+    and the fix-up jobs (cut rows, empty rows); built once per batch
+    adjacency, valid for any F and any leading row count.  Building it reads
+    the two job counts back to the host (one sync per plan)."""
 
-    def __init__(self, task_row, records, K, nnz, n_rows, val):
-        self.task_row, self.records, self.K = task_row, records, K
+    def __init__(self, plan, records, K, nnz, n_rows, val, n_jobs, n_empty):
+        self.plan, self.records, self.K = plan, records, K
         self.nnz, self.n_rows = nnz, n_rows
         self.val_ptr = val.data_ptr() if val is not None else 0
+        self.n_jobs, self.n_empty = n_jobs, n_empty
 
 
 TASK_K = 64
@@ -288,12 +291,15 @@ def spmm_task_plan(rowptr, col, val, n_rows, nnz, K=None):
     L = lib()
     K = int(K or TASK_K)
     dev = rowptr.device
-    nt = L.vqgnn_spmm_task_size(int(nnz), K)
-    task_row = torch.empty(max(nt, 1), dtype=torch.int32, device=dev)
+    m = L.vqgnn_spmm_task_size(int(nnz), K, int(n_rows))
+    plan = torch.empty(max(m, 1), dtype=torch.int32, device=dev)
     records = torch.empty(max(int(nnz), 1), dtype=torch.int64, device=dev)
+    counts = torch.empty(2, dtype=torch.int32, device=dev)
     check(L.vqgnn_spmm_task_plan(ptr(rowptr), ptr(col), ptr(val), int(n_rows), int(nnz), K,
-                                 ptr(task_row), ptr(records), stream_ptr()), "spmm_task_plan")
-    return TaskPlan(task_row, records, K, int(nnz), int(n_rows), val)
+                                 ptr(plan), ptr(records), ptr(counts), stream_ptr()),
+          "spmm_task_plan")
+    n_jobs, n_empty = (int(v) for v in counts.tolist())
+    return TaskPlan(plan, records, K, int(nnz), int(n_rows), val, n_jobs, n_empty)
 
 
 def spmm(rowptr, col, val, n_rows, nnz, X, F, X2=None, B=None, out=None, plan=None):
@@ -317,8 +323,8 @@ def spmm(rowptr, col, val, n_rows, nnz, X, F, X2=None, B=None, out=None, plan=No
         ws = workspace(L.vqgnn_spmm_task_workspace(int(nnz), plan.K, F), dev)
         check(L.vqgnn_spmm_task(ptr(rowptr), int(n_rows), int(n_cols), int(nnz), Bv, ptr(X),
                                 _ld(X), ptr(X2), _ld(X2) if X2 is not None else 0, F, ptr(out),
-                                _ld(out), ptr(plan.task_row), ptr(plan.records), plan.K,
-                                ptr(ws), stream_ptr()), "spmm_task")
+                                _ld(out), ptr(plan.plan), ptr(plan.records), plan.K,
+                                plan.n_jobs, plan.n_empty, ptr(ws), stream_ptr()), "spmm_task")
         return out
     ws = workspace(L.vqgnn_spmm_workspace(n_rows, nnz, F), dev)
     if isinstance(plan, PairPlan):
