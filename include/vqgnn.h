@@ -361,6 +361,25 @@ int vqgnn_gat_edge_grad(const int32_t* rows, const int32_t* col, const float* co
                         const float* params, float negative_slope, float* dalpha_l,
                         float* dalpha_r, float* ds_row, vqgnn_stream_t stream);
 
+/* 8b. Fused GAT aggregation (the default GAT forward): the task-split SpMM of
+ *     6e with each edge's coefficient exp(leaky(alpha_l[j]/s + alpha_r[i]/s))
+ *     * w computed in the kernel (the op order of vqgnn_gat_coef; s =
+ *     params[2] of vqgnn_gat_alpha), the ones column as a per-row
+ *     coefficient sum, and rows < norm_B divided by that sum + 1e-16 before
+ *     the store (models.py:188; norm_B = 0: no normalisation).  Replaces
+ *     vqgnn_gat_coef + vqgnn_spmm + vqgnn_gat_normalize; the coefficients are
+ *     never materialised unless coef (optional, [nnz], CSR order) is given for
+ *     the backward; den (optional, [n_rows]) receives the sums.  erow: the
+ *     COO row of every edge (vqgnn_csr_expand_rows).  Plan and workspace as
+ *     6e (records hold the adjacency values w).                              */
+int vqgnn_gat_spmm_task(const int32_t* rowptr, int32_t n_rows, int32_t n_cols, int64_t nnz,
+                        int32_t B, const float* X, int64_t ldx, const float* X2, int64_t ldx2,
+                        int32_t F, float* out, int64_t ldo, const int32_t* plan,
+                        const int64_t* records, int32_t K, int32_t n_jobs, int32_t n_empty,
+                        const int32_t* erow, const float* alpha_l, const float* alpha_r,
+                        const float* params, float negative_slope, int32_t norm_B, float* den,
+                        float* coef, void* workspace, vqgnn_stream_t stream);
+
 /* ------------------------------------------------------------------------ *
  * 9. Mini-batch construction on the device.
  *    Replaces OurDataLoader._k_hop_subgraph (dataloader.py:98-148; num_hops,

@@ -113,3 +113,71 @@ def test_gat_reference_forward_dense_input():
     ref, _ = conv_ref.gat_forward(x, conv.att_l.detach().cpu().numpy(),
                                   conv.att_r.detach().cpu().numpy(), b.rowptr, b.col, b.val)
     np.testing.assert_allclose(out.detach().cpu().numpy(), ref.numpy(), rtol=1e-5, atol=1e-6)
+
+
+def _hub_csr(n, B, rng):
+    """A batch-like CSR with hub rows (cut by the task split), empty rows and
+    single-edge rows; GAT-normalised (D^-1) positive weights."""
+    deg = rng.integers(1, 20, size=n)
+    deg[[5, n // 2, B - 1]] = [700, 333, 1200]
+    deg[rng.random(n) < 0.05] = 0
+    rowptr = np.zeros(n + 1, np.int64)
+    rowptr[1:] = np.cumsum(deg)
+    col = np.concatenate([np.sort(rng.choice(n, size=d, replace=d > n)) for d in deg])
+    val = np.repeat(1.0 / np.maximum(deg, 1), deg).astype(np.float32)
+    return rowptr, col.astype(np.int64), val
+
+
+@pytest.mark.parametrize("F", [32, 128, 256])
+def test_gat_fused_kernel_matches_coefficient_path(F, monkeypatch):
+    """vqgnn_gat_spmm_task (coefficients in the aggregation kernel) against the
+    coefficient pass + SpMM + normalise path, on hub rows cut across tasks,
+    empty rows and a multi-tile F; the optional coef / den outputs equal
+    vqgnn_gat_coef's."""
+    rng = np.random.default_rng(F + 1)
+    n, B = 3000, 1800
+    rowptr, col, val = _hub_csr(n, B, rng)
+    adj = CSR(torch.as_tensor(rowptr), torch.as_tensor(col), torch.as_tensor(val),
+              (n, n)).to(DEV)
+    nnz = adj.nnz()
+    x = torch.randn(B, F, device=DEV)
+    xf = torch.randn(n - B, F, device=DEV)
+    conv = _conv(F, 3).to(DEV)
+    al, ar, params = kernels.gat_alpha(x, conv.att_l.view(-1), conv.att_r.view(-1), F, X2=xf,
+                                       B=B, ones=True)
+    plan = adj.plan(F, B=B)
+    assert isinstance(plan, kernels.TaskPlan)
+    out, den, coef = kernels.gat_spmm(adj.rowptr, adj.col, adj.value, n, nnz, x, F, al, ar,
+                                      params, plan, adj.rows(), X2=xf, B=B, norm_B=B,
+                                      want_den=True, want_coef=True)
+    coef_ref, den_ref = kernels.gat_coef(adj.rowptr, adj.col, adj.value, n, nnz, al, ar, params)
+    assert torch.equal(coef, coef_ref)                    # same op order, same bits
+    torch.testing.assert_close(den, den_ref, rtol=1e-6, atol=0)
+    ref = kernels.spmm(adj.rowptr, adj.col, coef_ref, n, nnz, x, F, X2=xf, B=B,
+                       plan=adj.plan(F, B=B, kind="chunk"))
+    kernels.gat_normalize(ref, B, F, den_ref, 1e-16)
+    # fp64 bound: |got - ref64| <= 1e-5 * sum |coef| |x| / (den + eps) (rows < B)
+    xin = torch.cat([x, xf]).double().cpu().numpy()
+    c64 = coef_ref.double().cpu().numpy()
+    ref64 = conv_ref.spmm_fp64(rowptr, col, c64, xin)
+    sc = conv_ref.spmm_fp64(rowptr, col, np.abs(c64), np.abs(xin))
+    d64 = den_ref.double().cpu().numpy()[:, None] + 1e-16
+    ref64[:B] /= d64[:B]
+    sc[:B] /= d64[:B]
+    for got in (out, ref):
+        err = np.abs(got.cpu().numpy() - ref64)
+        assert (err <= 1e-5 * sc + 1e-30).all(), f"rel err {(err / (sc + 1e-30)).max():.2e}"
+    assert torch.equal(out[torch.as_tensor(np.diff(rowptr) == 0, device=DEV)],
+                       torch.zeros_like(out[torch.as_tensor(np.diff(rowptr) == 0, device=DEV)]))
+    again, _, _ = kernels.gat_spmm(adj.rowptr, adj.col, adj.value, n, nnz, x, F, al, ar, params,
+                                   plan, adj.rows(), X2=xf, B=B, norm_B=B)
+    assert torch.equal(out, again)
+    # the layer path uses the fused kernel by default and the chunk path on request
+    monkeypatch.setenv("VQGNN_SPMM", "chunk")
+    adj2 = CSR(torch.as_tensor(rowptr), torch.as_tensor(col), torch.as_tensor(val),
+               (n, n)).to(DEV)
+    slow = conv.fused_forward(x, adj2, xf, B)
+    monkeypatch.delenv("VQGNN_SPMM")
+    fast = conv.fused_forward(x, adj, xf, B)
+    sc32 = torch.from_numpy(sc).to(DEV).float()
+    assert ((fast - slow).abs() <= 2e-5 * sc32 + 1e-30).all()

@@ -77,6 +77,11 @@ SIGNATURES = {
     "vqgnn_spmm_task": (ctypes.c_int, [_c_void_p, _i32, _i32, _i64, _i32, _c_void_p, _i64,
                                        _c_void_p, _i64, _i32, _c_void_p, _i64, _c_void_p,
                                        _c_void_p, _i32, _i32, _i32, _c_void_p, _c_void_p]),
+    "vqgnn_gat_spmm_task": (ctypes.c_int, [_c_void_p, _i32, _i32, _i64, _i32, _c_void_p, _i64,
+                                           _c_void_p, _i64, _i32, _c_void_p, _i64, _c_void_p,
+                                           _c_void_p, _i32, _i32, _i32, _c_void_p, _c_void_p,
+                                           _c_void_p, _c_void_p, _f32, _i32, _c_void_p,
+                                           _c_void_p, _c_void_p, _c_void_p]),
     "vqgnn_spmm_plan_size": (_i64, [_i64, _i32]),
     "vqgnn_spmm_plan": (ctypes.c_int, [_c_void_p, _i32, _i64, _i32, _c_void_p, _c_void_p]),
     "vqgnn_csr_transpose_workspace": (_size, [_i32, _i32, _i64]),

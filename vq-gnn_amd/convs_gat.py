@@ -8,9 +8,11 @@ initialisation order, so the RNG stream at construction matches the reference.
 The arithmetic runs in HIP (include/vqgnn.h §8):
 
   alpha_l/r = x_in . att_l/r (+ global max -> scale s)    vqgnn_gat_alpha
-  coef_e    = exp(leaky(alpha_l[j]/s + alpha_r[i]/s)) * w  vqgnn_gat_coef
-  out       = sum_e coef_e * x_in[j]                       vqgnn_spmm (values = coef)
-  rows < B  : out /= sum_e coef_e + 1e-16                  vqgnn_gat_normalize
+  coef_e    = exp(leaky(alpha_l[j]/s + alpha_r[i]/s)) * w  } vqgnn_gat_spmm_task (one
+  out       = sum_e coef_e * x_in[j]                       } fused kernel; the
+  rows < B  : out /= sum_e coef_e + 1e-16                  } coefficients stay in
+                                                              registers)
+(VQGNN_SPMM=chunk: vqgnn_gat_coef + vqgnn_spmm + vqgnn_gat_normalize.)
 
 The backward (dX for the batch rows, d att_l, d att_r) differentiates the same
 chain: the transposed-coefficient SpMM, vqgnn_gat_edge_grad for the
@@ -47,14 +49,27 @@ class GATFunction(torch.autograd.Function):
         F = x.shape[1]
         xc = x.contiguous()
         al, ar, params = kernels.gat_alpha(xc, att_l, att_r, F, X2=x_first, B=B, ones=ones)
-        coef, den = kernels.gat_coef(adj.rowptr, adj.col, adj.value, n, nnz, al, ar, params,
-                                     slope)
-        out = kernels.spmm(adj.rowptr, adj.col, coef, n, nnz, xc, F, X2=x_first,
-                           B=B if x_first is not None else None,
-                           plan=adj.plan(F, B=B if x_first is not None else None,
-                                         kind="chunk"))
-        if normalize:
-            kernels.gat_normalize(out, B, F, den, 1e-16)
+        plan = adj.plan(F, B=B if x_first is not None else None)
+        if isinstance(plan, kernels.TaskPlan):
+            # fused: coefficients, ones-column sums and the normalisation in the
+            # aggregation kernel; coef / den kept only when a backward follows
+            # (grad mode is off inside forward: ask the context what the
+            # backward will need)
+            grad = any(ctx.needs_input_grad[:4])
+            out, den, coef = kernels.gat_spmm(
+                adj.rowptr, adj.col, adj.value, n, nnz, xc, F, al, ar, params, plan, adj.rows(),
+                X2=x_first, B=B if x_first is not None else None,
+                norm_B=B if normalize else 0, negative_slope=slope, want_den=grad,
+                want_coef=grad)
+        else:                     # VQGNN_SPMM=chunk: coefficient pass + SpMM + normalise
+            coef, den = kernels.gat_coef(adj.rowptr, adj.col, adj.value, n, nnz, al, ar, params,
+                                         slope)
+            out = kernels.spmm(adj.rowptr, adj.col, coef, n, nnz, xc, F, X2=x_first,
+                               B=B if x_first is not None else None,
+                               plan=adj.plan(F, B=B if x_first is not None else None,
+                                             kind="chunk"))
+            if normalize:
+                kernels.gat_normalize(out, B, F, den, 1e-16)
         ctx.save_for_backward(xc, x_first if x_first is not None else xc, att_l, att_r, al, ar,
                               params, coef, den, out)
         ctx.has_first = x_first is not None

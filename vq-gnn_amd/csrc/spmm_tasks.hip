@@ -57,11 +57,24 @@ struct TaskArgs {
   int F;                    // columns (multiple of 4)
   float* out;
   int64_t ldo;
-  float* carry;             // [ntasks][2][F]: head partial, tail partial
+  float* carry;             // [ntasks][2][cf]: head partial, tail partial (cf = F + 4:
+                            // GAT keeps the row's coefficient sum in slot F)
+  int cf;
   // near path: X and X2 as one 32-bit buffer range from ubase
   const char* ubase;
   uint32_t span, offx, ldxb, offx2, ldx2b;
   int dbg;                  // experiments: 1 = no row stores (results invalid)
+  // GAT mode (OurGATConv + the layer's ones-column normalisation): edge
+  // weight = exp(leaky(al[j]/s + ar[i]/s)) * w, rows < norm_B divided by
+  // their coefficient sum + 1e-16
+  const int32_t* erow;      // [nnz] COO row of every edge
+  const float* al;          // [n] alpha_l, alpha_r of x_in rows
+  const float* ar;
+  const float* params;      // params[2] = s
+  float slope;
+  int norm_B;
+  float* den;               // [n_rows] optional: coefficient sums
+  float* coef;              // [nnz] optional: the coefficients (for the backward)
 };
 
 __device__ __forceinline__ int upper_bound_i32(const int32_t* __restrict__ a, int n, int key) {
@@ -161,7 +174,16 @@ __device__ __forceinline__ void group_bcast(int x, int (&out)[sizeof...(Us)],
 // G lanes per task (64 / G tasks per wave), NC float4 pieces per lane (piece
 // i of lane k is float4 column G*i + k: a column tile of 4*G*NC floats), U
 // edges per block
-template <int G, int NC, int U, bool FAR>
+// GAT coefficient of one edge (convs.py:209-264, vq_softmax.py:33-57, the
+// op order of gat_coef_kernel): exp(leaky(al[j]/s + ar[i]/s)) * w
+__device__ __forceinline__ float gat_edge_coef(const TaskArgs& a, int e, uint32_t j, float w) {
+  const float s = a.params[2];
+  float x = __fadd_rn(__fdiv_rn(a.al[j], s), __fdiv_rn(a.ar[a.erow[e]], s));
+  x = x > 0.f ? x : __fmul_rn(x, a.slope);
+  return __fmul_rn(expf(x), w);
+}
+
+template <int G, int NC, int U, bool FAR, bool GAT = false>
 __global__ void __launch_bounds__(kTaskThreads)
 spmm_task_kernel(TaskArgs a) {
   constexpr int TPW = 64 / G;
@@ -205,12 +227,23 @@ spmm_task_kernel(TaskArgs a) {
   // Records outside [e0, e1) read as weight 0 without a row end.
   static_assert(U <= G, "records of a block live in the group's first U lanes");
   constexpr int kAnd = 0x1F & ~(G - 1);               // keep the group bits (32-lane swizzle)
+  // GAT: the record lane computes its edge's coefficient and broadcasts it as
+  // the weight (and, on column tile 0, stores it for the backward)
   auto load_rec = [&](int e) -> int2 {
     const int eu = e + k;
     const int2 q = __builtin_bit_cast(
         int2, __builtin_amdgcn_raw_buffer_load_b64(rsr, (uint32_t)eu * 8u, 0, 0));
-    return (k < U && eu >= e0 && eu < e1) ? q : make_int2(0, 0);
+    const bool in = k < U && eu >= e0 && eu < e1;
+    if constexpr (GAT) {
+      if (!in) return make_int2(0, 0);
+      const float c = gat_edge_coef(a, eu, (uint32_t)q.x & kColMask, __int_as_float(q.y));
+      if (a.coef && blockIdx.y == 0) a.coef[eu] = c;
+      return make_int2(q.x, __float_as_int(c));
+    } else {
+      return in ? q : make_int2(0, 0);
+    }
   };
+  float den = 0.f;     // GAT: the row's coefficient sum (the ones column), edge order
 
   // the wave runs as many U-edge blocks as its longest task needs
   int len = e1 - e0;
@@ -257,9 +290,28 @@ spmm_task_kernel(TaskArgs a) {
         acc[i].z = fmaf(w, v[u][i].z, acc[i].z);
         acc[i].w = fmaf(w, v[u][i].w, acc[i].w);
       }
+      if constexpr (GAT) den = __fadd_rn(den, w);
       open = open || real;
       if (x & kEndBit) {                   // the row ends at this edge
-        float* dst = head ? a.carry + (int64_t)t * 2 * a.F : a.out + (int64_t)r * a.ldo;
+        float* dst = head ? a.carry + (int64_t)t * 2 * a.cf : a.out + (int64_t)r * a.ldo;
+        if constexpr (GAT) {
+          if (head) {                      // partial: the fixup sums and normalises
+            if (k == 0 && blockIdx.y == 0) dst[a.F] = den;
+          } else {
+            if (a.den && k == 0 && blockIdx.y == 0) a.den[r] = den;
+            if (r < a.norm_B) {            // models.py:188: out[:, :F] /= out[:, F] + 1e-16
+              const float q = __fadd_rn(den, 1e-16f);
+#pragma unroll
+              for (int i = 0; i < NC; ++i) {
+                acc[i].x = __fdiv_rn(acc[i].x, q);
+                acc[i].y = __fdiv_rn(acc[i].y, q);
+                acc[i].z = __fdiv_rn(acc[i].z, q);
+                acc[i].w = __fdiv_rn(acc[i].w, q);
+              }
+            }
+          }
+          den = 0.f;
+        }
 #pragma unroll
         for (int i = 0; i < NC; ++i) {
           if (pv[i] && !(a.dbg & 1))
@@ -276,22 +328,28 @@ spmm_task_kernel(TaskArgs a) {
     rcur = rnxt;
   }
   if (open) {                              // the last row continues in the next task
-    float* dst = a.carry + ((int64_t)t * 2 + 1) * a.F;
+    float* dst = a.carry + ((int64_t)t * 2 + 1) * a.cf;
 #pragma unroll
     for (int i = 0; i < NC; ++i)
       if (pv[i]) *reinterpret_cast<float4*>(dst + 4 * (c4base + G * i)) = acc[i];
+    if constexpr (GAT) {
+      if (k == 0 && blockIdx.y == 0) dst[a.F] = den;
+    }
   }
 }
 
 // One wave per fix-up job.  A cut row: out[row] = tail[ts] + ... + tail[t-1]
-// + head[t], in task order (loads 8 tasks ahead of the in-order adds).  An
-// empty row: zeros.  Rows at or past n_rows (a call over leading rows) are
-// skipped.
+// + head[t], in task order (loads 8 tasks ahead of the in-order adds); GAT
+// sums the coefficient slot the same way, then normalises rows < norm_B.
+// An empty row: zeros.  Rows at or past n_rows (a call over leading rows)
+// are skipped.
+template <bool GAT>
 __global__ void __launch_bounds__(256)
 spmm_task_fixup_kernel(TaskArgs a) {
   const int lane = threadIdx.x & 63;
   const int w = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int F4 = a.F >> 2;
+  const int C4 = a.cf >> 2;                 // carry row stride in float4
   if (w < a.n_jobs) {
     const int r = a.jobs[3 * w], ts = a.jobs[3 * w + 1], t = a.jobs[3 * w + 2];
     if (r < 0 || r >= a.n_rows) return;
@@ -300,21 +358,44 @@ spmm_task_fixup_kernel(TaskArgs a) {
       return make_float4(__fadd_rn(x.x, y.x), __fadd_rn(x.y, y.y), __fadd_rn(x.z, y.z),
                          __fadd_rn(x.w, y.w));
     };
-    for (int c = lane; c < F4; c += 64) {
-      float4 sum = c4[((int64_t)ts * 2 + 1) * F4 + c];
+    // column F4 (GAT) is the coefficient-sum slot
+    const int ncol = GAT ? F4 + 1 : F4;
+    float q = 1.f;
+    bool norm = false;
+    if constexpr (GAT) {                   // every lane needs the row's coefficient sum
+      float d = a.carry[((int64_t)ts * 2 + 1) * a.cf + a.F];
+      for (int u = ts + 1; u < t; ++u) d = __fadd_rn(d, a.carry[((int64_t)u * 2 + 1) * a.cf + a.F]);
+      d = __fadd_rn(d, a.carry[(int64_t)t * 2 * a.cf + a.F]);
+      if (a.den && lane == 0) a.den[r] = d;
+      norm = r < a.norm_B;
+      q = __fadd_rn(d, 1e-16f);
+    }
+    for (int c = lane; c < ncol; c += 64) {
+      if (GAT && c == F4) continue;
+      float4 sum = c4[((int64_t)ts * 2 + 1) * C4 + c];
       int u = ts + 1;
       for (; u + 8 <= t; u += 8) {
-        float4 q[8];
+        float4 qq[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) q[i] = c4[((int64_t)(u + i) * 2 + 1) * F4 + c];
+        for (int i = 0; i < 8; ++i) qq[i] = c4[((int64_t)(u + i) * 2 + 1) * C4 + c];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) sum = add4(sum, q[i]);
+        for (int i = 0; i < 8; ++i) sum = add4(sum, qq[i]);
       }
-      for (; u < t; ++u) sum = add4(sum, c4[((int64_t)u * 2 + 1) * F4 + c]);
-      sum = add4(sum, c4[(int64_t)t * 2 * F4 + c]);
+      for (; u < t; ++u) sum = add4(sum, c4[((int64_t)u * 2 + 1) * C4 + c]);
+      sum = add4(sum, c4[(int64_t)t * 2 * C4 + c]);
+      if (norm) {
+        sum.x = __fdiv_rn(sum.x, q);
+        sum.y = __fdiv_rn(sum.y, q);
+        sum.z = __fdiv_rn(sum.z, q);
+        sum.w = __fdiv_rn(sum.w, q);
+      }
       reinterpret_cast<float4*>(a.out + (int64_t)r * a.ldo)[c] = sum;
     }
   } else if (w < a.n_jobs + a.n_empty) {
+    if constexpr (GAT) {
+      const int r0 = a.jobs[3 * a.ntasks + (w - a.n_jobs)];
+      if (a.den && lane == 0 && r0 >= 0 && r0 < a.n_rows) a.den[r0] = 0.f;
+    }
     const int r = a.jobs[3 * a.ntasks + (w - a.n_jobs)];    // the empty-row list
     if (r < 0 || r >= a.n_rows) return;
     float4* o = reinterpret_cast<float4*>(a.out + (int64_t)r * a.ldo);
@@ -322,32 +403,32 @@ spmm_task_fixup_kernel(TaskArgs a) {
   }
 }
 
-template <int G, int NC, int U, bool FAR>
+template <int G, int NC, int U, bool FAR, bool GAT>
 static void launch_task(const TaskArgs& a, int tiles, hipStream_t s) {
   const int waves = (a.ntasks + 64 / G - 1) / (64 / G);
   const int blocks = (waves + 3) / 4;
-  hipLaunchKernelGGL((spmm_task_kernel<G, NC, U, FAR>), dim3(blocks, tiles), dim3(kTaskThreads), 0,
-                     s, a);
+  hipLaunchKernelGGL((spmm_task_kernel<G, NC, U, FAR, GAT>), dim3(blocks, tiles),
+                     dim3(kTaskThreads), 0, s, a);
 }
 
 // U edges per block, at most G (a block's records live in the group's lanes)
-template <int G, int NC>
+template <int G, int NC, bool GAT>
 static void launch_task_u(const TaskArgs& a, int tiles, int U, bool near, hipStream_t s) {
   if (U > G) U = G;
   if (near) {
     if constexpr (G >= 16) {
-      if (U == 16) return launch_task<G, NC, 16, false>(a, tiles, s);
+      if (U == 16) return launch_task<G, NC, 16, false, GAT>(a, tiles, s);
     }
-    if (U == 8) return launch_task<G, NC, 8, false>(a, tiles, s);
-    if (U == 4) return launch_task<G, NC, 4, false>(a, tiles, s);
-    return launch_task<G, NC, 2, false>(a, tiles, s);
+    if (U == 8) return launch_task<G, NC, 8, false, GAT>(a, tiles, s);
+    if (U == 4) return launch_task<G, NC, 4, false, GAT>(a, tiles, s);
+    return launch_task<G, NC, 2, false, GAT>(a, tiles, s);
   }
   if constexpr (G >= 16) {
-    if (U == 16) return launch_task<G, NC, 16, true>(a, tiles, s);
+    if (U == 16) return launch_task<G, NC, 16, true, GAT>(a, tiles, s);
   }
-  if (U == 8) return launch_task<G, NC, 8, true>(a, tiles, s);
-  if (U == 4) return launch_task<G, NC, 4, true>(a, tiles, s);
-  return launch_task<G, NC, 2, true>(a, tiles, s);
+  if (U == 8) return launch_task<G, NC, 8, true, GAT>(a, tiles, s);
+  if (U == 4) return launch_task<G, NC, 4, true, GAT>(a, tiles, s);
+  return launch_task<G, NC, 2, true, GAT>(a, tiles, s);
 }
 
 static int task_env(const char* name, int dflt) {
@@ -403,16 +484,18 @@ extern "C" int vqgnn_spmm_task_plan(const int32_t* rowptr, const int32_t* col, c
 }
 
 extern "C" size_t vqgnn_spmm_task_workspace(int64_t nnz, int32_t K, int32_t F) {
-  return align_up((size_t)task_count(nnz, K > 0 ? K : 64) * 2 * F * sizeof(float), 256) + 256;
+  // carries: [ntasks][2][F + 4] (slot F: the GAT coefficient sum)
+  return align_up((size_t)task_count(nnz, K > 0 ? K : 64) * 2 * (F + 4) * sizeof(float), 256) +
+         256;
 }
 
-extern "C" int vqgnn_spmm_task(const int32_t* rowptr, int32_t n_rows, int32_t n_cols, int64_t nnz,
-                               int32_t B, const float* X, int64_t ldx, const float* X2,
-                               int64_t ldx2, int32_t F, float* out, int64_t ldo,
-                               const int32_t* plan, const int64_t* records, int32_t K,
-                               int32_t n_jobs, int32_t n_empty, void* workspace,
-                               vqgnn_stream_t stream) {
-  clear_error();
+// Shared setup of vqgnn_spmm_task / vqgnn_gat_spmm_task: validation, the
+// task geometry and the near (one 32-bit buffer range) or far source path.
+static int task_setup(TaskArgs& a, const int32_t* rowptr, int32_t n_rows, int32_t n_cols,
+                      int64_t nnz, int32_t B, const float* X, int64_t ldx, const float* X2,
+                      int64_t ldx2, int32_t F, float* out, int64_t ldo, const int32_t* plan,
+                      const int64_t* records, int32_t K, int32_t n_jobs, int32_t n_empty,
+                      void* workspace, bool* near) {
   VQGNN_REQUIRE(rowptr && out && plan && (nnz == 0 || (X && records && workspace)),
                 "spmm_task: null pointer");
   VQGNN_REQUIRE(n_jobs >= 0 && n_empty >= 0, "spmm_task: bad job counts");
@@ -425,8 +508,6 @@ extern "C" int vqgnn_spmm_task(const int32_t* rowptr, int32_t n_rows, int32_t n_
   VQGNN_REQUIRE(n_cols <= (int32_t)kColMask, "spmm_task: %d columns exceed 2^26", n_cols);
   VQGNN_REQUIRE(B >= 0 && (X2 || B == 0), "spmm_task: B=%d without X2", B);
   VQGNN_REQUIRE(K >= 8 && K % 4 == 0, "spmm_task: K=%d", K);
-  hipStream_t s = as_stream(stream);
-  TaskArgs a{};
   a.rec = reinterpret_cast<const int2*>(records);
   a.ntasks = task_count(nnz, K);
   a.task_start = plan;
@@ -444,12 +525,13 @@ extern "C" int vqgnn_spmm_task(const int32_t* rowptr, int32_t n_rows, int32_t n_
   a.X2 = X2 ? X2 : X;
   a.ldx2 = X2 ? ldx2 : ldx;
   a.F = F;
+  a.cf = F + 4;
   a.out = out;
   a.ldo = ldo;
   a.carry = reinterpret_cast<float*>(workspace);
-  // near path: both sources inside one 32-bit byte range
   const int nx = a.B, nx2 = X2 ? n_cols - B : 0;
-  const uintptr_t x0 = (uintptr_t)X, x1 = x0 + (uintptr_t)((int64_t)(nx > 0 ? nx - 1 : 0) * ldx + F) * 4;
+  const uintptr_t x0 = (uintptr_t)X;
+  const uintptr_t x1 = x0 + (uintptr_t)((int64_t)(nx > 0 ? nx - 1 : 0) * ldx + F) * 4;
   uintptr_t lo = x0, hi = x1;
   uintptr_t y0 = 0, y1 = 0;
   if (nx2 > 0) {
@@ -458,9 +540,9 @@ extern "C" int vqgnn_spmm_task(const int32_t* rowptr, int32_t n_rows, int32_t n_
     lo = lo < y0 ? lo : y0;
     hi = hi > y1 ? hi : y1;
   }
-  const bool near = hi - lo < 0x7FFFFFF0ull && (int64_t)ldx * 4 < 0x7FFFFFFF &&
-                    (int64_t)a.ldx2 * 4 < 0x7FFFFFFF && !task_env("VQGNN_SPMM_FAR", 0);
-  if (near) {
+  *near = hi - lo < 0x7FFFFFF0ull && (int64_t)ldx * 4 < 0x7FFFFFFF &&
+          (int64_t)a.ldx2 * 4 < 0x7FFFFFFF && !task_env("VQGNN_SPMM_FAR", 0);
+  if (*near) {
     a.ubase = reinterpret_cast<const char*>(lo);
     a.span = (uint32_t)(hi - lo);
     a.offx = (uint32_t)(x0 - lo);
@@ -468,8 +550,14 @@ extern "C" int vqgnn_spmm_task(const int32_t* rowptr, int32_t n_rows, int32_t n_
     a.offx2 = nx2 > 0 ? (uint32_t)(y0 - lo) : 0;
     a.ldx2b = (uint32_t)(a.ldx2 * 4);
   }
-  if (nnz > 0) {
-    const int F4 = F / 4;
+  a.dbg = task_env("VQGNN_TASK_DBG", 0);
+  return VQGNN_OK;
+}
+
+template <bool GAT>
+static void task_launch(const TaskArgs& a, bool near, hipStream_t s) {
+  if (a.nnz > 0) {
+    const int F4 = a.F / 4;
     // lanes per task: VQGNN_TASK_G (8, 16 or 32; default 32); pieces per lane
     // so that one column tile covers min(F, 128) floats
     int G = task_env("VQGNN_TASK_G", 32);
@@ -479,20 +567,63 @@ extern "C" int vqgnn_spmm_task(const int32_t* rowptr, int32_t n_rows, int32_t n_
     const int tiles = (F4 + nc * G - 1) / (nc * G);
     const int Ue = task_env("VQGNN_TASK_U", 8);
     const int U = Ue >= 16 ? 16 : (Ue >= 8 ? 8 : (Ue >= 4 ? 4 : 2));
-    a.dbg = task_env("VQGNN_TASK_DBG", 0);
     if (G == 8) {
-      if (nc == 1) launch_task_u<8, 1>(a, tiles, U, near, s);
-      else if (nc == 2) launch_task_u<8, 2>(a, tiles, U, near, s);
-      else launch_task_u<8, 4>(a, tiles, U, near, s);
+      if (nc == 1) launch_task_u<8, 1, GAT>(a, tiles, U, near, s);
+      else if (nc == 2) launch_task_u<8, 2, GAT>(a, tiles, U, near, s);
+      else launch_task_u<8, 4, GAT>(a, tiles, U, near, s);
     } else if (G == 16) {
-      if (nc == 1) launch_task_u<16, 1>(a, tiles, U, near, s);
-      else launch_task_u<16, 2>(a, tiles, U, near, s);
+      if (nc == 1) launch_task_u<16, 1, GAT>(a, tiles, U, near, s);
+      else launch_task_u<16, 2, GAT>(a, tiles, U, near, s);
     } else {
-      launch_task_u<32, 1>(a, tiles, U, near, s);
+      launch_task_u<32, 1, GAT>(a, tiles, U, near, s);
     }
   }
-  const int nfix = n_jobs + n_empty;
+  const int nfix = a.n_jobs + a.n_empty;
   if (nfix > 0)
-    hipLaunchKernelGGL(spmm_task_fixup_kernel, dim3((nfix + 3) / 4), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(spmm_task_fixup_kernel<GAT>, dim3((nfix + 3) / 4), dim3(256), 0, s, a);
+}
+
+extern "C" int vqgnn_spmm_task(const int32_t* rowptr, int32_t n_rows, int32_t n_cols, int64_t nnz,
+                               int32_t B, const float* X, int64_t ldx, const float* X2,
+                               int64_t ldx2, int32_t F, float* out, int64_t ldo,
+                               const int32_t* plan, const int64_t* records, int32_t K,
+                               int32_t n_jobs, int32_t n_empty, void* workspace,
+                               vqgnn_stream_t stream) {
+  clear_error();
+  TaskArgs a{};
+  bool near = false;
+  const int rc = task_setup(a, rowptr, n_rows, n_cols, nnz, B, X, ldx, X2, ldx2, F, out, ldo,
+                            plan, records, K, n_jobs, n_empty, workspace, &near);
+  if (rc != VQGNN_OK) return rc;
+  task_launch<false>(a, near, as_stream(stream));
   return check_launch("spmm_task");
+}
+
+extern "C" int vqgnn_gat_spmm_task(const int32_t* rowptr, int32_t n_rows, int32_t n_cols,
+                                   int64_t nnz, int32_t B, const float* X, int64_t ldx,
+                                   const float* X2, int64_t ldx2, int32_t F, float* out,
+                                   int64_t ldo, const int32_t* plan, const int64_t* records,
+                                   int32_t K, int32_t n_jobs, int32_t n_empty,
+                                   const int32_t* erow, const float* alpha_l,
+                                   const float* alpha_r, const float* params,
+                                   float negative_slope, int32_t norm_B, float* den, float* coef,
+                                   void* workspace, vqgnn_stream_t stream) {
+  clear_error();
+  TaskArgs a{};
+  bool near = false;
+  const int rc = task_setup(a, rowptr, n_rows, n_cols, nnz, B, X, ldx, X2, ldx2, F, out, ldo,
+                            plan, records, K, n_jobs, n_empty, workspace, &near);
+  if (rc != VQGNN_OK) return rc;
+  VQGNN_REQUIRE(nnz == 0 || (erow && alpha_l && alpha_r && params), "gat_spmm_task: null pointer");
+  VQGNN_REQUIRE(norm_B >= 0, "gat_spmm_task: norm_B=%d", norm_B);
+  a.erow = erow;
+  a.al = alpha_l;
+  a.ar = alpha_r;
+  a.params = params;
+  a.slope = negative_slope;
+  a.norm_B = norm_B;
+  a.den = den;
+  a.coef = coef;
+  task_launch<true>(a, near, as_stream(stream));
+  return check_launch("gat_spmm_task");
 }

@@ -436,6 +436,36 @@ def gat_coef(rowptr, col, val, n_rows, nnz, al, ar, params, negative_slope=0.2):
     return coef[:nnz], den
 
 
+def gat_spmm(rowptr, col, val, n_rows, nnz, X, F, al, ar, params, plan, erow, X2=None,
+             B=None, norm_B=0, negative_slope=0.2, want_den=False, want_coef=False, out=None):
+    """Fused GAT aggregation (include/vqgnn.h §8b) on a task plan built from
+    this CSR's values: coefficients in the kernel, the ones column as the
+    per-row sum, rows < norm_B normalised.  -> (out [n_rows, F], den or None,
+    coef [nnz] (CSR order) or None)."""
+    require_gpu(X, "gat_spmm")
+    if not isinstance(plan, TaskPlan):
+        raise ValueError("gat_spmm: needs the CSR's task plan")
+    if (val.data_ptr() if val is not None else 0) != plan.val_ptr:
+        raise ValueError("gat_spmm: the task plan's records hold other values than val")
+    dev = X.device
+    L = lib()
+    if out is None:
+        out = torch.empty(n_rows, F, dtype=torch.float32, device=dev)
+    Bv = int(B) if X2 is not None else 0
+    n_cols = Bv + X2.shape[0] if X2 is not None else X.shape[0]
+    den = torch.empty(max(int(n_rows), 1), dtype=torch.float32, device=dev) if want_den else None
+    coef = torch.empty(max(int(nnz), 1), dtype=torch.float32, device=dev) if want_coef else None
+    ws = workspace(L.vqgnn_spmm_task_workspace(int(nnz), plan.K, F), dev)
+    check(L.vqgnn_gat_spmm_task(ptr(rowptr), int(n_rows), int(n_cols), int(nnz), Bv, ptr(X),
+                                _ld(X), ptr(X2), _ld(X2) if X2 is not None else 0, F, ptr(out),
+                                _ld(out), ptr(plan.plan), ptr(plan.records), plan.K,
+                                plan.n_jobs, plan.n_empty, ptr(erow), ptr(al), ptr(ar),
+                                ptr(params), float(negative_slope), int(norm_B), ptr(den),
+                                ptr(coef), ptr(ws), stream_ptr()), "gat_spmm")
+    return out, (den[:n_rows] if den is not None else None), \
+        (coef[:nnz] if coef is not None else None)
+
+
 def gat_normalize(out, B, F, den, eps=1e-16):
     check(lib().vqgnn_gat_normalize(ptr(out), _ld(out), int(B), int(F), ptr(den), float(eps),
                                     stream_ptr()), "gat_normalize")
