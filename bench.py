@@ -86,12 +86,22 @@ def main():
         else:
             dist.init_process_group("gloo")
         from vq_gnn_amd.dist import CodebookSync
-        comm = CodebookSync(count_group=dist.new_group(backend="gloo"))
+        cgroup = dist.new_group(backend="gloo")
+        comm = CodebookSync(count_group=cgroup)
 
     cfg = CONFIGS[args.config]
-    g = synthetic_graph(cfg["N"], cfg["parts"], cfg["edges"], seed=cfg.get("seed", 0))
-    _, _, batch = make_batch(cfg, rank=rank, graph=g)
-    B, n, nnz = batch.B, batch.n, batch.nnz
+    if cfg.get("device_build"):      # reddit-sized: graph and batch built on the device
+        from vq_gnn_amd.graph import make_batch_device
+        dgraph, (bidx, subset, adj) = make_batch_device(cfg, rank=rank, device=dev)
+        N_graph = dgraph.N
+        B, n, nnz = int(bidx.numel()), int(subset.numel()), adj.nnz()
+        del dgraph
+        batch = None
+    else:
+        g = synthetic_graph(cfg["N"], cfg["parts"], cfg["edges"], seed=cfg.get("seed", 0))
+        _, _, batch = make_batch(cfg, rank=rank, graph=g)
+        N_graph = g.N
+        B, n, nnz = batch.B, batch.n, batch.nnz
     F, M, D = cfg["F"], cfg["M"], 4
     nb = F // D
     W = 2 * D if args.semantics == "update" else D
@@ -99,7 +109,7 @@ def main():
     gen = torch.Generator().manual_seed(1)
     X = torch.randn(B, F, generator=gen)
     G = torch.randn(B, F, generator=torch.Generator().manual_seed(2)) * 1e-3
-    codes0 = torch.randint(0, M, (g.N, nb), dtype=torch.int16,
+    codes0 = torch.randint(0, M, (N_graph, nb), dtype=torch.int16,
                            generator=torch.Generator().manual_seed(5))
     torch.manual_seed(0)
     bank = VQBank(nb, M, D, warm_up_flag=True)
@@ -108,12 +118,13 @@ def main():
     bank = bank.to(dev)
     Xd, Gd = X.to(dev), G.to(dev)
     codes = codes0.to(dev)
-    bidx, subset, adj = batch_to_device(batch, dev)
+    if batch is not None:
+        bidx, subset, adj = batch_to_device(batch, dev)
     if comm is not None:
         bank.comm = comm
-        tot = comm.global_count(B)
-        comm.cache_count(B, tot)
-        bank.comm_max_B = comm.global_max(B)
+        # every rank's batch rows bounded once (the loader's batch bound): the
+        # timed steps then issue no host-side collective
+        comm.capacity = comm.global_max(B)
     gat = None
     if cfg["conv"] == "GAT":
         from vq_gnn_amd.convs_gat import OurGATConv
@@ -303,15 +314,8 @@ def main():
                     kernel=dominant["kernel"])
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and gat is None:
-        from oracle.cpu_baseline import layer_step_timer
-        threads = min(16, os.cpu_count() or 1)
-        t_cpu, nsteps = layer_step_timer(X, G, batch, codes0, M, D, threads,
-                                         max_seconds=args.cpu_seconds)
-        cpu = dict(value=nnz / t_cpu, unit="edges/s", cores=threads, kind="port",
-                   sample=f"full {args.config} layer step (update semantics, {nb} branches, "
-                          f"B={B}, nnz={nnz}), median of {nsteps} steps after 1 warm-up; "
-                          f"oracle/cpu_baseline.py, torch {torch.__version__} CPU")
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_leg(args, X, G, batch, bidx, subset, adj, codes0, M, D, B, nnz, nb, gat)
 
     if rank == 0:
         out = dict(
@@ -334,6 +338,53 @@ def main():
         print(json.dumps(out))
     if dist.is_initialized():
         dist.destroy_process_group()
+
+
+def cpu_leg(args, X, G, batch, bidx, subset, adj, codes0, M, D, B, nnz, nb, gat):
+    """cpu_baseline: the reference layer step (oracle/cpu_baseline.py) on the
+    host cores this process may use -- the affinity set, capped by
+    OMP_NUM_THREADS when the box sets it (its CPU share) -- and on one
+    thread, each on a bounded sample of the same workload scaled to edges/s
+    (about 10-30 s of CPU work in total)."""
+    from types import SimpleNamespace
+
+    from oracle.cpu_baseline import host_topology, layer_step_timer
+    if batch is None:          # device-built batch: the same CSR on the host
+        rp, cl, vl = adj.csr()
+        batch = SimpleNamespace(batch_idx=bidx.cpu().numpy(), subset=subset.cpu().numpy(),
+                                rowptr=rp.cpu().numpy(), col=cl.cpu().numpy(),
+                                val=vl.cpu().numpy(), n=int(subset.numel()))
+    host = host_topology()
+    threads = host["affinity"]
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        threads = min(threads, int(omp))
+    att = None
+    if gat is not None:
+        att = (gat.att_l.detach().cpu().view(-1).numpy(), gat.att_r.detach().cpu().view(-1).numpy())
+    # the headline config: the full step on `threads` threads (~4 s per step
+    # on 16); the other configs: a quarter of the branches and at most 8 M
+    # edges per step
+    full = args.config == "arxiv_gcn"
+    t_all, n_all, desc_all = layer_step_timer(
+        X, G, batch, codes0, M, D, threads, max_seconds=args.cpu_seconds,
+        branch_sample=None if full else max(2, nb // 4),
+        edge_sample=None if full else 8_000_000, gat=att)
+    # one thread: every 8th branch (at least 2) and 1/16 of the edges (at most
+    # 128 M edge-columns)
+    t_one, n_one, desc_one = layer_step_timer(
+        X, G, batch, codes0, M, D, 1, max_seconds=4.0, min_steps=5,
+        branch_sample=max(2, nb // 8),
+        edge_sample=max(min(nnz // 16, 128_000_000 // X.shape[1]), 1), gat=att)
+    torch.set_num_threads(threads)
+    sem = "update semantics" + (", GAT aggregation" if gat is not None else "")
+    return dict(value=nnz / t_all, unit="edges/s", cores=threads, kind="port",
+                sample=f"{args.config} layer step ({sem}, {nb} branches, B={B}, nnz={nnz}): "
+                       f"{desc_all}; median of {n_all} steps after 1 warm-up; "
+                       f"oracle/cpu_baseline.py, torch {torch.__version__} CPU",
+                value_1thread=nnz / t_one,
+                sample_1thread=f"{desc_one}; median of {n_one} steps",
+                host=host)
 
 
 if __name__ == "__main__":

@@ -83,7 +83,10 @@ int vqgnn_bn_stats(const float* X, int64_t ldx, const float* G, int64_t ldg,
  *                       CPU threads (its row chunks depend on them)
  *    vqgnn_bn_finalize takes fp64 sums, so its batch modes use FP64; arith
  *    only picks the form of the eval coefficients.
- *    count = rows over all ranks.  momenta and eps are the reference's
+ *    count = rows over all ranks; count <= 0 reads it from sums[4F] (a
+ *    double on the device: the multi-GPU path appends the local row count to
+ *    the sums, so the one all-reduce also yields the global count without a
+ *    host round trip).  momenta and eps are the reference's
  *    Python floats (double).
  *    coef[6][F]: alpha_f, beta_f, alpha_g, beta_g, shift_f, shift_g; every
  *    consumer normalises x as fma(x - shift, alpha, beta), which is ATen's

@@ -37,7 +37,10 @@ def main(out_dir):
             bank.init_branch(b)
         return bank.to(dev)
 
-    mine = torch.arange(rank, Bu, world)          # this rank's rows of the union batch
+    # uneven batches: rank 0 takes the first 1,800 rows of the union, rank 1
+    # the remaining 1,200 (no capacity: the ranks agree on max(B) per call)
+    cut = 1800
+    mine = torch.arange(0, cut) if rank == 0 else torch.arange(cut, Bu)
     bank = fresh_bank()
     bank.comm = CodebookSync(count_group=dist.new_group(backend="gloo"))
     codes = codes0.to(dev)
@@ -55,8 +58,23 @@ def main(out_dir):
         rc = codes0.to(dev)
         Xu, Gu, nu = X.to(dev), G.to(dev), node.to(dev)
         ref.feature_update(Xu, 0, nb, True, codes=rc, batch_idx=nu)
+        emb_pre = ref.emb.clone()
         ref.update(Xu, Gu, 0, nb, True, codes=rc, batch_idx=nu)
         torch.cuda.synchronize()
+        # fp64 distances of the update (vq.py:223-236 on the union batch's
+        # statistics) to classify any index mismatch as a near-tie or not
+        x64, g64 = X.double(), G.double()
+        zx = (x64 - x64.mean(0)) / torch.sqrt(x64.var(0, unbiased=False) + 1e-5)
+        zg = (g64 - g64.mean(0)) / torch.sqrt(g64.var(0, unbiased=False) + 1e-24)
+        e64 = emb_pre.double().cpu()
+        dists = []
+        for b in range(nb):
+            z = torch.cat([zx[:, b * D:(b + 1) * D], zg[:, b * D:(b + 1) * D]], 1)
+            e = e64[b]
+            dists.append(((z * z).sum(1, keepdim=True) + (e * e).sum(1)[None] - 2 * z @ e.T)
+                         .float().numpy())
+        res["ref_dist"] = np.stack(dists)
+        res["node"] = node.numpy()
         for k in ("emb", "emb_out", "ema_w", "cs", "rm_f", "rv_f", "rm_g", "rv_g"):
             res["ref_" + k] = getattr(ref, k).cpu().numpy()
         res["ref_codes"] = rc.cpu().numpy()
@@ -70,6 +88,21 @@ def main(out_dir):
     sync.start_codes_exchange(ids, loc.contiguous(), c2, max_B=24, M=M).wait()
     torch.cuda.synchronize()
     res["dup_codes"] = c2.cpu().numpy()
+    # two exchanges of the same shape in flight on one CodebookSync (two
+    # layers' banks): the second start lands the first before reusing the
+    # shared wire buffers, so each codes array gets its own records
+    ca = torch.zeros(N, nb, dtype=torch.int16, device=dev)
+    cb = torch.zeros(N, nb, dtype=torch.int16, device=dev)
+    ids = (torch.arange(12) * 2 + rank).to(dev)
+    la = ((torch.arange(12, device=dev)[:, None] + torch.arange(nb, device=dev)[None]) % M).to(torch.int16)
+    lb = ((la.to(torch.int32) + 5) % M).to(torch.int16)
+    pa = sync.start_codes_exchange(ids, la.contiguous(), ca, max_B=12, M=M)
+    pb = sync.start_codes_exchange(ids, lb.contiguous(), cb, max_B=12, M=M)
+    pb.wait()
+    pa.wait()
+    torch.cuda.synchronize()
+    res["two_a"] = ca[:24].cpu().numpy()
+    res["two_b"] = cb[:24].cpu().numpy()
     np.savez(os.path.join(out_dir, f"r{rank}.npz"), **res)
     dist.barrier()
     dist.destroy_process_group()

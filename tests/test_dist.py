@@ -27,6 +27,40 @@ def _worker(rank, world, port, out_dir):
     res = {}
     res["count"] = sync.global_count(B)
     res["max"] = sync.global_max(B)
+    # per-rank batch sizes that change between calls: without a capacity,
+    # every call agrees on this call's max(B)
+    res["max_seq"] = np.array([sync.rows_per_rank(b) for b in ([5, 2, 9], [3, 7, 1])[rank]])
+    # the update path's BatchNorm all-reduce carries the row count: [4F + 1]
+    # fp64 sums with B last (bn_stats(with_count=True))
+    for b in ([5, 2, 9], [3, 7, 1])[rank]:
+        flat = torch.zeros(4 * 2 + 1, dtype=torch.float64)
+        flat[:8] = torch.arange(8, dtype=torch.float64) * (rank + 1)
+        flat[8] = b
+        sync.allreduce_stats_(flat, b)
+        res.setdefault("counts_seq", []).append(float(flat[8]))
+    res["counts_seq"] = np.array(res["counts_seq"])
+    # with a capacity the update path issues no host-side collective
+    capped = CodebookSync(count_group=sync.count_group, capacity=9)
+    real = dist.all_reduce
+
+    def no_host_collective(t, *a, **k):
+        if t.dtype == torch.int64 and t.numel() == 1:
+            raise AssertionError("host collective on the capped update path")
+        return real(t, *a, **k)
+
+    dist.all_reduce = no_host_collective
+    try:
+        flat = torch.zeros(9, dtype=torch.float64)
+        flat[8] = B
+        res["capped_bound"] = capped.allreduce_stats_(flat, B)
+        res["capped_count"] = float(flat[8])
+        try:
+            capped.rows_per_rank(10)
+            res["over"] = 0
+        except ValueError:
+            res["over"] = 1
+    finally:
+        dist.all_reduce = real
     # BN sums (fp64) and EMA statistic (int64) all-reduce
     sums = torch.arange(8, dtype=torch.float64).view(4, 2) * (rank + 1)
     sync.allreduce_(sums)
@@ -57,6 +91,10 @@ def test_codebook_sync_gloo_world2(tmp_path):
     r = [np.load(tmp_path / f"r{k}.npz") for k in range(2)]
     for k in range(2):
         assert int(r[k]["count"]) == 8 and int(r[k]["max"]) == 5
+        np.testing.assert_array_equal(r[k]["max_seq"], [5, 7, 9])
+        np.testing.assert_array_equal(r[k]["counts_seq"], [8.0, 9.0, 10.0])
+        assert int(r[k]["capped_bound"]) == 9 and float(r[k]["capped_count"]) == 8.0
+        assert int(r[k]["over"]) == 1
         np.testing.assert_array_equal(r[k]["sums"], np.arange(8).reshape(4, 2) * 3.0)
         st = r[k]["stats"]
         assert st[0, 0, 0, 0] == 3 and st[0, 1, 2, 4] == 3 * (1 << 40)

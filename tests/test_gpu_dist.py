@@ -8,6 +8,9 @@ import sys
 
 import numpy as np
 import pytest
+import torch
+
+from helpers import tie_aware_mismatch
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -31,9 +34,19 @@ def test_two_ranks_match_union_batch(tmp_path):
     # replicas are bit-identical (identical finalize on exact int64 statistics)
     for k in ("emb", "emb_out", "ema_w", "cs", "rm_f", "rv_f", "rm_g", "rv_g", "codes"):
         np.testing.assert_array_equal(r0[k], r1[k])
-    # and equal the single-process union batch: codes (tie-aware), state
-    mism = int((r0["codes"] != r0["ref_codes"]).sum())
-    assert mism <= 2, f"{mism} code mismatches vs the union batch"
+    # and equal the single-process union batch: codes bit-exact except rows
+    # within 1e-5 of a tie under the fp64 distances (the multi-rank BN sums
+    # are added in another order, so a coefficient may move by an ulp)
+    node = r0["node"]
+    other = np.setdiff1d(np.arange(r0["codes"].shape[0]), node)
+    np.testing.assert_array_equal(r0["codes"][other], r0["ref_codes"][other])
+    n_mis = n_bad = 0
+    for b in range(r0["codes"].shape[1]):
+        m, bad = tie_aware_mismatch(torch.from_numpy(r0["codes"][node, b].astype(np.int64)),
+                                    torch.from_numpy(r0["ref_codes"][node, b].astype(np.int64)),
+                                    torch.from_numpy(r0["ref_dist"][b]))
+        n_mis, n_bad = n_mis + m, n_bad + bad
+    assert n_bad == 0, f"{n_bad} of {n_mis} code mismatches are not near-ties"
     for k in ("rm_f", "rv_f", "rm_g", "rv_g"):
         np.testing.assert_allclose(r0[k], r0["ref_" + k], rtol=1e-6, atol=1e-7)
     for k in ("emb", "emb_out", "ema_w", "cs"):
@@ -46,3 +59,27 @@ def test_two_ranks_match_union_batch(tmp_path):
     for rk in range(2):
         own = (np.arange(10, 20)[:, None] + 7 * (rk + 1) + np.arange(nb)[None]) % M
         np.testing.assert_array_equal(r0["dup_codes"][100 + 10 * rk:110 + 10 * rk], own)
+    # two in-flight exchanges on shared wire buffers keep their own records
+    for r in (r0, r1):
+        ids = np.arange(24)
+        loc = (ids // 2)[:, None] + np.arange(nb)[None]
+        np.testing.assert_array_equal(r["two_a"], loc % M)
+        np.testing.assert_array_equal(r["two_b"], (loc % M + 5) % M)
+
+
+def test_rccl_world1_deferred_update(tmp_path):
+    """The RCCL path itself (one GPU per box: a world of one): asynchronous
+    EMA all-reduce + code all_gather with work queued behind them give the
+    same state, bit for bit, as the single-process bank -- with a capacity
+    (no host collective) and without one."""
+    env = dict(os.environ)
+    env["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "tests", "dist_nccl_worker.py"), str(tmp_path)]
+    p = subprocess.run(cmd, env=env, cwd=ROOT, timeout=300, capture_output=True, text=True)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    r = np.load(tmp_path / "nccl.npz")
+    for tag in ("cap", "nocap"):
+        for k in ("emb", "emb_out", "ema_w", "cs", "rm_f", "rv_f", "rm_g", "rv_g", "codes"):
+            np.testing.assert_array_equal(r[f"{tag}_{k}"], r["ref_" + k], err_msg=f"{tag} {k}")

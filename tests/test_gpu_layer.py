@@ -164,6 +164,86 @@ def test_opt_in_backward_vq_update_moves_codebooks():
     assert model.convs[1]._bank.bn_inited[0]
 
 
+def test_opt_in_backward_vq_update_vs_oracle():
+    """SURVEY §8(f)2 (v1 hook semantics, vq_gnn_v1/models.py:71-125, batched
+    over branches): the update run from the aggregation's backward equals
+    vq_ref.update(X_B[:, branch], dOut[:B, branch]) per branch -- indices
+    bit-exact (scattered into c_indices), BatchNorm state bit-exact, EMA state
+    within 1e-5 -- and once the gradient halves of the codebooks have moved,
+    info_backward (vq_gnn_v2/models.py:198) equals the oracle's
+    sum(A[B:] @ x_input * grad_first_order) within 1e-5 of its magnitude."""
+    torch.manual_seed(5)
+    g, b = _small_batch("GCN", seed=5)
+    F_in, F_out, M, D = 32, 16, 64, 4
+    nb = F_in // D
+    layer = _layer(F_in, F_out, M, g.N, "GCN", vq_update_in_backward=True).to(DEV).train()
+    x = torch.randn(b.B, F_in)
+    xd = x.to(DEV)
+    batch_A = graph.batch_to_device(b, DEV)
+    layer(xd, batch_A, 1.0, False)                 # init pass (feature_update)
+    for blk in layer.gnn_block:
+        blk.inited = True
+    bank = layer._bank
+    states = []
+    for i in range(nb):
+        st = vq_ref.new_state(M, D, warm_up=True)
+        for k, src in (("embedding", bank.emb), ("ema_w", bank.ema_w),
+                       ("embedding_output", bank.emb_out), ("ema_cluster_size", bank.cs),
+                       ("rm_f", bank.rm_f), ("rv_f", bank.rv_f), ("rm_g", bank.rm_g),
+                       ("rv_g", bank.rv_g)):
+            st[k] = src[i].detach().cpu().clone()
+        st["bn_inited"] = bank.bn_inited[i]
+        states.append(st)
+    captured = {}
+    orig = layer._backward_vq_update
+
+    def spy(x_det, grad_B, bidx):
+        captured["g"] = grad_B.detach().clone()
+        orig(x_det, grad_B, bidx)
+
+    layer._backward_vq_update = spy
+    xg = xd.clone().requires_grad_(True)
+    out, *_ = layer(xg, batch_A, 1.0, False)
+    R = torch.randn(b.B, F_out, device=DEV)
+    (out * R).sum().backward()
+    torch.cuda.synchronize()
+    gB = captured["g"].cpu()
+    assert gB.shape == (b.B, F_in) and gB.abs().max() > 0
+    codes = layer._codes.cpu()
+    bidx = torch.from_numpy(b.batch_idx)
+    for i in range(nb):
+        sl = slice(i * D, (i + 1) * D)
+        idx, _, _ = vq_ref.update(states[i], x[:, sl], gB[:, sl])
+        assert torch.equal(codes[bidx, i].long(), idx[:, 0]), f"branch {i}: index mismatch"
+        for k, mine in (("rm_f", bank.rm_f), ("rv_f", bank.rv_f), ("rm_g", bank.rm_g),
+                        ("rv_g", bank.rv_g)):
+            assert torch.equal(mine[i].cpu(), states[i][k]), f"branch {i} {k}"
+        for k, mine in (("embedding", bank.emb), ("embedding_output", bank.emb_out),
+                        ("ema_cluster_size", bank.cs), ("ema_w", bank.ema_w)):
+            a, r = mine[i].detach().cpu(), states[i][k]
+            scale = 1.0 + (r.abs().amax(dim=-1, keepdim=True) if r.dim() == 2 else r.abs())
+            err = ((a - r).abs() / scale).max().item()
+            assert err < 1e-5, f"branch {i} {k}: rel err {err:.2e}"
+    # the gradient halves moved: info_backward is live and matches the oracle
+    emb_out = bank.emb_out.detach().cpu()
+    assert emb_out[:, :, D:].abs().max() > 0
+    layer._backward_vq_update = orig
+    with torch.no_grad():
+        _, _, _, _, _, info_b, _ = layer(xd, batch_A, 0.5, False)
+    codes = layer._codes.cpu()
+    xin = conv_ref.gather_input(x, b.subset, b.B, codes.numpy(), emb_out.numpy(), D).double()
+    gfo = conv_ref.grad_first_order(b.subset, b.B, codes.numpy(), emb_out.numpy(), D).double()
+    rows = np.repeat(np.arange(b.n), np.diff(b.rowptr))
+    A = torch.sparse_coo_tensor(torch.stack([torch.from_numpy(rows), torch.from_numpy(b.col)]),
+                                torch.from_numpy(b.val).double(), (b.n, b.n))
+    agg = torch.sparse.mm(A, xin)[b.B:]
+    ref = float((agg * gfo * 0.5).sum())
+    mag = float((torch.sparse.mm(A.abs(), xin.abs())[b.B:]
+                 * gfo.abs() * 0.5).sum())
+    assert abs(float(info_b) - ref) <= 1e-5 * mag, (float(info_b), ref, mag)
+    assert abs(ref) > 0
+
+
 def test_layer_gat_forward_backward_vs_oracle():
     """conv_type='GAT' (models.py:93-97, :178-189): codebook gather, ones
     column, attention aggregation, normalisation of the batch rows, Linear."""
@@ -185,16 +265,30 @@ def test_layer_gat_forward_backward_vs_oracle():
     xin1 = np.concatenate([xin, np.ones((b.n, 1), np.float32)], 1)
     agg, _ = conv_ref.gat_forward(xin1, att_l.numpy(), att_r.numpy(), b.rowptr, b.col, b.val,
                                   B=b.B, normalize=True)
-    ref = agg[:b.B] @ lin_w.t() + lin_b
-    torch.testing.assert_close(out.detach().cpu(), ref, rtol=1e-4, atol=1e-4)
-    # backward vs fp64 autograd of the same chain
-    R = torch.randn(b.B, F_out)
-    (out * R.to(DEV)).sum().backward()
+    # fp64 chain and its magnitude bound: |got - ref64| <= 1e-5 * scale, with
+    # scale = (sum_e coef_e |x_j| / den) |W| + |b| (north_star: 1e-5 relative)
     x64 = x.double().requires_grad_(True)
     agg64 = conv_ref.gat_forward_fp64(x64, torch.from_numpy(xin[b.B:]), att_l.double(),
                                       att_r.double(), b.rowptr, b.col, b.val, b.B)
+    with torch.no_grad():
+        xin_abs = torch.from_numpy(np.abs(xin1)).double()
+        _, coef = conv_ref.gat_forward(xin1, att_l.numpy(), att_r.numpy(), b.rowptr, b.col,
+                                       b.val)
+        rows = np.repeat(np.arange(b.n), np.diff(b.rowptr))
+        Ac = torch.sparse_coo_tensor(torch.stack([torch.from_numpy(rows), torch.from_numpy(b.col)]),
+                                     coef.double(), (b.n, b.n))
+        aabs = torch.sparse.mm(Ac, xin_abs)[:b.B]
+        aabs = aabs[:, :-1] / (aabs[:, -1:] + 1e-16)
+        scale = aabs @ lin_w.double().abs().t() + lin_b.double().abs()
+        ref64 = agg64[:b.B] @ lin_w.double().t() + lin_b.double()
+        err = ((out.detach().cpu().double() - ref64).abs() / scale).max().item()
+    assert err < 1e-5, f"GAT layer output rel err {err:.2e}"
+    # backward vs fp64 autograd of the same chain, normwise within 1e-5
+    R = torch.randn(b.B, F_out)
+    (out * R.to(DEV)).sum().backward()
     ((agg64[:b.B] @ lin_w.double().t() + lin_b.double()) * R.double()).sum().backward()
-    np.testing.assert_allclose(xg.grad.cpu().numpy(), x64.grad.numpy(), rtol=2e-3, atol=2e-4)
+    gerr = ((xg.grad.cpu().double() - x64.grad).abs().max() / x64.grad.abs().max()).item()
+    assert gerr < 1e-5, f"GAT dX normwise rel err {gerr:.2e}"
     assert layer.conv.att_l.grad is not None and torch.isfinite(layer.conv.att_l.grad).all()
 
 

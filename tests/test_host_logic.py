@@ -176,3 +176,21 @@ def test_gat_oracle_known_answer():
         ref[rows[e]] += exp_coef[e] * x[col[e]].astype(np.float64)
     ref[:2, :2] /= ref[:2, 2:] + 1e-16
     np.testing.assert_allclose(out.numpy(), ref[:, :2], rtol=1e-6, atol=1e-7)
+
+
+def test_synthetic_graph_device_structure():
+    """graph.synthetic_graph_device (run here on the CPU device): symmetric,
+    no self edges, no duplicates, exactly the requested edge count, and about
+    intra_frac of the edges inside a cluster."""
+    from vq_gnn_amd.graph import synthetic_graph_device
+    g, cptr = synthetic_graph_device(5000, 10, 40000, seed=3, device="cpu")
+    rp, col = g.rowptr, g.col.long()
+    assert int(rp[-1]) == 80000 and g.N == 5000
+    row = torch.repeat_interleave(torch.arange(5000), rp[1:] - rp[:-1])
+    assert not bool((row == col).any())
+    key = row * 5000 + col
+    assert bool((key[1:] > key[:-1]).all())                 # sorted, no duplicates
+    assert torch.equal(torch.sort(col * 5000 + row).values, key)   # symmetric
+    cl = torch.searchsorted(cptr, torch.arange(5000), right=True) - 1
+    intra = float((cl[row] == cl[col]).double().mean())
+    assert 0.7 < intra < 0.85          # dedup drops more intra-cluster repeats

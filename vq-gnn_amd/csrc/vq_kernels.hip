@@ -311,6 +311,9 @@ __global__ void bn_finalize_kernel(const double* __restrict__ sums, int64_t n, i
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= F) return;
   const bool have = sums != nullptr;
+  // n <= 0: the row count travels in sums[4F] (multi-GPU: summed by the same
+  // all-reduce as the statistics, so no host round trip)
+  if (have && n <= 0) n = (int64_t)sums[4 * F];
   bn_emit(a, F, 0, c, have ? bn_from_sums(sums[c], sums[F + c], n) : BnCol{}, have, n);
   if (with_grad)
     bn_emit(a, F, 1, c, have ? bn_from_sums(sums[2 * F + c], sums[3 * F + c], n) : BnCol{},
@@ -1849,7 +1852,7 @@ extern "C" int vqgnn_bn_finalize(const double* sums, int64_t count, int32_t F, i
   VQGNN_REQUIRE(F > 0 && coef && rm_f && rv_f, "bn_finalize: bad arguments");
   VQGNN_REQUIRE(mode >= 0 && mode <= 3, "bn_finalize: mode must be 0..3");
   VQGNN_REQUIRE(arith_ok(arith_x) && arith_ok(arith_g), "bn_finalize: bad arithmetic code");
-  VQGNN_REQUIRE(mode == 0 || (sums && count > 0), "bn_finalize: sums/count required");
+  VQGNN_REQUIRE(mode == 0 || sums, "bn_finalize: sums required");
   VQGNN_REQUIRE(!with_grad || (rm_g && rv_g), "bn_finalize: grad running stats required");
   // batch statistics from fp64 sums follow the FP64 arithmetic; the eval
   // coefficients take the form of the requested path

@@ -23,41 +23,57 @@ from . import kernels
 
 
 class CodebookSync:
-    def __init__(self, group=None, count_group=None):
+    """capacity: an upper bound of every rank's batch rows B (e.g. the loader's
+    batch size, OurDataLoader.max_batch_rows()).  With it an update issues no
+    host-side collective: the global row count travels inside the BatchNorm
+    all-reduce (bn_stats(with_count=True)), the fixed-point shift of the EMA
+    statistic uses world * capacity as its row bound, and the code exchange
+    pads to capacity rows.  Without it every update first agrees on max(B)
+    with one blocking all-reduce (correct for any batch sizes, but a host
+    round trip per call)."""
+
+    def __init__(self, group=None, count_group=None, capacity=None):
         self.group = group
-        # row counts are host integers: summed over a CPU (gloo) group when
-        # given, so the device stream never syncs for them
+        # host-integer collectives (max B when no capacity is given) run over a
+        # CPU (gloo) group when given, so the device stream never syncs for them
         self.count_group = count_group
         self.world = dist.get_world_size(group)
-        self._count_cache = {}
+        self.capacity = None if capacity is None else int(capacity)
         self._wire = {}       # persistent code-exchange buffers per shape
+        self._inflight = {}   # buffer key -> the PendingWire still reading them
 
     def allreduce_(self, t: torch.Tensor, async_op: bool = False):
         """In-place sum over the ranks; async_op=True returns the work (its
         wait() orders the current stream after the collective)."""
         return dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=async_op)
 
+    def rows_per_rank(self, B: int) -> int:
+        """The per-rank row bound every rank agrees on: capacity, or max(B)
+        over the ranks (one blocking collective) when no capacity is set."""
+        if self.capacity is not None:
+            if B > self.capacity:
+                raise ValueError(f"batch of {B} rows exceeds CodebookSync capacity "
+                                 f"{self.capacity}")
+            return self.capacity
+        return self.global_max(B)
+
     def allreduce_stats_(self, sums: torch.Tensor, B: int) -> int:
-        """All-reduce the fp64 BatchNorm sums in place -> global row count."""
+        """All-reduce the fp64 BatchNorm sums in place ([4F + 1] with the row
+        count last: bn_finalize(count=0) reads the global count on the device)
+        -> the per-rank row bound (rows_per_rank)."""
         self.allreduce_(sums)
-        return self.global_count(B)
+        return self.rows_per_rank(B)
 
     def global_count(self, B: int) -> int:
-        if B in self._count_cache:
-            return self._count_cache[B]
+        """Sum of B over the ranks (a blocking host collective; not on the
+        update path, which carries the count in the BatchNorm all-reduce)."""
         t = torch.tensor([B], dtype=torch.int64)
         if self.count_group is not None:
             dist.all_reduce(t, group=self.count_group)
-            total = int(t.item())
-        else:
-            dev = t.to(_device_of(self.group))
-            dist.all_reduce(dev, group=self.group)
-            total = int(dev.item())
-        return total
-
-    def cache_count(self, B: int, total: int) -> None:
-        """Fixed batches (bench): remember the global count for this local B."""
-        self._count_cache[B] = total
+            return int(t.item())
+        dev = t.to(_device_of(self.group))
+        dist.all_reduce(dev, group=self.group)
+        return int(dev.item())
 
     @staticmethod
     def _wire_dtype(M):
@@ -104,13 +120,22 @@ class CodebookSync:
         B, nb = local.shape
         if max_B is None:
             max_B = self.global_max(B)
-        send, recv, winner = self._wire_buffers(max_B, nb, M, codes.shape[0], local.device)
+        key = (max_B, nb, M, codes.shape[0], str(local.device))
+        # an exchange still in flight on these buffers (another bank of the
+        # same shape) is landed first: its all_gather reads `send` and its
+        # scatter reads `recv`
+        prev = self._inflight.pop(key, None)
+        if prev is not None:
+            prev.wait()
+        send, recv, winner = self._wire_buffers(key)
         kernels.pack_codes(batch_idx, local, M, max_B, send, codes=codes)
         work = dist.all_gather_into_tensor(recv, send, group=self.group, async_op=True)
-        return PendingWire(work, recv, self.world * max_B, nb, M, winner, codes)
+        pend = PendingWire(work, recv, self.world * max_B, nb, M, winner, codes)
+        self._inflight[key] = pend
+        return pend
 
-    def _wire_buffers(self, max_B, nb, M, N, device):
-        key = (max_B, nb, M, N, str(device))
+    def _wire_buffers(self, key):
+        max_B, nb, M, N, device = key
         buf = self._wire.get(key)
         if buf is None:
             rec = kernels.codes_wire_record(nb, M)

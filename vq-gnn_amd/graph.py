@@ -82,6 +82,91 @@ def synthetic_graph(N, num_parts, num_undirected_edges, intra_frac=0.8, zipf_a=0
     return Graph(N, rowptr, c.astype(np.int64), cptr)
 
 
+def synthetic_graph_device(N, num_parts, num_undirected_edges, intra_frac=0.8, zipf_a=0.9,
+                           seed=0, device="cuda"):
+    """``synthetic_graph``'s generator with torch ops on the device: the same
+    distribution (contiguous clusters, intra_frac intra-cluster edges,
+    Zipf-weighted endpoints, no self edges, deduplicated, symmetrised) from
+    its own RNG stream, for reddit-sized graphs (57 M undirected edges) that
+    take minutes in numpy.  -> loader.DeviceGraph (no edge values) and the
+    cluster pointer."""
+    from .loader import DeviceGraph
+    dev = torch.device(device)
+    gen = torch.Generator(device=dev).manual_seed(seed)
+    i64 = dict(dtype=torch.int64, device=dev)
+    sizes = torch.full((num_parts,), N // num_parts, **i64)
+    sizes[: N % num_parts] += 1
+    cptr = torch.zeros(num_parts + 1, **i64)
+    cptr[1:] = torch.cumsum(sizes, 0)
+    cl = torch.repeat_interleave(torch.arange(num_parts, **i64), sizes)
+    # Zipf weight by a random rank inside each cluster
+    key = cl.double() + 0.5 * torch.rand(N, generator=gen, device=dev, dtype=torch.float64)
+    order = torch.argsort(key)
+    rank = torch.empty(N, **i64)
+    rank[order] = torch.arange(N, **i64) - cptr[cl[order]] + 1
+    cum = torch.cat([torch.zeros(1, dtype=torch.float64, device=dev),
+                     torch.cumsum(rank.double() ** (-zipf_a), 0)])
+
+    def sample_in(c, u):
+        lo, hi = cum[cptr[c]], cum[cptr[c + 1]]
+        idx = torch.searchsorted(cum, lo + u * (hi - lo), right=True) - 1
+        return torch.minimum(torch.maximum(idx, cptr[c]), cptr[c + 1] - 1)
+
+    target = int(num_undirected_edges)
+    keys = torch.empty(0, **i64)
+    want = target
+    while keys.numel() < target:
+        m = int(want * 1.3) + 1024
+        ca = cl[torch.randint(0, N, (m,), generator=gen, device=dev)]   # P(c) = size_c / N
+        intra = torch.rand(m, generator=gen, device=dev) < intra_frac
+        cb = torch.where(intra, ca, (ca + torch.randint(1, max(num_parts, 2), (m,), generator=gen,
+                                                        device=dev)) % num_parts)
+        a = sample_in(ca, torch.rand(m, generator=gen, device=dev, dtype=torch.float64))
+        b = sample_in(cb, torch.rand(m, generator=gen, device=dev, dtype=torch.float64))
+        keep = a != b
+        a, b = a[keep], b[keep]
+        keys = torch.unique(torch.cat([keys, torch.minimum(a, b) * N + torch.maximum(a, b)]))
+        del ca, intra, cb, a, b, keep
+        want = target - keys.numel()
+    if keys.numel() > target:
+        sel = torch.randperm(keys.numel(), generator=gen, device=dev)[:target]
+        keys = torch.sort(keys[sel]).values
+    u, v = keys // N, keys % N
+    del keys
+    k2 = torch.sort(torch.cat([u * N + v, v * N + u])).values
+    del u, v
+    r, c = k2 // N, k2 % N
+    del k2
+    rowptr = torch.zeros(N + 1, **i64)
+    rowptr[1:] = torch.cumsum(torch.bincount(r, minlength=N), 0)
+    g = DeviceGraph(rowptr, c.to(torch.int32), None, N, dev)
+    return g, cptr
+
+
+def make_batch_device(cfg: dict, rank: int = 0, device="cuda", graph=None):
+    """``make_batch`` built on the device (graph: synthetic_graph_device,
+    normalisation: vqgnn_norm_adj, batch: vqgnn_khop_subset/edges) for the
+    reddit-sized configs.  -> (normalised DeviceGraph, (batch_idx, subset,
+    CSR)); ``graph`` reuses a normalised DeviceGraph."""
+    from .preprocess import norm_adj_graph
+    dev = torch.device(device)
+    if graph is None:
+        g, cptr = synthetic_graph_device(cfg["N"], cfg["parts"], cfg["edges"],
+                                         seed=cfg.get("seed", 0), device=dev)
+        graph = norm_adj_graph(g, cfg["conv"], dev)
+        graph.cluster_ptr = cptr
+        del g
+    gen = torch.Generator(device=dev).manual_seed(3 + rank)
+    if "batch_clusters" in cfg:
+        cptr = graph.cluster_ptr.cpu()
+        perm = torch.randperm(cfg["parts"], generator=gen, device=dev).cpu()
+        node_idx = torch.cat([torch.arange(int(cptr[c]), int(cptr[c + 1]))
+                              for c in perm[: cfg["batch_clusters"]].tolist()]).to(dev)
+    else:
+        node_idx = torch.randperm(graph.N, generator=gen, device=dev)[: cfg["batch_nodes"]]
+    return graph, graph.batch(node_idx)
+
+
 def norm_adj(g: Graph, conv_type: str):
     """vq_gnn_v2/utils/misc.py:14-34.  Returns (rowptr, col, val) of the
     normalised full-graph adjacency (float32 values as torch_sparse keeps)."""
@@ -182,8 +267,14 @@ CONFIGS = {
                       batch_clusters=40, seed=0),
     "ppi_sage": dict(N=44_906, parts=1, edges=615_000, F=256, M=4096, conv="SAGE",
                      batch_nodes=30_000, seed=0),
+    # reddit (README.md:75): 602 input features zero-padded to 604 = 151
+    # branches of D = 4 in layer 1 (vq_gnn_v2/utils/misc.py:212-216), hidden
+    # 128 after it; built on the device
+    # (make_batch_device: 57.3 M undirected edges take minutes in numpy)
     "reddit_gcn": dict(N=232_965, parts=50, edges=57_300_000, F=128, M=1024, conv="GCN",
-                       batch_nodes=10_000, seed=0),
+                       batch_nodes=10_000, seed=0, device_build=True),
+    "reddit_gcn_l1": dict(N=232_965, parts=50, edges=57_300_000, F=604, M=1024, conv="GCN",
+                          batch_nodes=10_000, seed=0, device_build=True),
 }
 
 

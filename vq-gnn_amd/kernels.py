@@ -32,18 +32,25 @@ def bn_arith_of(t: torch.Tensor, D: int) -> int:
     return BN_CONTIG if (_ld(t) == D or t.shape[0] <= 1) else BN_STRIDED
 
 
-def bn_stats(X: torch.Tensor, G: torch.Tensor | None, F: int) -> torch.Tensor:
-    """fp64 column sums [4, F]: sum x, sum x^2, sum g, sum g^2 (vq.py:162/223)."""
+def bn_stats(X: torch.Tensor, G: torch.Tensor | None, F: int,
+             with_count: bool = False) -> torch.Tensor:
+    """fp64 column sums [4, F]: sum x, sum x^2, sum g, sum g^2 (vq.py:162/223).
+    with_count: a flat [4F + 1] buffer whose last element is the row count B
+    (summed with the statistics by the multi-GPU all-reduce; bn_finalize with
+    count=0 reads it on the device)."""
     require_gpu(X, "bn_stats")
     B = X.shape[0]
     L = lib()
     ws = workspace(L.vqgnn_bn_stats_workspace(B, F), X.device)
-    sums = torch.empty(4, F, dtype=torch.float64, device=X.device)
+    flat = torch.empty(4 * F + int(with_count), dtype=torch.float64, device=X.device)
+    sums = flat[:4 * F].view(4, F)
     if G is None:
         sums[2:].zero_()
+    if with_count:
+        flat[4 * F:].fill_(float(B))
     check(L.vqgnn_bn_stats(ptr(X), _ld(X), ptr(G), _ld(G) if G is not None else 0, B, F,
                            int(G is not None), ptr(sums), ptr(ws), stream_ptr()), "bn_stats")
-    return sums
+    return flat if with_count else sums
 
 
 def _coef(F, with_grad, dev):
@@ -306,6 +313,9 @@ def spmm(rowptr, col, val, n_rows, nnz, X, F, X2=None, B=None, out=None, plan=No
     """out[i] = sum_e val[e] * xin[col[e]]; xin = X rows (< B), X2 rows (>= B).
     Every column index must be < the rows of xin (X rows, or B + X2 rows)."""
     require_gpu(X, "spmm")
+    if rowptr.dtype != torch.int32 or (col is not None and col.dtype != torch.int32):
+        raise TypeError("spmm: rowptr / col must be int32 device arrays (CSR.rowptr / CSR.col; "
+                        "CSR.csr() returns int64 copies)")
     dev = X.device
     if out is None:
         out = torch.empty(n_rows, F, dtype=torch.float32, device=dev)

@@ -81,7 +81,6 @@ class VQBank(nn.Module):
         # optional list: (start, end) HIP events around every assign launch
         # (bench.py times vq_assign_kernel alone with it); None = off
         self.assign_events = None
-        self.comm_max_B = None
         # multi-GPU: codes of the other ranks' batches arrive asynchronously
         # (dist.PendingCodes); sync_codes() lands them
         self._pending_codes = None
@@ -139,11 +138,11 @@ class VQBank(nn.Module):
         if p is not None:
             p.wait()
 
-    def _exchange_codes(self, batch_idx, local, codes):
+    def _exchange_codes(self, batch_idx, local, codes, max_B):
         """Own codes now (scattered by the pack kernel), everyone's
         asynchronously (landed by sync_codes)."""
         self._pending_codes = self.comm.start_codes_exchange(batch_idx, local, codes,
-                                                             self.comm_max_B, self.M)
+                                                             max_B, self.M)
 
     def _slab(self, W, b0, nbr):
         """Zeroed statistic slab [1, nbr, M, W+1] for branches [b0, b0+nbr)."""
@@ -203,10 +202,11 @@ class VQBank(nn.Module):
                                                    0.0, self.rm_f[sl], self.rv_f[sl],
                                                    nbt_f=self.nbt_f[sl], D=D, arith_x=ax,
                                                    ref_threads=self._threads())
-        elif training:
-            sums = kernels.bn_stats(X, None, F)
-            count = comm.allreduce_stats_(sums, B)
-            coef, _ = kernels.bn_finalize(sums, count, F, False, BN_TRAIN, 0.1, 1e-5, 0.0, 0.0,
+        elif training:         # multi-GPU: the global count rides in the sums
+            sums = kernels.bn_stats(X, None, F, with_count=True)
+            max_B = comm.allreduce_stats_(sums, B)
+            count = comm.world * max_B      # row bound of the fixed-point shift
+            coef, _ = kernels.bn_finalize(sums, 0, F, False, BN_TRAIN, 0.1, 1e-5, 0.0, 0.0,
                                           0.0, self.rm_f[sl], self.rv_f[sl], nbt_f=self.nbt_f[sl],
                                           D=D)
         else:
@@ -228,7 +228,7 @@ class VQBank(nn.Module):
             stats = kernels.vq_ema_reduce(stats)
             comm.allreduce_(stats)
             if local is not None:
-                self._exchange_codes(batch_idx, local, codes)
+                self._exchange_codes(batch_idx, local, codes, max_B)
         if training:
             kernels.vq_ema_finalize(stats, D, D, self.decay, self.warm_up_flag, 1.0, self.epsilon,
                                     self.cs[sl], self.ema_w[sl], self.emb[sl], self.emb_out[sl],
@@ -286,10 +286,11 @@ class VQBank(nn.Module):
             coef, batch, _ = kernels.bn_stats_finalize(X, G, F, *bn_args, **bn_kw, arith_x=ax,
                                                        arith_g=ag,
                                                        ref_threads=self._threads())
-        else:
-            sums = kernels.bn_stats(X, G, F)
-            count = comm.allreduce_stats_(sums, B)
-            coef, batch = kernels.bn_finalize(sums, count, F, True, *bn_args, **bn_kw,
+        else:                  # multi-GPU: the global count rides in the sums
+            sums = kernels.bn_stats(X, G, F, with_count=True)
+            max_B = comm.allreduce_stats_(sums, B)
+            count = comm.world * max_B      # row bound of the fixed-point shift
+            coef, batch = kernels.bn_finalize(sums, 0, F, True, *bn_args, **bn_kw,
                                               arith_x=ax_eval, arith_g=ag_eval)
         for b in range(b0, b0 + nbr):
             self.bn_inited[b] = True
@@ -313,12 +314,12 @@ class VQBank(nn.Module):
             stats = kernels.vq_ema_reduce(stats)
             if defer:
                 if local is not None:      # codes first: the all-reduce is waited on later
-                    self._exchange_codes(batch_idx, local, codes)
+                    self._exchange_codes(batch_idx, local, codes, max_B)
                 work = comm.allreduce_(stats, async_op=True)
             else:
                 comm.allreduce_(stats)
                 if local is not None:
-                    self._exchange_codes(batch_idx, local, codes)
+                    self._exchange_codes(batch_idx, local, codes, max_B)
         if training:
             fin_args = (stats, D, 2 * D, self.decay, self.warm_up_flag, scale, self.epsilon,
                         self.cs[sl], self.ema_w[sl], self.emb[sl], self.emb_out[sl],
