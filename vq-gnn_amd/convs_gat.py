@@ -22,6 +22,7 @@ gradient, and the x_in^T d alpha reductions.
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 from torch import nn
@@ -49,7 +50,10 @@ class GATFunction(torch.autograd.Function):
         F = x.shape[1]
         xc = x.contiguous()
         al, ar, params = kernels.gat_alpha(xc, att_l, att_r, F, X2=x_first, B=B, ones=ones)
-        plan = adj.plan(F, B=B if x_first is not None else None)
+        # the fused attention path runs on the task plan (coefficients computed
+        # per edge record), also for dense-block adjacencies
+        plan = adj.plan(F, B=B if x_first is not None else None,
+                        kind=None if os.environ.get("VQGNN_SPMM") == "chunk" else "task")
         if isinstance(plan, kernels.TaskPlan):
             # fused: coefficients, ones-column sums and the normalisation in the
             # aggregation kernel; coef / den kept only when a backward follows

@@ -132,6 +132,19 @@ class CSR:
         import os
         from . import kernels
         mode = kind or os.environ.get("VQGNN_SPMM", "task")
+        if mode == "tile" and os.environ.get("VQGNN_SPMM_PAIR", "0") != "1":
+            # opt-in: the dense blocks through LDS tiles, the
+            # sparse remainder through the task kernel; measured no faster
+            # than the task kernel alone on the reddit batch, whose sparse
+            # remainder (41 % of the edges) is bound by MALL row reads
+            p = self._plans.get("tile", False)
+            if p is False:
+                p = kernels.spmm_tile_plan(self.rowptr, self.col, self.value, self._sizes[0],
+                                           self._sizes[1], self._host_nnz, min_fraction=0.0)
+                self._plans["tile"] = p
+            if p is not None and (n_rows is None or int(n_rows) == self._sizes[0]):
+                return p
+            mode = "task"
         if mode == "task" and os.environ.get("VQGNN_SPMM_PAIR", "0") != "1":
             p = self._plans.get("task")
             if p is None:
