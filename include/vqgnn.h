@@ -487,6 +487,20 @@ int vqgnn_coo_to_csr(const int64_t* row, const int64_t* col, const float* val, i
                      int64_t n_rows, int64_t n_cols, int32_t* out_rowptr, int32_t* out_col,
                      float* out_val, int64_t* status, void* workspace, vqgnn_stream_t stream);
 
+/* 9b. Uniform random walks for the 'edge', 'rw' and 'cont' samplers
+ *     (dataloader.py:70-90: SparseTensor.random_walk -> torch_cluster
+ *     random_walk with p = q = 1; torch_cluster is not vendored in the
+ *     reference).  out [n_start][walk_length + 1] int64: out[i][0] =
+ *     start[i]; step l moves from v to col[rowptr[v] + (int64)(u * (float)
+ *     deg(v))] with u in [0, 1), or stays on v when deg(v) = 0 — torch_cluster's
+ *     uniform step.  u = (splitmix64(splitmix64(seed ^ splitmix64(i)) + l)
+ *     >> 40) * 2^-24: deterministic per seed, not torch's CPU RNG stream
+ *     (oracle/subgraph_ref.walk_uniforms restates it).  status (device
+ *     int64) = VQGNN_KHOP_OUT_OF_RANGE if a start node is outside [0, N). */
+int vqgnn_random_walk(const int64_t* rowptr, const int32_t* col, int64_t N, const int64_t* start,
+                      int64_t n_start, int32_t walk_length, uint64_t seed, int64_t* out,
+                      int64_t* status, vqgnn_stream_t stream);
+
 /* ------------------------------------------------------------------------ *
  * 10. Full-graph preprocessing.  Graph CSR as in §9:
  *     rowptr int64 [N+1], col int32 (sorted within rows), val fp32 or NULL

@@ -69,3 +69,55 @@ def sparse_tensor_csr(row, col, value, n_rows, n_cols):
     rowptr = torch.zeros(int(n_rows) + 1, dtype=torch.int64)
     rowptr[1:] = torch.cumsum(torch.bincount(row, minlength=int(n_rows)), 0)
     return rowptr, col, value
+
+
+# ---------------------------------------------------------------------------
+# Random walks of the 'edge' / 'rw' / 'cont' samplers (dataloader.py:70-90):
+# SparseTensor.random_walk -> torch_cluster random_walk (p = q = 1).
+# torch_cluster is a dependency the reference does not vendor; its uniform
+# step (rw_cpu.cpp) draws rand = torch.rand([n, walk_length]) and moves from
+# v to col[rowptr[v] + (int64)(rand * deg(v))], staying on v when deg(v) = 0.
+# The step uniforms here are the HIP kernel's counter-based stream
+# (include/vqgnn.h §9b), restated so the GPU walk is checked bit for bit;
+# the structure is pinned by known answers (tests/test_subgraph_oracle.py),
+# torch's RNG stream is not reproduced ("parity unpinned" for the draws).
+# ---------------------------------------------------------------------------
+_M64 = (1 << 64) - 1
+
+
+def walk_mix(z: int) -> int:
+    """splitmix64 finaliser (include/vqgnn.h §9b)."""
+    z = (z + 0x9E3779B97F4A7C15) & _M64
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & _M64
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & _M64
+    return z ^ (z >> 31)
+
+
+def walk_uniforms(seed: int, n: int, walk_length: int):
+    """u[i][l] in [0, 1) as float32: (mix(mix(seed ^ mix(i)) + l) >> 40) * 2^-24."""
+    import numpy as np
+    u = np.empty((n, walk_length), dtype=np.float32)
+    for i in range(n):
+        base = walk_mix((seed & _M64) ^ walk_mix(i))
+        for l in range(walk_length):
+            u[i, l] = np.float32((walk_mix((base + l) & _M64) >> 40) * 2.0 ** -24)
+    return u
+
+
+def random_walk(rowptr, col, start, walk_length, u):
+    """torch_cluster's uniform random walk given the step uniforms u [n, L]:
+    [n, L + 1] int64, out[:, 0] = start."""
+    import numpy as np
+    rowptr = np.asarray(rowptr, dtype=np.int64)
+    col = np.asarray(col, dtype=np.int64)
+    start = np.asarray(start, dtype=np.int64)
+    out = np.empty((start.shape[0], walk_length + 1), dtype=np.int64)
+    for i, v in enumerate(start):
+        out[i, 0] = v
+        for l in range(walk_length):
+            rs, re = rowptr[v], rowptr[v + 1]
+            if re > rs:
+                e = rs + int(np.float32(u[i, l]) * np.float32(re - rs))
+                v = col[min(e, re - 1)]
+            out[i, l + 1] = v
+    return out

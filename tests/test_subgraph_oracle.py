@@ -118,3 +118,27 @@ def test_oracle_edge_cases():
     rp, c, v = subgraph_ref.sparse_tensor_csr([1, 0, 1, 1], [2, 3, 0, 2], [1., 2., 3., 4.], 3, 4)
     assert rp.tolist() == [0, 1, 4, 4] and c.tolist() == [3, 0, 2, 2]
     assert v.tolist() == [2., 3., 1., 4.]
+
+
+# ---- random walks (torch_cluster's uniform step, dataloader.py:70-90) -------
+def test_random_walk_known_answers():
+    """deg 0 stays; a node with one neighbour always moves there; with k
+    neighbours u picks floor(u * k)."""
+    import numpy as np
+    # 0 -> {1}, 1 -> {2}, 2 -> {} (sink), 3 -> {0, 1, 2, 4}, 4 -> {3}
+    rowptr = np.array([0, 1, 2, 2, 6, 7])
+    col = np.array([1, 2, 0, 1, 2, 4, 3])
+    u = np.array([[0.0, 0.0, 0.0], [0.99, 0.5, 0.1], [0.3, 0.3, 0.3]], dtype=np.float32)
+    out = subgraph_ref.random_walk(rowptr, col, [0, 3, 2], 3, u)
+    np.testing.assert_array_equal(out[0], [0, 1, 2, 2])      # 0 -> 1 -> 2 -> sink stays
+    np.testing.assert_array_equal(out[1], [3, 4, 3, 0])      # floor(.99*4)=3 -> 4 -> 3 -> floor(.1*4)=0
+    np.testing.assert_array_equal(out[2], [2, 2, 2, 2])      # sink
+
+
+def test_walk_uniforms_range_and_spread():
+    import numpy as np
+    u = subgraph_ref.walk_uniforms(12345, 400, 5)
+    assert u.dtype == np.float32 and (u >= 0).all() and (u < 1).all()
+    assert abs(float(u.mean()) - 0.5) < 0.02
+    assert len(np.unique(u)) > 1990                        # no obvious repeats
+    assert not np.array_equal(subgraph_ref.walk_uniforms(1, 4, 3), subgraph_ref.walk_uniforms(2, 4, 3))

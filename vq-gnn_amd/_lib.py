@@ -164,6 +164,8 @@ SIGNATURES = {
                                     _i32, _c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p,
                                     _c_void_p, _c_void_p, _c_void_p, _c_void_p]),
     "vqgnn_coo_to_csr_workspace": (_size, [_i64, _i64, _i64]),
+    "vqgnn_random_walk": (ctypes.c_int, [_c_void_p, _c_void_p, _i64, _c_void_p, _i64, _i32,
+                                         ctypes.c_uint64, _c_void_p, _c_void_p, _c_void_p]),
     "vqgnn_coo_to_csr": (ctypes.c_int, [_c_void_p, _c_void_p, _c_void_p, _i64, _i64, _i64,
                                         _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
                                         _c_void_p]),

@@ -250,6 +250,47 @@ int bits_for(int64_t n) {
   return b;
 }
 
+// Uniform random walks (torch_cluster random_walk with p = q = 1, which
+// SparseTensor.random_walk calls for the 'edge' / 'rw' / 'cont' samplers,
+// dataloader.py:70-90): one thread per walk; step l draws u in [0, 1) and
+// moves to col[rowptr[v] + (int64)(u * (float)deg)], or stays on v when it
+// has no neighbour.  u is the top 24 bits of splitmix64(seed, walk, step)
+// scaled by 2^-24 (a float in [0, 1), like torch.rand).
+__device__ __forceinline__ unsigned long long walk_mix(unsigned long long z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__global__ void __launch_bounds__(kSgThreads)
+random_walk_kernel(const int64_t* __restrict__ rowptr, const int32_t* __restrict__ col, int64_t N,
+                   const int64_t* __restrict__ start, int64_t n_start, int walk_length,
+                   unsigned long long seed, long long* __restrict__ out,
+                   long long* __restrict__ status) {
+  const int64_t i = blockIdx.x * (int64_t)kSgThreads + threadIdx.x;
+  if (i >= n_start) return;
+  int64_t v = start[i];
+  long long* o = out + i * (walk_length + 1);
+  o[0] = v;
+  if (v < 0 || v >= N) {
+    *status = VQGNN_KHOP_OUT_OF_RANGE;
+    for (int l = 1; l <= walk_length; ++l) o[l] = v;
+    return;
+  }
+  const unsigned long long base = walk_mix(seed ^ walk_mix((unsigned long long)i));
+  for (int l = 0; l < walk_length; ++l) {
+    const int64_t rs = rowptr[v], re = rowptr[v + 1];
+    if (re > rs) {
+      const unsigned long long h = walk_mix(base + (unsigned long long)l);
+      const float u = (float)(h >> 40) * 5.9604644775390625e-08f;   // 2^-24
+      const int64_t e = rs + (int64_t)(u * (float)(re - rs));
+      v = col[e < re ? e : re - 1];
+    }
+    o[l + 1] = v;
+  }
+}
+
 }  // namespace
 
 }  // namespace vqgnn
@@ -451,4 +492,23 @@ extern "C" int vqgnn_coo_to_csr(const int64_t* row, const int64_t* col, const fl
   hipLaunchKernelGGL(coo_finish_kernel, grid, dim3(kSgThreads), 0, s, keys_out, perm, val, nnz,
                      n_rows, n_cols, out_rowptr, out_col, out_val);
   return check_launch("coo_to_csr");
+}
+
+extern "C" int vqgnn_random_walk(const int64_t* rowptr, const int32_t* col, int64_t N,
+                                 const int64_t* start, int64_t n_start, int32_t walk_length,
+                                 uint64_t seed, int64_t* out, int64_t* status,
+                                 vqgnn_stream_t stream) {
+  clear_error();
+  VQGNN_REQUIRE(rowptr && status && N >= 0 && n_start >= 0 && walk_length >= 0,
+                "random_walk: bad arguments");
+  VQGNN_REQUIRE(n_start == 0 || (start && out && col), "random_walk: null pointer");
+  hipStream_t s = as_stream(stream);
+  if (hipMemsetAsync(status, 0, sizeof(int64_t), s) != hipSuccess)
+    return check_launch("random_walk memset");
+  if (n_start > 0)
+    hipLaunchKernelGGL(random_walk_kernel, dim3((unsigned)((n_start + kSgThreads - 1) / kSgThreads)),
+                       dim3(kSgThreads), 0, s, rowptr, col, N, start, n_start, walk_length,
+                       (unsigned long long)seed, reinterpret_cast<long long*>(out),
+                       reinterpret_cast<long long*>(status));
+  return check_launch("random_walk");
 }

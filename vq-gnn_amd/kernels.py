@@ -595,6 +595,24 @@ def _khop_status(status: int) -> None:
         raise IndexError("k_hop_subgraph: node index out of range")
 
 
+def random_walk(rowptr, col, N, start, walk_length, seed):
+    """torch_cluster random_walk (p = q = 1) of every start node on the
+    device graph (rowptr int64 [N+1], col int32): [n_start, walk_length + 1]
+    int64 (include/vqgnn.h §9b; the step uniforms come from ``seed``)."""
+    require_gpu(rowptr, "random_walk")
+    dev = rowptr.device
+    start = start.to(device=dev, dtype=torch.int64).contiguous()
+    n = int(start.numel())
+    out = torch.empty(n, int(walk_length) + 1, dtype=torch.int64, device=dev)
+    status = torch.empty(1, dtype=torch.int64, device=dev)
+    check(lib().vqgnn_random_walk(ptr(rowptr), ptr(col), int(N), ptr(start), n, int(walk_length),
+                                  int(seed) & ((1 << 64) - 1), ptr(out), ptr(status),
+                                  stream_ptr()), "random_walk")
+    if int(status.item()) != 0:
+        raise IndexError("random_walk: start node outside [0, N)")
+    return out
+
+
 def khop_subgraph(rowptr, col, val, N, node_idx, num_hops=1, train_flag=True,
                   order=KHOP_ORDER_CSR):
     """_k_hop_subgraph (dataloader.py:98-148) of node_idx on the full graph

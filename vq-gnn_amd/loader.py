@@ -10,9 +10,11 @@ Mirrors the reference's batch pipeline with the arithmetic in HIP
 * ``prepare_batch_input`` = vq_gnn_v2/utils/misc.py:57-75: returns
   ``(x[batch_idx], (batch_idx, subset, adj)), (num_B, num_B_prime)`` with
   ``adj`` the batch CSR sorted by (row, col), built on the device.
-* ``OurDataLoader`` = vq_gnn_v2/dataloader.py:11-95 for the ``'node'`` and
-  ``'cluster'`` samplers (the random-walk samplers need torch_sparse's
-  ``random_walk`` and raise ``NotImplementedError``).
+* ``OurDataLoader`` = vq_gnn_v2/dataloader.py:11-95 with every sampler:
+  ``'node'``, ``'cluster'`` and the random-walk samplers ``'edge'``, ``'rw'``,
+  ``'cont'`` (SparseTensor.random_walk -> torch_cluster's uniform walk, here
+  ``vqgnn_random_walk`` with its own counter-based RNG seeded from torch's
+  generator; include/vqgnn.h §9b).
 
 Batches the loader yields carry their CSR (``SubgraphBatch.adj``), so
 ``prepare_batch_input`` does not rebuild it; the reference-order
@@ -156,9 +158,8 @@ class OurDataLoader(torch.utils.data.DataLoader):
     def __init__(self, data, cluster_indices, batch_size, gnn_type='GCN', sampler_type='node',
                  walk_length=None, recovery_flag=True, train_flag=True, cont_sliding_window=1,
                  device="cuda", **kwargs):
-        if sampler_type not in ('node', 'cluster'):
-            raise NotImplementedError(
-                f"sampler_type={sampler_type!r}: needs torch_sparse random_walk")
+        if sampler_type not in ('node', 'cluster', 'edge', 'rw', 'cont'):
+            raise ValueError('Sampler type not supported!')
         if kwargs.get("num_workers", 0):
             raise ValueError("the collate runs HIP kernels: num_workers must be 0")
         self.sampler_type, self.gnn_type = sampler_type, gnn_type
@@ -175,16 +176,52 @@ class OurDataLoader(torch.utils.data.DataLoader):
             super().__init__(cluster_indices, collate_fn=self.__collate_cluster__,
                              batch_size=batch_size, **kwargs)
         else:
+            # dataloader.py:40-46: seeds per batch so that the sampled batch
+            # holds about batch_size nodes
+            if sampler_type == 'edge':
+                self.batch_size = batch_size // 2
+            elif sampler_type == 'rw':
+                self.batch_size = batch_size // (self.walk_length + 1)
+            elif sampler_type == 'cont':
+                self.batch_size = batch_size // self.cont_sliding_window
             super().__init__(range(self.N), collate_fn=self.__collate__,
-                             batch_size=batch_size, **kwargs)
+                             batch_size=self.batch_size, **kwargs)
 
     def __collate_cluster__(self, batches):
         idx = torch.cat([torch.as_tensor(b) for b in batches], dim=0)
         return [(self._k_hop_subgraph(idx), idx)]
 
+    def _walk(self, start, walk_length):
+        """SparseTensor.random_walk(start, walk_length) on the device graph;
+        the seed is drawn from torch's default CPU generator (torch.manual_seed
+        makes a run reproducible, as torch.rand does for torch_cluster)."""
+        seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+        return kernels.random_walk(self.graph.rowptr, self.graph.col, self.N, start, walk_length,
+                                   seed)
+
     def __collate__(self, idx):
+        """dataloader.py:60-95: the sampler's node lists, then one
+        (_k_hop_subgraph, node_idx) per list."""
         idx = torch.tensor(idx)
-        return [(self._k_hop_subgraph(idx), idx)]
+        dev = self.graph.device
+        if self.sampler_type == 'node':
+            node_idx_list = [idx]
+        elif self.sampler_type == 'edge':                       # :70-71
+            node_idx_list = [self._walk(idx, 1).view(-1).unique()]
+        elif self.sampler_type == 'rw':                         # :73-74
+            node_idx_list = [self._walk(idx, self.walk_length).view(-1).unique()]
+        else:                                                   # 'cont', :76-88
+            node_idx = idx.to(dev)
+            node_idx_list = [node_idx]
+            for _ in range(self.walk_length):
+                node_idx = torch.cat([node_idx] * 3)
+                node_idx = self._walk(node_idx, 1)[:, 1].unique()[:self.batch_size]
+                node_idx_list.append(node_idx)
+            if self.cont_sliding_window > 1:
+                w = self.cont_sliding_window
+                node_idx_list = [torch.cat(node_idx_list[i:i + w]).unique()
+                                 for i in range(len(node_idx_list) - w + 1)]
+        return [(self._k_hop_subgraph(n), n) for n in node_idx_list]
 
     def _k_hop_subgraph(self, node_idx, num_hops=1, relabel_nodes=True):
         if not relabel_nodes:
