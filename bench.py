@@ -313,6 +313,23 @@ def main():
                     unit=dominant["unit"], frac=dominant["frac"], traffic=dominant["traffic"],
                     kernel=dominant["kernel"])
 
+    # measured device copy rate beside the 8 TB/s spec (a 1 GiB HBM -> HBM
+    # copy, read + write bytes), after the timed region
+    copy_peak = None
+    if rank == 0:
+        src = torch.empty(1 << 28, dtype=torch.float32, device=dev)
+        dst = torch.empty_like(src)
+        dst.copy_(src)
+        c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        c0.record()
+        for _ in range(5):
+            dst.copy_(src)
+        c1.record()
+        torch.cuda.synchronize()
+        copy_peak = 2 * src.numel() * 4 * 5 / (c0.elapsed_time(c1) * 1e-3) / 1e9
+        del src, dst
+    rl_spmm["measured_copy_gbs"] = copy_peak
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_leg(args, X, G, batch, bidx, subset, adj, codes0, M, D, B, nnz, nb, gat)

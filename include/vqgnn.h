@@ -436,6 +436,26 @@ int vqgnn_gat_spmm_task(const int32_t* rowptr, int32_t n_rows, int32_t n_cols, i
                         const float* params, float negative_slope, int32_t norm_B, float* den,
                         float* coef, void* workspace, vqgnn_stream_t stream);
 
+/* 8b. GAT backward, row-parallel (F % 4 == 0, rows 16-byte aligned):
+ *     vqgnn_gat_edge_grad_csr: the coefficient chain of vqgnn_gat_edge_grad
+ *       over a CSR (one wave per target row; d alpha_r and ds_row written
+ *       once per row, d alpha_l by atomics; dalpha_l must be zeroed).
+ *     vqgnn_gat_att_grad: d att_l / d att_r [F + ones] = x_in^T d alpha_l /
+ *       d alpha_r with x_in = [X (rows < B) ; X2 ; ones column if ones]
+ *       (the alpha = x_in . att of convs.py:189-190), fixed-order two-stage
+ *       reduction; workspace vqgnn_gat_att_grad_workspace(n, F, ones) bytes. */
+int vqgnn_gat_edge_grad_csr(const int32_t* rowptr, int32_t n_rows, const int32_t* col,
+                            const float* coef, const float* X, int64_t ldx, const float* X2,
+                            int64_t ldx2, int32_t B, int32_t F, const float* dy, int64_t lddy,
+                            const float* dden, const float* alpha_l, const float* alpha_r,
+                            const float* params, float negative_slope, float* dalpha_l,
+                            float* dalpha_r, float* ds_row, vqgnn_stream_t stream);
+size_t vqgnn_gat_att_grad_workspace(int32_t n, int32_t F, int32_t ones);
+int vqgnn_gat_att_grad(const float* X, int64_t ldx, const float* X2, int64_t ldx2, int32_t B,
+                       int32_t n, int32_t F, int32_t ones, const float* dalpha_l,
+                       const float* dalpha_r, float* datt_l, float* datt_r, void* workspace,
+                       vqgnn_stream_t stream);
+
 /* ------------------------------------------------------------------------ *
  * 9. Mini-batch construction on the device.
  *    Replaces OurDataLoader._k_hop_subgraph (dataloader.py:98-148; num_hops,

@@ -181,3 +181,38 @@ def test_gat_fused_kernel_matches_coefficient_path(F, monkeypatch):
     fast = conv.fused_forward(x, adj, xf, B)
     sc32 = torch.from_numpy(sc).to(DEV).float()
     assert ((fast - slow).abs() <= 2e-5 * sc32 + 1e-30).all()
+
+
+@pytest.mark.parametrize("F", [32, 128])
+def test_gat_row_parallel_backward_kernels(F):
+    """The row-parallel coefficient-chain backward equals the edge-parallel
+    kernel (same formula, other summation order: within 1e-5 of the column's
+    scale), and gat_att_grad equals x_in^T d alpha in fp64 within 1e-5."""
+    g, b = _batch(seed=7)
+    n, B = b.n, b.B
+    adj = CSR(torch.from_numpy(b.rowptr), torch.from_numpy(b.col), torch.from_numpy(b.val),
+              (n, n)).to(DEV)
+    torch.manual_seed(F)
+    x = torch.randn(B, F, device=DEV)
+    xf = torch.randn(n - B, F, device=DEV)
+    conv = _conv(F, 5).to(DEV)
+    al, ar, params = kernels.gat_alpha(x, conv.att_l.view(-1), conv.att_r.view(-1), F, X2=xf,
+                                       B=B, ones=True)
+    coef, den = kernels.gat_coef(adj.rowptr, adj.col, adj.value, n, adj.nnz(), al, ar, params)
+    dy = torch.randn(n, F, device=DEV)
+    dden = torch.randn(n, device=DEV)
+    old = kernels.gat_edge_grad(adj.rows(), adj.col, coef, adj.nnz(), x, F, dy, dden, al, ar,
+                                params, X2=xf, B=B)
+    new = kernels.gat_edge_grad_csr(adj.rowptr, adj.col, coef, n, x, F, dy, dden, al, ar, params,
+                                    X2=xf, B=B)
+    for a, c in zip(old, new):
+        scale = a.abs().max().item() + 1e-30
+        assert (a - c).abs().max().item() <= 1e-5 * scale
+    dal, dar = new[0], new[1]
+    gl, gr = kernels.gat_att_grad(x, F, dal, dar, X2=xf, B=B, ones=True)
+    xin = torch.cat([torch.cat([x, xf]).double(), torch.ones(n, 1, dtype=torch.float64,
+                                                            device=DEV)], 1)
+    for got, da in ((gl, dal), (gr, dar)):
+        ref = xin.t() @ da.double()
+        mag = xin.abs().t() @ da.double().abs()
+        assert ((got.double() - ref).abs() / (mag + 1e-30)).max().item() < 1e-5

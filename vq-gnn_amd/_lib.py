@@ -92,6 +92,15 @@ SIGNATURES = {
     "vqgnn_spmm_tile": (ctypes.c_int, [_i32, _i32, _i32, _c_void_p, _i64, _c_void_p, _i64, _i32,
                                        _c_void_p, _i64, _c_void_p, _i32, _c_void_p, _c_void_p,
                                        _c_void_p, _c_void_p]),
+    "vqgnn_gat_edge_grad_csr": (ctypes.c_int, [_c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p,
+                                               _i64, _c_void_p, _i64, _i32, _i32, _c_void_p,
+                                               _i64, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
+                                               _f32, _c_void_p, _c_void_p, _c_void_p,
+                                               _c_void_p]),
+    "vqgnn_gat_att_grad_workspace": (_size, [_i32, _i32, _i32]),
+    "vqgnn_gat_att_grad": (ctypes.c_int, [_c_void_p, _i64, _c_void_p, _i64, _i32, _i32, _i32,
+                                          _i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
+                                          _c_void_p, _c_void_p]),
     "vqgnn_gat_spmm_task": (ctypes.c_int, [_c_void_p, _i32, _i32, _i64, _i32, _c_void_p, _i64,
                                            _c_void_p, _i64, _i32, _c_void_p, _i64, _c_void_p,
                                            _c_void_p, _i32, _i32, _i32, _c_void_p, _c_void_p,

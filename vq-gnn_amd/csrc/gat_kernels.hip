@@ -193,9 +193,237 @@ gat_edge_grad_kernel(const int32_t* __restrict__ rows, const int32_t* __restrict
   atomicAdd(dsrow + i, -q * a);
 }
 
+// Row-parallel form of the coefficient-chain backward (CSR order, F % 4 == 0):
+// one wave per target row i, 4 groups of 16 lanes take every 4th edge of the
+// row; a group's lanes hold float4 pieces of the dot x_in[j] . dy[i] (the row
+// dy[i] stays in L1), reduced across the 16 lanes.  d alpha_l[j] by atomics
+// (j = source, scattered); d alpha_r[i] and ds_row[i] are the row's sums,
+// written once (no atomics, no zero-init needed for them).
+template <int P>   // float4 pieces of a row per lane: P * 16 * 4 >= F
+__global__ void __launch_bounds__(kGatThreads)
+gat_edge_grad_csr_kernel(const int32_t* __restrict__ rowptr, int n_rows,
+                         const int32_t* __restrict__ col, const float* __restrict__ coef,
+                         const float* __restrict__ X, int64_t ldx, const float* __restrict__ X2,
+                         int64_t ldx2, int B, int F, const float* __restrict__ dy, int64_t lddy,
+                         const float* __restrict__ dden, const float* __restrict__ al,
+                         const float* __restrict__ ar, const float* __restrict__ params,
+                         float slope, float* __restrict__ dal, float* __restrict__ dar,
+                         float* __restrict__ dsrow, int dbg) {
+  constexpr int U = 4;                    // edges per group and step (loads in flight)
+  const int i = (int)((blockIdx.x * (int64_t)kGatThreads + threadIdx.x) >> 6);
+  const int lane = threadIdx.x & 63, g = lane >> 4, l16 = lane & 15;
+  if (i >= n_rows) return;
+  const int rs = rowptr[i], re = rowptr[i + 1];
+  const int F4 = F >> 2;
+  const float s = params[2];
+  const float ari = ar[i] / s;
+  const float ddi = dden ? dden[i] : 0.f;
+  // the row's dy, held in registers for all its edges
+  const float4* g4 = reinterpret_cast<const float4*>(dy + (int64_t)i * lddy);
+  float4 gy[P];
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    const int c = l16 + 16 * p;
+    gy[p] = c < F4 ? g4[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  float acc_r = 0.f, acc_s = 0.f;
+  for (int e0 = rs + g; e0 < re; e0 += 4 * U) {
+    int jj[U];
+    bool ok[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = e0 + 4 * u;
+      ok[u] = e < re;
+      jj[u] = ok[u] ? col[e] : 0;
+    }
+    float dot[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const float4* x4 = reinterpret_cast<const float4*>(
+          jj[u] < B ? X + (int64_t)jj[u] * ldx : X2 + (int64_t)(jj[u] - B) * ldx2);
+      float d = 0.f;
+#pragma unroll
+      for (int p = 0; p < P; ++p) {
+        const int c = l16 + 16 * p;
+        if (ok[u] && c < F4) {
+          const float4 a = (dbg & 2) ? gy[p] : x4[c], b = gy[p];
+          d = fmaf(a.x, b.x, d);
+          d = fmaf(a.y, b.y, d);
+          d = fmaf(a.z, b.z, d);
+          d = fmaf(a.w, b.w, d);
+        }
+      }
+      dot[u] = d;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int o = 8; o > 0; o >>= 1) dot[u] += __shfl_xor(dot[u], o);
+    }
+    if (l16 == 0) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (!ok[u]) continue;
+        const int e = e0 + 4 * u;
+        const float a = al[jj[u]] / s + ari;
+        const float q = (dot[u] + ddi) * coef[e] * (a > 0.f ? 1.f : slope) / s;
+        if (dbg & 1) dal[i] = q; else atomicAdd(dal + jj[u], q);
+        acc_r += q;
+        acc_s += -q * a;
+      }
+    }
+  }
+  acc_r += __shfl_xor(acc_r, 16);
+  acc_s += __shfl_xor(acc_s, 16);
+  acc_r += __shfl_xor(acc_r, 32);
+  acc_s += __shfl_xor(acc_s, 32);
+  if (lane == 0) {
+    dar[i] = acc_r;
+    dsrow[i] = acc_s;
+  }
+}
+
+// d att = x_in^T d alpha for both attention vectors at once (x_in = [X ; X2 ;
+// ones]): block b sums rows [b*kAttRows, ...) — thread = (row phase, float4
+// column) — into partial[b][2][C] (fixed order), then gat_att_reduce_kernel
+// folds the partials in block order (deterministic).  C = F + ones.
+constexpr int kAttRows = 1024;
+__global__ void __launch_bounds__(kGatThreads)
+gat_att_partial_kernel(const float* __restrict__ X, int64_t ldx, const float* __restrict__ X2,
+                       int64_t ldx2, int B, int n, int F, int ones,
+                       const float* __restrict__ dal, const float* __restrict__ dar,
+                       float* __restrict__ partial) {
+  __shared__ float4 red_l[kGatThreads], red_r[kGatThreads];
+  __shared__ float red_s[2][kGatThreads];
+  const int F4 = F >> 2;
+  const int C = F + ones;
+  const int cols = F4 < kGatThreads ? F4 : kGatThreads;
+  const int phases = kGatThreads / cols;
+  const int tid = threadIdx.x;
+  const int ph = tid / cols, c4 = tid % cols;
+  const int r0 = blockIdx.x * kAttRows, r1 = min(n, r0 + kAttRows);
+  float* out = partial + (int64_t)blockIdx.x * 2 * C;
+  for (int cb = 0; cb < F4; cb += cols) {           // column blocks of `cols` float4
+    const int c = cb + c4;
+    float4 gl = make_float4(0.f, 0.f, 0.f, 0.f), gr = gl;
+    float sl = 0.f, sr = 0.f;
+    if (ph < phases && c < F4) {
+      for (int r = r0 + ph; r < r1; r += phases) {
+        const float4 x = reinterpret_cast<const float4*>(
+            r < B ? X + (int64_t)r * ldx : X2 + (int64_t)(r - B) * ldx2)[c];
+        const float a = dal[r], b = dar[r];
+        gl.x = fmaf(a, x.x, gl.x); gl.y = fmaf(a, x.y, gl.y);
+        gl.z = fmaf(a, x.z, gl.z); gl.w = fmaf(a, x.w, gl.w);
+        gr.x = fmaf(b, x.x, gr.x); gr.y = fmaf(b, x.y, gr.y);
+        gr.z = fmaf(b, x.z, gr.z); gr.w = fmaf(b, x.w, gr.w);
+        if (cb == 0 && c4 == 0) {
+          sl += a;
+          sr += b;
+        }
+      }
+    }
+    red_l[tid] = gl;
+    red_r[tid] = gr;
+    red_s[0][tid] = sl;
+    red_s[1][tid] = sr;
+    __syncthreads();
+    if (ph == 0 && c < F4) {
+      for (int p = 1; p < phases; ++p) {
+        const float4 u = red_l[p * cols + c4], v = red_r[p * cols + c4];
+        gl.x += u.x; gl.y += u.y; gl.z += u.z; gl.w += u.w;
+        gr.x += v.x; gr.y += v.y; gr.z += v.z; gr.w += v.w;
+      }
+      reinterpret_cast<float4*>(out)[c] = gl;
+      reinterpret_cast<float4*>(out + C)[c] = gr;
+    }
+    if (cb == 0 && tid == 0 && ones) {
+      float tl = 0.f, tr = 0.f;
+      for (int p = 0; p < phases; ++p) {
+        tl += red_s[0][p * cols];
+        tr += red_s[1][p * cols];
+      }
+      out[F] = tl;
+      out[C + F] = tr;
+    }
+    __syncthreads();
+  }
+}
+
+__global__ void gat_att_reduce_kernel(const float* __restrict__ partial, int nblocks, int C,
+                                      float* __restrict__ att_l, float* __restrict__ att_r) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= 2 * C) return;
+  float acc = 0.f;
+  for (int b = 0; b < nblocks; ++b) acc += partial[(int64_t)b * 2 * C + c];
+  if (c < C) att_l[c] = acc; else att_r[c - C] = acc;
+}
+
 }  // namespace vqgnn
 
 using namespace vqgnn;
+
+extern "C" int vqgnn_gat_edge_grad_csr(const int32_t* rowptr, int32_t n_rows, const int32_t* col,
+                                       const float* coef, const float* X, int64_t ldx,
+                                       const float* X2, int64_t ldx2, int32_t B, int32_t F,
+                                       const float* dy, int64_t lddy, const float* dden,
+                                       const float* alpha_l, const float* alpha_r,
+                                       const float* params, float negative_slope,
+                                       float* dalpha_l, float* dalpha_r, float* ds_row,
+                                       vqgnn_stream_t stream) {
+  clear_error();
+  VQGNN_REQUIRE(n_rows >= 0 && F > 0 && F % 4 == 0, "gat_edge_grad_csr: F=%d must be a multiple of 4", F);
+  if (n_rows == 0) return VQGNN_OK;
+  VQGNN_REQUIRE(rowptr && col && coef && X && dy && alpha_l && alpha_r && params && dalpha_l &&
+                    dalpha_r && ds_row,
+                "gat_edge_grad_csr: null pointer");
+  VQGNN_REQUIRE(((((uintptr_t)X | (uintptr_t)dy | (uintptr_t)X2) & 15) == 0 && ldx % 4 == 0 &&
+                 lddy % 4 == 0 && (!X2 || ldx2 % 4 == 0)),
+                "gat_edge_grad_csr: rows must be 16-byte aligned");
+  VQGNN_REQUIRE(F <= 4 * 16 * 8, "gat_edge_grad_csr: F=%d > 512", F);
+  const int64_t threads = (int64_t)n_rows * 64;
+  const dim3 grid((unsigned)((threads + kGatThreads - 1) / kGatThreads));
+  const int P = (F / 4 + 15) / 16;
+  const char* dbg_env = getenv("VQGNN_GAT_DBG");     // experiments: results invalid
+  const int dbg = dbg_env ? atoi(dbg_env) : 0;
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, grid, dim3(kGatThreads), 0, as_stream(stream), rowptr, n_rows, col,
+                       coef, X, ldx, X2, ldx2, B, F, dy, lddy, dden, alpha_l, alpha_r, params,
+                       negative_slope, dalpha_l, dalpha_r, ds_row, dbg);
+  };
+  if (P <= 1) go(gat_edge_grad_csr_kernel<1>);
+  else if (P <= 2) go(gat_edge_grad_csr_kernel<2>);
+  else if (P <= 4) go(gat_edge_grad_csr_kernel<4>);
+  else go(gat_edge_grad_csr_kernel<8>);
+  return check_launch("gat_edge_grad_csr");
+}
+
+extern "C" size_t vqgnn_gat_att_grad_workspace(int32_t n, int32_t F, int32_t ones) {
+  const int nb = (n + kAttRows - 1) / kAttRows;
+  return align_up((size_t)(nb > 0 ? nb : 1) * 2 * (F + (ones ? 1 : 0)) * sizeof(float), 256);
+}
+
+extern "C" int vqgnn_gat_att_grad(const float* X, int64_t ldx, const float* X2, int64_t ldx2,
+                                  int32_t B, int32_t n, int32_t F, int32_t ones,
+                                  const float* dalpha_l, const float* dalpha_r, float* datt_l,
+                                  float* datt_r, void* workspace, vqgnn_stream_t stream) {
+  clear_error();
+  VQGNN_REQUIRE(n > 0 && F > 0 && F % 4 == 0 && B >= 0 && B <= n,
+                "gat_att_grad: bad shape (n=%d B=%d F=%d)", n, B, F);
+  VQGNN_REQUIRE(X && dalpha_l && dalpha_r && datt_l && datt_r && workspace && (B == n || X2),
+                "gat_att_grad: null pointer");
+  VQGNN_REQUIRE(((((uintptr_t)X | (uintptr_t)X2) & 15) == 0 && ldx % 4 == 0 &&
+                 (!X2 || ldx2 % 4 == 0)),
+                "gat_att_grad: rows must be 16-byte aligned");
+  const int C = F + (ones ? 1 : 0);
+  const int nb = (n + kAttRows - 1) / kAttRows;
+  float* part = reinterpret_cast<float*>(workspace);
+  hipStream_t s = as_stream(stream);
+  hipLaunchKernelGGL(gat_att_partial_kernel, dim3(nb), dim3(kGatThreads), 0, s, X, ldx, X2, ldx2, B,
+                     n, F, ones ? 1 : 0, dalpha_l, dalpha_r, part);
+  hipLaunchKernelGGL(gat_att_reduce_kernel, dim3((2 * C + 255) / 256), dim3(256), 0, s, part, nb,
+                     C, datt_l, datt_r);
+  return check_launch("gat_att_grad");
+}
 
 extern "C" size_t vqgnn_gat_alpha_workspace(int32_t n) {
   const int rows_per_block = (kGatThreads / 64) * kGatRowsPerWave;

@@ -583,6 +583,40 @@ def gat_edge_grad(rows, col, coef, nnz, X, F, dy, dden, al, ar, params, X2=None,
     return dal, dar, dsr
 
 
+def gat_edge_grad_csr(rowptr, col, coef, n_rows, X, F, dy, dden, al, ar, params, X2=None,
+                      B=None, negative_slope=0.2):
+    """Row-parallel coefficient-chain backward over the CSR (include/vqgnn.h
+    §8b): -> (dalpha_l [n], dalpha_r [n], ds_row [n])."""
+    dev = X.device
+    n = al.shape[0]
+    dal = torch.zeros(n, dtype=torch.float32, device=dev)
+    dar = torch.zeros(n, dtype=torch.float32, device=dev)
+    dsr = torch.zeros(n, dtype=torch.float32, device=dev)
+    Bv = int(B) if X2 is not None else X.shape[0]
+    check(lib().vqgnn_gat_edge_grad_csr(ptr(rowptr), int(n_rows), ptr(col), ptr(coef), ptr(X),
+                                        _ld(X), ptr(X2), _ld(X2) if X2 is not None else 0, Bv,
+                                        int(F), ptr(dy), _ld(dy), ptr(dden), ptr(al), ptr(ar),
+                                        ptr(params), float(negative_slope), ptr(dal), ptr(dar),
+                                        ptr(dsr), stream_ptr()), "gat_edge_grad_csr")
+    return dal, dar, dsr
+
+
+def gat_att_grad(X, F, dal, dar, X2=None, B=None, ones=True):
+    """(x_in^T dal, x_in^T dar) [F + ones] with x_in = [X ; X2 ; 1] (§8b)."""
+    dev = X.device
+    n = dal.shape[0]
+    C = F + int(bool(ones))
+    Bv = int(B) if X2 is not None else X.shape[0]
+    gl = torch.empty(C, dtype=torch.float32, device=dev)
+    gr = torch.empty(C, dtype=torch.float32, device=dev)
+    L = lib()
+    ws = workspace(L.vqgnn_gat_att_grad_workspace(n, int(F), int(bool(ones))), dev)
+    check(L.vqgnn_gat_att_grad(ptr(X), _ld(X), ptr(X2), _ld(X2) if X2 is not None else 0, Bv, n,
+                               int(F), int(bool(ones)), ptr(dal), ptr(dar), ptr(gl), ptr(gr),
+                               ptr(ws), stream_ptr()), "gat_att_grad")
+    return gl, gr
+
+
 # ---- mini-batch construction (include/vqgnn.h §9) ----
 
 KHOP_ORDER_CSR, KHOP_ORDER_REF = 0, 1
