@@ -293,20 +293,10 @@ def main():
                    bytes_per_launch=spmm_bytes, ms_per_launch=spmm_ms,
                    traffic=pmc.get(agg_pmc))
     rl_spmm["frac"] = rl_spmm["achieved"] / rl_spmm["peak"]
-    # the filtered assign (vq_kernels.hip: D = 4, W in {4, 8}, codebook planes +
-    # fused accumulators within 160 KiB of LDS) is one timed span: the bf16
-    # filter kernel plus the exact kernel's pass over the undecided rows
-    mp = (M + 15) // 16 * 16 + 48
-    filt = (os.environ.get("VQGNN_ASSIGN_FILTER", "0") == "1" and D == 4 and W in (4, 8)
-            and (4 * mp * 16 + 4 * mp + 8 * 64 + 16 + 2048 * 4 + 7) // 8 * 8 + M * (W + 1) * 8
-            <= 160 * 1024)
-    vq_name = "vq_assign_filter_kernel+vq_assign_kernel(list)" if filt else "vq_assign_kernel"
-    rl_vq = dict(kernel=vq_name, bound="mfma",
+    rl_vq = dict(kernel="vq_assign_kernel", bound="mfma",
                  achieved=vq_flops / (assign_ms * 1e-3) / 1e12, peak=157.3, unit="TFLOP/s",
                  flops_per_launch=vq_flops, ms_per_launch=assign_ms,
-                 traffic=(pmc.get("vq_assign_filter_kernel", 0.0) + pmc.get("vq_assign_kernel", 0.0)
-                          if filt and "vq_assign_filter_kernel" in pmc
-                          else None if filt else pmc.get("vq_assign_kernel")))
+                 traffic=pmc.get("vq_assign_kernel"))
     rl_vq["frac"] = rl_vq["achieved"] / rl_vq["peak"]
     dominant = rl_spmm if spmm_ms >= assign_ms else rl_vq
     roofline = dict(bound=dominant["bound"], achieved=dominant["achieved"], peak=dominant["peak"],

@@ -436,20 +436,13 @@ int vqgnn_gat_spmm_task(const int32_t* rowptr, int32_t n_rows, int32_t n_cols, i
                         const float* params, float negative_slope, int32_t norm_B, float* den,
                         float* coef, void* workspace, vqgnn_stream_t stream);
 
-/* 8b. GAT backward, row-parallel (F % 4 == 0, rows 16-byte aligned):
- *     vqgnn_gat_edge_grad_csr: the coefficient chain of vqgnn_gat_edge_grad
- *       over a CSR (one wave per target row; d alpha_r and ds_row written
- *       once per row, d alpha_l by atomics; dalpha_l must be zeroed).
- *     vqgnn_gat_att_grad: d att_l / d att_r [F + ones] = x_in^T d alpha_l /
- *       d alpha_r with x_in = [X (rows < B) ; X2 ; ones column if ones]
- *       (the alpha = x_in . att of convs.py:189-190), fixed-order two-stage
- *       reduction; workspace vqgnn_gat_att_grad_workspace(n, F, ones) bytes. */
-int vqgnn_gat_edge_grad_csr(const int32_t* rowptr, int32_t n_rows, const int32_t* col,
-                            const float* coef, const float* X, int64_t ldx, const float* X2,
-                            int64_t ldx2, int32_t B, int32_t F, const float* dy, int64_t lddy,
-                            const float* dden, const float* alpha_l, const float* alpha_r,
-                            const float* params, float negative_slope, float* dalpha_l,
-                            float* dalpha_r, float* ds_row, vqgnn_stream_t stream);
+/* 8b. GAT backward helper: vqgnn_gat_att_grad: d att_l / d att_r [F + ones]
+ *       = x_in^T d alpha_l / d alpha_r with x_in = [X (rows < B) ; X2 ; ones
+ *       column if ones] (the alpha = x_in . att of convs.py:189-190), F % 4 ==
+ *       0, rows 16-byte aligned; fixed-order two-stage reduction; workspace
+ *       vqgnn_gat_att_grad_workspace(n, F, ones) bytes.
+ *     (vqgnn_gat_edge_grad runs 16 lanes per edge with coalesced row reads
+ *     when F % 4 == 0, F <= 512 and the rows are 16-byte aligned.)            */
 size_t vqgnn_gat_att_grad_workspace(int32_t n, int32_t F, int32_t ones);
 int vqgnn_gat_att_grad(const float* X, int64_t ldx, const float* X2, int64_t ldx2, int32_t B,
                        int32_t n, int32_t F, int32_t ones, const float* dalpha_l,
@@ -568,16 +561,6 @@ int vqgnn_partition(const int64_t* rowptr, const int32_t* col, int64_t N, int32_
  *     frees the events.                                                       */
 int vqgnn_assign_timing(int32_t enable);
 int32_t vqgnn_assign_timing_read(float* ms, int32_t cap);
-
-/* 5a'. Filtered assign (opt-in): for D = 4, W in {4, 8} and
- *     one LDS-resident codebook, vqgnn_vq_assign first scores every codeword
- *     with bf16-split MFMAs, resolves rows whose best and second-best scores
- *     are more than twice the error bound apart exactly among 4 candidates,
- *     and sends the remaining rows through the exact kernel (bit-identical
- *     outputs either way; with timing on, one event span covers both).
- *     mode 1 on, 0 off, -1 the VQGNN_ASSIGN_FILTER environment variable
- *     (default off).                                                          */
-void vqgnn_assign_filter(int32_t mode);
 
 /* 5b. Multi-GPU code exchange wire format (keeps every replica's c_indices
  *     identical; models.py:46/:63 across ranks).  A record per batch row:

@@ -1,4 +1,4 @@
-"""Time gat_edge_grad_csr variants (VQGNN_GAT_DBG) on the arxiv batch."""
+"""Time the GAT backward kernels (edge grad, att grad) on the arxiv batch."""
 import os
 import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -20,9 +20,8 @@ al, ar, params = kernels.gat_alpha(x, att_l, att_r, F, X2=xf, B=B, ones=True)
 coef, den = kernels.gat_coef(adj.rowptr, adj.col, adj.value, n, adj.nnz(), al, ar, params)
 dy = torch.randn(n, F, device=DEV)
 dden = torch.randn(n, device=DEV)
-for dbg in ("0", "1", "2", "3"):
-    os.environ["VQGNN_GAT_DBG"] = dbg
-    f = lambda: kernels.gat_edge_grad_csr(adj.rowptr, adj.col, coef, n, x, F, dy, dden, al, ar, params, X2=xf, B=B)  # noqa: E731
+for dbg in ("0",):
+    f = lambda: kernels.gat_edge_grad(adj.rows(), adj.col, coef, adj.nnz(), x, F, dy, dden, al, ar, params, X2=xf, B=B)  # noqa: E731
     f()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -33,10 +32,9 @@ for dbg in ("0", "1", "2", "3"):
     torch.cuda.synchronize()
     print(f"dbg={dbg}: {e0.elapsed_time(e1) / 5 * 1e3:.1f} us (incl. 3 zero-fills)", flush=True)
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-os.environ["VQGNN_GAT_DBG"] = "0"
 e0.record()
 for _ in range(5):
-    kernels.gat_edge_grad(adj.rows(), adj.col, coef, adj.nnz(), x, F, dy, dden, al, ar, params, X2=xf, B=B)
+    kernels.gat_att_grad(x, F, al, ar, X2=xf, B=B, ones=True)
 e1.record()
 torch.cuda.synchronize()
-print(f"edge-parallel: {e0.elapsed_time(e1) / 5 * 1e3:.1f} us", flush=True)
+print(f"att_grad: {e0.elapsed_time(e1) / 5 * 1e3:.1f} us", flush=True)

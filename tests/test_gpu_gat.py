@@ -183,11 +183,12 @@ def test_gat_fused_kernel_matches_coefficient_path(F, monkeypatch):
     assert ((fast - slow).abs() <= 2e-5 * sc32 + 1e-30).all()
 
 
-@pytest.mark.parametrize("F", [32, 128])
-def test_gat_row_parallel_backward_kernels(F):
-    """The row-parallel coefficient-chain backward equals the edge-parallel
-    kernel (same formula, other summation order: within 1e-5 of the column's
-    scale), and gat_att_grad equals x_in^T d alpha in fp64 within 1e-5."""
+@pytest.mark.parametrize("F", [32, 128, 36])
+def test_gat_edge_grad_and_att_grad_kernels(F):
+    """The coefficient-chain backward (16-lane group kernel for aligned F,
+    per-edge kernel otherwise) against an fp64 restatement of the chain
+    (within 1e-5 of the magnitude), and gat_att_grad = x_in^T d alpha in
+    fp64 within 1e-5."""
     g, b = _batch(seed=7)
     n, B = b.n, b.B
     adj = CSR(torch.from_numpy(b.rowptr), torch.from_numpy(b.col), torch.from_numpy(b.val),
@@ -201,18 +202,27 @@ def test_gat_row_parallel_backward_kernels(F):
     coef, den = kernels.gat_coef(adj.rowptr, adj.col, adj.value, n, adj.nnz(), al, ar, params)
     dy = torch.randn(n, F, device=DEV)
     dden = torch.randn(n, device=DEV)
-    old = kernels.gat_edge_grad(adj.rows(), adj.col, coef, adj.nnz(), x, F, dy, dden, al, ar,
-                                params, X2=xf, B=B)
-    new = kernels.gat_edge_grad_csr(adj.rowptr, adj.col, coef, n, x, F, dy, dden, al, ar, params,
-                                    X2=xf, B=B)
-    for a, c in zip(old, new):
-        scale = a.abs().max().item() + 1e-30
-        assert (a - c).abs().max().item() <= 1e-5 * scale
-    dal, dar = new[0], new[1]
+    dal, dar, dsr = kernels.gat_edge_grad(adj.rows(), adj.col, coef, adj.nnz(), x, F, dy, dden,
+                                          al, ar, params, X2=xf, B=B)
+    # fp64 chain: q_e = (x_in[j] . dy[i] + dden[i]) coef_e leaky'(a_e) / s
+    rows, cols = adj.rows().long(), adj.col.long()
+    xin = torch.cat([x, xf]).double()
+    s = params[2].double()
+    a = al.double()[cols] / s + ar.double()[rows] / s
+    dot = (xin[cols] * dy.double()[rows]).sum(1) + dden.double()[rows]
+    q = dot * coef.double() * torch.where(a > 0, 1.0, 0.2).double() / s
+    qa = (dot.abs() * coef.double() / s)
+    n_ = al.numel()
+    for got, idx, val, mag_v in ((dal, cols, q, qa), (dar, rows, q, qa),
+                                 (dsr, rows, -q * a, (qa * a.abs()))):
+        ref = torch.zeros(n_, dtype=torch.float64, device=DEV).index_add_(0, idx, val)
+        mag = torch.zeros(n_, dtype=torch.float64, device=DEV).index_add_(0, idx, mag_v)
+        assert ((got.double() - ref).abs() / (mag + 1e-30)).max().item() < 1e-5
+    if F % 4:
+        return
     gl, gr = kernels.gat_att_grad(x, F, dal, dar, X2=xf, B=B, ones=True)
-    xin = torch.cat([torch.cat([x, xf]).double(), torch.ones(n, 1, dtype=torch.float64,
-                                                            device=DEV)], 1)
+    xin1 = torch.cat([xin, torch.ones(n, 1, dtype=torch.float64, device=DEV)], 1)
     for got, da in ((gl, dal), (gr, dar)):
-        ref = xin.t() @ da.double()
-        mag = xin.abs().t() @ da.double().abs()
+        ref = xin1.t() @ da.double()
+        mag = xin1.abs().t() @ da.double().abs()
         assert ((got.double() - ref).abs() / (mag + 1e-30)).max().item() < 1e-5

@@ -92,11 +92,6 @@ SIGNATURES = {
     "vqgnn_spmm_tile": (ctypes.c_int, [_i32, _i32, _i32, _c_void_p, _i64, _c_void_p, _i64, _i32,
                                        _c_void_p, _i64, _c_void_p, _i32, _c_void_p, _c_void_p,
                                        _c_void_p, _c_void_p]),
-    "vqgnn_gat_edge_grad_csr": (ctypes.c_int, [_c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p,
-                                               _i64, _c_void_p, _i64, _i32, _i32, _c_void_p,
-                                               _i64, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
-                                               _f32, _c_void_p, _c_void_p, _c_void_p,
-                                               _c_void_p]),
     "vqgnn_gat_att_grad_workspace": (_size, [_i32, _i32, _i32]),
     "vqgnn_gat_att_grad": (ctypes.c_int, [_c_void_p, _i64, _c_void_p, _i64, _i32, _i32, _i32,
                                           _i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
@@ -158,7 +153,6 @@ SIGNATURES = {
     # §5a measurement
     "vqgnn_assign_timing": (ctypes.c_int, [_i32]),
     "vqgnn_assign_timing_read": (_i32, [_c_void_p, _i32]),
-    "vqgnn_assign_filter": (None, [_i32]),
     # §5b multi-GPU code exchange
     "vqgnn_codes_wire_record": (_i32, [_i32, _i32]),
     "vqgnn_pack_codes": (ctypes.c_int, [_c_void_p, _i32, _c_void_p, _i32, _i32, _i32, _c_void_p,

@@ -103,16 +103,10 @@ class GATFunction(torch.autograd.Function):
             dy = dz
         if ctx.hook is not None:
             ctx.hook(dy[:B])
-        # coefficient chain -> d alpha_l, d alpha_r, d s (row-parallel over the
-        # CSR when the rows are float4-aligned; the edge-parallel kernel else)
-        if F % 4 == 0 and F <= 512:
-            dal, dar, dsr = kernels.gat_edge_grad_csr(adj.rowptr, adj.col, coef, adj.size(0), xc,
-                                                      F, dy, dden, al, ar, params, X2=x_first,
-                                                      B=B, negative_slope=ctx.slope)
-        else:
-            dal, dar, dsr = kernels.gat_edge_grad(adj.rows(), adj.col, coef, nnz, xc, F, dy,
-                                                  dden, al, ar, params, X2=x_first, B=B,
-                                                  negative_slope=ctx.slope)
+        # coefficient chain -> d alpha_l, d alpha_r, d s
+        dal, dar, dsr = kernels.gat_edge_grad(adj.rows(), adj.col, coef, nnz, xc, F, dy, dden,
+                                              al, ar, params, X2=x_first, B=B,
+                                              negative_slope=ctx.slope)
         ds = dsr.sum()
         # s = sqrt(max_l^2+1) sqrt(max_r^2+1); torch.max spreads its gradient
         # evenly over tied maxima

@@ -193,93 +193,74 @@ gat_edge_grad_kernel(const int32_t* __restrict__ rows, const int32_t* __restrict
   atomicAdd(dsrow + i, -q * a);
 }
 
-// Row-parallel form of the coefficient-chain backward (CSR order, F % 4 == 0):
-// one wave per target row i, 4 groups of 16 lanes take every 4th edge of the
-// row; a group's lanes hold float4 pieces of the dot x_in[j] . dy[i] (the row
-// dy[i] stays in L1), reduced across the 16 lanes.  d alpha_l[j] by atomics
-// (j = source, scattered); d alpha_r[i] and ds_row[i] are the row's sums,
-// written once (no atomics, no zero-init needed for them).
-template <int P>   // float4 pieces of a row per lane: P * 16 * 4 >= F
+// Group form of the coefficient-chain backward (F % 4 == 0, rows 16-byte
+// aligned): a wave takes 16 consecutive edges, a group of 16 lanes 4 of them,
+// each lane float4 pieces of x_in[j] . dy[i] (coalesced 256-byte row reads;
+// the 4 edges' loads in flight together), reduced across the 16 lanes; lane 0
+// of the group applies the chain and the atomics as the per-edge kernel does.
+template <int P>   // float4 pieces per lane: P * 16 * 4 >= F
 __global__ void __launch_bounds__(kGatThreads)
-gat_edge_grad_csr_kernel(const int32_t* __restrict__ rowptr, int n_rows,
-                         const int32_t* __restrict__ col, const float* __restrict__ coef,
-                         const float* __restrict__ X, int64_t ldx, const float* __restrict__ X2,
-                         int64_t ldx2, int B, int F, const float* __restrict__ dy, int64_t lddy,
+gat_edge_grad_grp_kernel(const int32_t* __restrict__ rows, const int32_t* __restrict__ col,
+                         const float* __restrict__ coef, int nnz, const float* __restrict__ X,
+                         int64_t ldx, const float* __restrict__ X2, int64_t ldx2, int B, int F,
+                         const float* __restrict__ dy, int64_t lddy,
                          const float* __restrict__ dden, const float* __restrict__ al,
                          const float* __restrict__ ar, const float* __restrict__ params,
                          float slope, float* __restrict__ dal, float* __restrict__ dar,
-                         float* __restrict__ dsrow, int dbg) {
-  constexpr int U = 4;                    // edges per group and step (loads in flight)
-  const int i = (int)((blockIdx.x * (int64_t)kGatThreads + threadIdx.x) >> 6);
+                         float* __restrict__ dsrow) {
+  constexpr int U = 4;
+  const int64_t wave = (blockIdx.x * (int64_t)kGatThreads + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63, g = lane >> 4, l16 = lane & 15;
-  if (i >= n_rows) return;
-  const int rs = rowptr[i], re = rowptr[i + 1];
+  const int64_t e0 = wave * 16 + g * U;
+  if (wave * 16 >= nnz) return;
   const int F4 = F >> 2;
+  int ii[U], jj[U];
+  bool ok[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t e = e0 + u;
+    ok[u] = e < nnz;
+    ii[u] = ok[u] ? rows[e] : 0;
+    jj[u] = ok[u] ? col[e] : 0;
+  }
+  float dot[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const float4* x4 = reinterpret_cast<const float4*>(
+        jj[u] < B ? X + (int64_t)jj[u] * ldx : X2 + (int64_t)(jj[u] - B) * ldx2);
+    const float4* g4 = reinterpret_cast<const float4*>(dy + (int64_t)ii[u] * lddy);
+    float d = 0.f;
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+      const int c = l16 + 16 * p;
+      if (ok[u] && c < F4) {
+        const float4 a = x4[c], b = g4[c];
+        d = fmaf(a.x, b.x, d);
+        d = fmaf(a.y, b.y, d);
+        d = fmaf(a.z, b.z, d);
+        d = fmaf(a.w, b.w, d);
+      }
+    }
+    dot[u] = d;
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) dot[u] += __shfl_xor(dot[u], o);
+  }
+  if (l16 != 0) return;
   const float s = params[2];
-  const float ari = ar[i] / s;
-  const float ddi = dden ? dden[i] : 0.f;
-  // the row's dy, held in registers for all its edges
-  const float4* g4 = reinterpret_cast<const float4*>(dy + (int64_t)i * lddy);
-  float4 gy[P];
 #pragma unroll
-  for (int p = 0; p < P; ++p) {
-    const int c = l16 + 16 * p;
-    gy[p] = c < F4 ? g4[c] : make_float4(0.f, 0.f, 0.f, 0.f);
-  }
-  float acc_r = 0.f, acc_s = 0.f;
-  for (int e0 = rs + g; e0 < re; e0 += 4 * U) {
-    int jj[U];
-    bool ok[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int e = e0 + 4 * u;
-      ok[u] = e < re;
-      jj[u] = ok[u] ? col[e] : 0;
-    }
-    float dot[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const float4* x4 = reinterpret_cast<const float4*>(
-          jj[u] < B ? X + (int64_t)jj[u] * ldx : X2 + (int64_t)(jj[u] - B) * ldx2);
-      float d = 0.f;
-#pragma unroll
-      for (int p = 0; p < P; ++p) {
-        const int c = l16 + 16 * p;
-        if (ok[u] && c < F4) {
-          const float4 a = (dbg & 2) ? gy[p] : x4[c], b = gy[p];
-          d = fmaf(a.x, b.x, d);
-          d = fmaf(a.y, b.y, d);
-          d = fmaf(a.z, b.z, d);
-          d = fmaf(a.w, b.w, d);
-        }
-      }
-      dot[u] = d;
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-#pragma unroll
-      for (int o = 8; o > 0; o >>= 1) dot[u] += __shfl_xor(dot[u], o);
-    }
-    if (l16 == 0) {
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        if (!ok[u]) continue;
-        const int e = e0 + 4 * u;
-        const float a = al[jj[u]] / s + ari;
-        const float q = (dot[u] + ddi) * coef[e] * (a > 0.f ? 1.f : slope) / s;
-        if (dbg & 1) dal[i] = q; else atomicAdd(dal + jj[u], q);
-        acc_r += q;
-        acc_s += -q * a;
-      }
-    }
-  }
-  acc_r += __shfl_xor(acc_r, 16);
-  acc_s += __shfl_xor(acc_s, 16);
-  acc_r += __shfl_xor(acc_r, 32);
-  acc_s += __shfl_xor(acc_s, 32);
-  if (lane == 0) {
-    dar[i] = acc_r;
-    dsrow[i] = acc_s;
+  for (int u = 0; u < U; ++u) {
+    if (!ok[u]) continue;
+    const int i = ii[u], j = jj[u];
+    const float dcoef = dot[u] + (dden ? dden[i] : 0.f);
+    const float a = al[j] / s + ar[i] / s;
+    const float da = dcoef * coef[e0 + u] * (a > 0.f ? 1.f : slope);
+    const float q = da / s;
+    atomicAdd(dal + j, q);
+    atomicAdd(dar + i, q);
+    atomicAdd(dsrow + i, -q * a);
   }
 }
 
@@ -361,41 +342,6 @@ __global__ void gat_att_reduce_kernel(const float* __restrict__ partial, int nbl
 }  // namespace vqgnn
 
 using namespace vqgnn;
-
-extern "C" int vqgnn_gat_edge_grad_csr(const int32_t* rowptr, int32_t n_rows, const int32_t* col,
-                                       const float* coef, const float* X, int64_t ldx,
-                                       const float* X2, int64_t ldx2, int32_t B, int32_t F,
-                                       const float* dy, int64_t lddy, const float* dden,
-                                       const float* alpha_l, const float* alpha_r,
-                                       const float* params, float negative_slope,
-                                       float* dalpha_l, float* dalpha_r, float* ds_row,
-                                       vqgnn_stream_t stream) {
-  clear_error();
-  VQGNN_REQUIRE(n_rows >= 0 && F > 0 && F % 4 == 0, "gat_edge_grad_csr: F=%d must be a multiple of 4", F);
-  if (n_rows == 0) return VQGNN_OK;
-  VQGNN_REQUIRE(rowptr && col && coef && X && dy && alpha_l && alpha_r && params && dalpha_l &&
-                    dalpha_r && ds_row,
-                "gat_edge_grad_csr: null pointer");
-  VQGNN_REQUIRE(((((uintptr_t)X | (uintptr_t)dy | (uintptr_t)X2) & 15) == 0 && ldx % 4 == 0 &&
-                 lddy % 4 == 0 && (!X2 || ldx2 % 4 == 0)),
-                "gat_edge_grad_csr: rows must be 16-byte aligned");
-  VQGNN_REQUIRE(F <= 4 * 16 * 8, "gat_edge_grad_csr: F=%d > 512", F);
-  const int64_t threads = (int64_t)n_rows * 64;
-  const dim3 grid((unsigned)((threads + kGatThreads - 1) / kGatThreads));
-  const int P = (F / 4 + 15) / 16;
-  const char* dbg_env = getenv("VQGNN_GAT_DBG");     // experiments: results invalid
-  const int dbg = dbg_env ? atoi(dbg_env) : 0;
-  auto go = [&](auto kern) {
-    hipLaunchKernelGGL(kern, grid, dim3(kGatThreads), 0, as_stream(stream), rowptr, n_rows, col,
-                       coef, X, ldx, X2, ldx2, B, F, dy, lddy, dden, alpha_l, alpha_r, params,
-                       negative_slope, dalpha_l, dalpha_r, ds_row, dbg);
-  };
-  if (P <= 1) go(gat_edge_grad_csr_kernel<1>);
-  else if (P <= 2) go(gat_edge_grad_csr_kernel<2>);
-  else if (P <= 4) go(gat_edge_grad_csr_kernel<4>);
-  else go(gat_edge_grad_csr_kernel<8>);
-  return check_launch("gat_edge_grad_csr");
-}
 
 extern "C" size_t vqgnn_gat_att_grad_workspace(int32_t n, int32_t F, int32_t ones) {
   const int nb = (n + kAttRows - 1) / kAttRows;
@@ -498,9 +444,27 @@ extern "C" int vqgnn_gat_edge_grad(const int32_t* rows, const int32_t* col, cons
                                  ldx % 4 == 0 && lddy % 4 == 0 && (!X2 || ldx2 % 4 == 0)),
                 "gat_edge_grad: F%%4==0 needs 16-byte aligned rows");
   const int n = (int)nnz;
-  hipLaunchKernelGGL(gat_edge_grad_kernel, dim3((n + kGatThreads - 1) / kGatThreads),
-                     dim3(kGatThreads), 0, as_stream(stream), rows, col, coef, n, X, ldx, X2,
-                     ldx2, B, F, dy, lddy, dden, alpha_l, alpha_r, params, negative_slope,
-                     dalpha_l, dalpha_r, ds_row);
+  const bool grp = (F & 3) == 0 && F <= 512 &&
+                   ((((uintptr_t)X | (uintptr_t)dy | (uintptr_t)X2) & 15) == 0 && ldx % 4 == 0 &&
+                    lddy % 4 == 0 && (!X2 || ldx2 % 4 == 0));
+  if (grp) {   // 16 lanes per edge, coalesced row reads
+    const int64_t threads = ((int64_t)n + 15) / 16 * 64;
+    const dim3 grid((unsigned)((threads + kGatThreads - 1) / kGatThreads));
+    const int P = (F / 4 + 15) / 16;
+    auto go = [&](auto kern) {
+      hipLaunchKernelGGL(kern, grid, dim3(kGatThreads), 0, as_stream(stream), rows, col, coef, n,
+                         X, ldx, X2, ldx2, B, F, dy, lddy, dden, alpha_l, alpha_r, params,
+                         negative_slope, dalpha_l, dalpha_r, ds_row);
+    };
+    if (P <= 1) go(gat_edge_grad_grp_kernel<1>);
+    else if (P <= 2) go(gat_edge_grad_grp_kernel<2>);
+    else if (P <= 4) go(gat_edge_grad_grp_kernel<4>);
+    else go(gat_edge_grad_grp_kernel<8>);
+  } else {
+    hipLaunchKernelGGL(gat_edge_grad_kernel, dim3((n + kGatThreads - 1) / kGatThreads),
+                       dim3(kGatThreads), 0, as_stream(stream), rows, col, coef, n, X, ldx, X2,
+                       ldx2, B, F, dy, lddy, dden, alpha_l, alpha_r, params, negative_slope,
+                       dalpha_l, dalpha_r, ds_row);
+  }
   return check_launch("gat_edge_grad");
 }

@@ -576,8 +576,6 @@ constexpr size_t kLdsBudget = 160 * 1024;
 // codewords of LDS slack after each staged chunk: the sweep prefetches one
 // tile pair ahead without a bound check (staged as e = 0, |e|^2 = +inf)
 constexpr int kSweepSlack = 32;
-constexpr int kFilterSlack = 48;   // the filter sweep reads 64 codewords a step
-constexpr int kLocalList = 2048;   // undecided rows a filter workgroup lists in LDS
 
 struct AssignGeom {
   int parts;          // row parts per branch (= EMA partial slabs)
@@ -644,9 +642,7 @@ static int env_int_vq(const char* name, int dflt) {
 constexpr int kAsgWaves = 8;    // waves per workgroup
 constexpr int kAsgGroups = 2;   // 16-row groups per wave and iteration
 
-// LIST: the row-list pass behind the filtered path (rows rlist[b*B + i],
-// i < rcnt[b]); the default instantiation carries none of it
-template <int KC, bool FUSED, int WM, bool LIST = false>
+template <int KC, bool FUSED, int WM>
 __global__ void __launch_bounds__(kAsgWaves * 64)
 vq_assign_kernel(const float* __restrict__ X, int64_t ldx,
                  const float* __restrict__ Gr, int64_t ldg,
@@ -656,8 +652,7 @@ vq_assign_kernel(const float* __restrict__ X, int64_t ldx,
                  int64_t* __restrict__ idx_out, int16_t* __restrict__ codes, int64_t ldc,
                  const int64_t* __restrict__ batch_idx,
                  int* __restrict__ idx32, unsigned long long* __restrict__ partial,
-                 int rows_per_part, int chunk, int shift_f, int shift_g,
-                 const int* __restrict__ rlist, const int* __restrict__ rcnt, int m_sweep);
+                 int rows_per_part, int chunk, int shift_f, int shift_g, int m_sweep);
 
 // k-slot layout: 0 general (W < 4*KC, padded), 1 W == 4*KC == D (features),
 // 2 W == 4*KC == 2*D (features then grads)
@@ -813,7 +808,7 @@ __device__ __forceinline__ void stage_chunk(const float* __restrict__ E, int ldw
   }
 }
 
-template <int KC, bool FUSED, int WM, bool LIST>
+template <int KC, bool FUSED, int WM>
 __global__ void __launch_bounds__(kAsgWaves * 64)
 vq_assign_kernel(const float* __restrict__ X, int64_t ldx,
                  const float* __restrict__ Gr, int64_t ldg,
@@ -823,8 +818,7 @@ vq_assign_kernel(const float* __restrict__ X, int64_t ldx,
                  int64_t* __restrict__ idx_out, int16_t* __restrict__ codes, int64_t ldc,
                  const int64_t* __restrict__ batch_idx,
                  int* __restrict__ idx32, unsigned long long* __restrict__ partial,
-                 int rows_per_part, int chunk, int shift_f, int shift_g,
-                 const int* __restrict__ rlist, const int* __restrict__ rcnt, int m_sweep) {
+                 int rows_per_part, int chunk, int shift_f, int shift_g, int m_sweep) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int NG = kAsgGroups, WV = kAsgWaves, NT = WV * 64, K4 = 4 * KC;
   const int F = nb * D;
@@ -846,17 +840,7 @@ vq_assign_kernel(const float* __restrict__ X, int64_t ldx,
   const bool vec_rows = WM != 0 && (ldw & 3) == 0 && (emb_bstride & 3) == 0 &&
                         (reinterpret_cast<uintptr_t>(emb) & 15) == 0;
 
-  // rlist (the exact pass behind vq_assign_filter_kernel): this branch's rows
-  // are rlist[b*B + i], i < rcnt[b], at least 64 per part (the undecided
-  // rows are few and skewed across branches: the grid covers the worst
-  // branch, and parts past the count leave before staging the codebook)
-  int b_rows = B, rpp = rows_per_part;
-  if constexpr (LIST) {
-    b_rows = rcnt[b];
-    const int nparts = (int)gridDim.x / nb;
-    rpp = max((b_rows + nparts - 1) / nparts, 64);
-    if (part * rpp >= b_rows) return;   // whole workgroup: no barrier reached
-  }
+  const int b_rows = B, rpp = rows_per_part;
 
   if constexpr (FUSED) {
     for (int i = tid; i < M * (W + 1); i += NT) acc[i] = 0ull;
@@ -882,10 +866,6 @@ vq_assign_kernel(const float* __restrict__ X, int64_t ldx,
     sh[kc] = kval[kc] ? coef[(isg[kc] ? 5 * F : 4 * F) + c] : 0.f;
   }
 
-  auto act = [&](int r) {
-    if constexpr (LIST) return rlist[(int64_t)b * B + r];
-    else return r;
-  };
   const int part_begin = part * rpp;
   const int part_end = min(b_rows, part_begin + rpp);
   const int n_iters = part_end > part_begin ? (part_end - part_begin + NG * 16 * WV - 1) /
@@ -909,7 +889,7 @@ vq_assign_kernel(const float* __restrict__ X, int64_t ldx,
     const int row0 = part_begin + it * RPI + wave * RPW;
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
-      const int rowi = act(min(row0 + g * 16 + j, part_end - 1));
+      const int rowi = min(row0 + g * 16 + j, part_end - 1);
 #pragma unroll
       for (int kc = 0; kc < KC; ++kc) {
         float v = 0.f;
@@ -930,7 +910,7 @@ vq_assign_kernel(const float* __restrict__ X, int64_t ldx,
   int64_t nbi = -1;                       // batch_idx of this lane's output row
   auto load_bidx = [&](int it) {
     const int row = part_begin + it * RPI + wave * RPW + q * 16 + j;
-    return (codes && q < NG && row < part_end) ? batch_idx[act(row)] : (int64_t)-1;
+    return (codes && q < NG && row < part_end) ? batch_idx[row] : (int64_t)-1;
   };
   if (n_iters > 0) {
     load_rows(0, nxt);
@@ -1112,7 +1092,7 @@ vq_assign_kernel(const float* __restrict__ X, int64_t ldx,
     if (q < NG) {
       const int lrow = row0 + q * 16 + j;
       if (lrow < part_end) {
-        const int row = act(lrow);
+        const int row = lrow;
         const int m = pickn<NG>(bidx, q);
         if (idx_out) idx_out[(int64_t)b * B + row] = (int64_t)m;
         if (idx32) idx32[(int64_t)b * B + row] = m;
@@ -1135,431 +1115,6 @@ vq_assign_kernel(const float* __restrict__ X, int64_t ldx,
   }
 
   if constexpr (FUSED) {   // fold into the single zeroed slab: integer, exact, order-free
-    __syncthreads();
-    unsigned long long* out = partial + (int64_t)b * M * (W + 1);
-    for (int i = tid; i < M * (W + 1); i += NT)
-      if (acc[i]) atomicAdd(out + i, acc[i]);
-  }
-}
-
-// ---------------------------------------------------------------------------
-// 3b. Filtered assignment: bf16 MFMA scores + exact resolve, exact fallback
-//
-// The exact kernel above runs the distance contraction on the f32 MFMA, which
-// on gfx950 shares the FP32 VALU datapath (SQ_VALU_MFMA_COEXEC_CYCLES = 0):
-// 2 MFMAs (64 SIMD cycles) + 12 VALU per 16x16 tile and row group.  Here the
-// sweep scores every codeword with ONE v_mfma_f32_16x16x32_bf16 (16 cycles,
-// 8 of them blocking VALU issue) on a bf16 split of the operands:
-//   A (codeword m): [eh | el | eh | ee_h ee_m ee_l]     (e = eh + el + O(2^-18 e))
-//   B (row x):      [-2xh | -2xh | -2xl | 1 1 1]        (x = xh + xl + O(2^-18 x))
-//   score_m = ee_m - 2 (xh.eh + xh.el + xl.eh)  ~  ee_m - 2 x.e_m
-// and keeps per lane only the smallest and second-smallest score (v_med3 +
-// v_min per value) and the tile of the smallest.  Error bound (products of
-// bf16 are exact in f32; <= 32 f32 roundings in the MFMA; the reference's own
-// rounding of fl(fl(|x|^2 + |e|^2) - 2 dot)):
-//   |score_m + |x|^2 - d_m| <= 2^-14.5 sum_k |x_k e_mk| + 2^-19 (|e_m|^2 + |x|^2)
-// so with eps = 2^-13 sum_k |x_k| max_m|e_mk| + 2^-18 (max_m |e_m|^2 + |x|^2)
-// (a 2x margin) a row whose best score beats every other by more than 2 eps
-// has a unique exact argmin among the 4 codewords of the winning (tile,
-// lane): they are recomputed with the reference's exact operations and order
-// (as the exact kernel's resolve does) and the smallest wins.  Every other row
-// (near ties, exact ties, non-finite values: the test fails) is appended to a
-// per-branch list and assigned by the exact kernel in its row-list mode, which
-// also adds that row's EMA statistics: the result is bit-identical to the
-// exact kernel for every row.  One codebook chunk (M + slack fits the LDS).
-// ---------------------------------------------------------------------------
-typedef short bf16x8 __attribute__((ext_vector_type(8)));
-
-__device__ __forceinline__ unsigned short f2bf(float v) {   // round to nearest even
-  unsigned u = __float_as_uint(v);
-  u += 0x7FFFu + ((u >> 16) & 1u);
-  return (unsigned short)(u >> 16);
-}
-__device__ __forceinline__ float bf2f(unsigned short h) { return __uint_as_float((unsigned)h << 16); }
-// v rounded to bf16 (nearest even), kept as a float
-__device__ __forceinline__ float bf_round(float v) {
-  unsigned u = __float_as_uint(v);
-  u += 0x7FFFu + ((u >> 16) & 1u);
-  return __uint_as_float(u & 0xFFFF0000u);
-}
-
-// v_min_f32 a, b with an unused operand `after`: the asm depends on it, so it
-// is scheduled after the instruction producing `after`
-__device__ __forceinline__ float vmin_after(float a, float b, float after) {
-  float r;
-  asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b), "v"(after));
-  return r;
-}
-
-// LDS bytes of the filter kernel: 4 bf16 planes of 16 B per codeword, |e|^2,
-// the bound constants, the fused EMA accumulators
-static size_t filter_lds_bytes(int M, int W, bool fused) {
-  const int mp = (M + 15) / 16 * 16 + kFilterSlack;
-  size_t b = (size_t)4 * mp * 16 + (size_t)mp * 4 + kAsgWaves * 16 * 4 + 16 +
-             (size_t)kLocalList * 4;
-  if (fused) b = align_up(b, 8) + (size_t)M * (W + 1) * sizeof(unsigned long long);
-  return b;
-}
-
-template <int W, bool FUSED>
-__global__ void __launch_bounds__(kAsgWaves * 64)
-vq_assign_filter_kernel(const float* __restrict__ X, int64_t ldx,
-                        const float* __restrict__ Gr, int64_t ldg,
-                        int B, int nb, int D, int M,
-                        const float* __restrict__ coef, float grad_scale,
-                        const float* __restrict__ emb, int ldw, int64_t emb_bstride,
-                        int64_t* __restrict__ idx_out, int16_t* __restrict__ codes, int64_t ldc,
-                        const int64_t* __restrict__ batch_idx,
-                        unsigned long long* __restrict__ partial,
-                        int rows_per_part, int shift_f, int shift_g,
-                        int* __restrict__ rlist, int* __restrict__ rcnt, int m_sweep) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  constexpr int KC = W / 4, NG = kAsgGroups, WV = kAsgWaves, NT = WV * 64;
-  const int F = nb * D;
-  const int wg = xcd_remap(blockIdx.x, gridDim.x);
-  const int b = wg % nb;
-  const int part = wg / nb;
-  const int mp = (M + 15) / 16 * 16 + kFilterSlack;    // codewords per plane
-  char* fpl = reinterpret_cast<char*>(smem);             // [4][mp][16 B]
-  float* se = reinterpret_cast<float*>(fpl + (size_t)4 * mp * 16);   // [mp]
-  float* bnd = se + mp;              // [wave][16]: per-wave max|e_k| (W), max|e|^2
-  int* lcnt = reinterpret_cast<int*>(bnd + WV * 16);    // undecided rows listed here
-  int* llist = lcnt + 4;                                // [kLocalList]
-  unsigned long long* acc = reinterpret_cast<unsigned long long*>(
-      fpl + (((size_t)4 * mp * 16 + (size_t)mp * 4 + WV * 64 + 16 + (size_t)kLocalList * 4 + 7) /
-             8) * 8);
-  const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
-  const int q = lane >> 4, j = lane & 15;
-  const float* E = emb + (int64_t)b * emb_bstride;
-
-  if (tid == 0) *lcnt = 0;
-  if constexpr (FUSED) {
-    for (int i = tid; i < M * (W + 1); i += NT) acc[i] = 0ull;
-  }
-  __syncthreads();
-  // ---- staging: bf16 split planes, exact |e|^2 (reference order), bounds ----
-  // (bounds: per-thread maxima, then a per-wave shuffle reduction into LDS;
-  // LDS atomics here became 64-iteration readlane loops per wave)
-  float tb[W + 1];
-#pragma unroll
-  for (int k = 0; k <= W; ++k) tb[k] = 0.f;
-  for (int m = tid; m < mp; m += NT) {
-    float e[W];
-    const bool mv = m < M;
-#pragma unroll
-    for (int k = 0; k < W; ++k) e[k] = mv ? E[(int64_t)m * ldw + k] : 0.f;
-    float s2 = 0.f;
-#pragma unroll
-    for (int k = 0; k < W; ++k) s2 = (k == 0) ? __fmul_rn(e[k], e[k]) : __fadd_rn(s2, __fmul_rn(e[k], e[k]));
-    se[m] = mv ? s2 : INFINITY;
-    unsigned short sl[32];
-#pragma unroll
-    for (int k = 0; k < 32; ++k) sl[k] = 0;
-#pragma unroll
-    for (int k = 0; k < W; ++k) {
-      const unsigned short h = f2bf(e[k]);
-      const unsigned short l = f2bf(e[k] - bf2f(h));
-      sl[k] = h;
-      sl[W + k] = l;
-      sl[2 * W + k] = h;
-    }
-    if (mv) {
-      const unsigned short h1 = f2bf(s2);
-      const float r1 = s2 - bf2f(h1);
-      const unsigned short h2 = f2bf(r1);
-      sl[3 * W] = h1;
-      sl[3 * W + 1] = h2;
-      sl[3 * W + 2] = f2bf(r1 - bf2f(h2));
-#pragma unroll
-      for (int k = 0; k < W; ++k) tb[k] = fmaxf(tb[k], fabsf(e[k]));
-      tb[W] = fmaxf(tb[W], s2);
-    } else {
-      sl[3 * W] = 0x7F80;   // +inf: never the best score
-    }
-#pragma unroll
-    for (int pq = 0; pq < 4; ++pq) {
-      uint4 v;
-      v.x = (unsigned)sl[8 * pq] | ((unsigned)sl[8 * pq + 1] << 16);
-      v.y = (unsigned)sl[8 * pq + 2] | ((unsigned)sl[8 * pq + 3] << 16);
-      v.z = (unsigned)sl[8 * pq + 4] | ((unsigned)sl[8 * pq + 5] << 16);
-      v.w = (unsigned)sl[8 * pq + 6] | ((unsigned)sl[8 * pq + 7] << 16);
-      *reinterpret_cast<uint4*>(fpl + ((size_t)pq * mp + m) * 16) = v;
-    }
-  }
-#pragma unroll
-  for (int k = 0; k <= W; ++k) {
-    float v = tb[k];
-#pragma unroll
-    for (int sft = 32; sft >= 1; sft >>= 1) v = fmaxf(v, __shfl_xor(v, sft));
-    if (lane == 0) bnd[wave * 16 + k] = v;
-  }
-
-  // k-slot kc*4 + q of this lane: column, normalisation coefficients (as the
-  // exact kernel, WM == 2 for W = 8: features then gradients)
-  float al[KC], be[KC], sh[KC];
-  bool isg[KC];
-  int colx[KC];
-#pragma unroll
-  for (int kc = 0; kc < KC; ++kc) {
-    const int k = kc * 4 + q;
-    isg[kc] = W == 8 ? (kc >= 1) : false;
-    const int kk = isg[kc] ? k - D : k;
-    const int c = b * D + kk;
-    colx[kc] = c;
-    al[kc] = coef[(isg[kc] ? 2 * F : 0) + c];
-    be[kc] = coef[(isg[kc] ? 3 * F : F) + c];
-    sh[kc] = coef[(isg[kc] ? 5 * F : 4 * F) + c];
-  }
-  const int part_begin = part * rows_per_part;
-  const int part_end = min(B, part_begin + rows_per_part);
-  constexpr int RPW = 16 * NG, RPI = WV * RPW;
-  const int n_iters = part_end > part_begin ? (part_end - part_begin + RPI - 1) / RPI : 0;
-  const __amdgpu_buffer_rsrc_t rsx = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)X, 0, (int)(uint32_t)min((int64_t)B * ldx * 4, (int64_t)0xFFFFFFFF), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rsg = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(Gr ? Gr : X), 0,
-      (int)(uint32_t)min((int64_t)B * (Gr ? ldg : ldx) * 4, (int64_t)0xFFFFFFFF), 0x00020000);
-  auto load_rows = [&](int it, float (&raw)[NG][KC]) {
-    const int row0 = part_begin + it * RPI + wave * RPW;
-#pragma unroll
-    for (int g = 0; g < NG; ++g) {
-      const int rowi = min(row0 + g * 16 + j, part_end - 1);
-#pragma unroll
-      for (int kc = 0; kc < KC; ++kc) {
-        const bool gk = isg[kc];
-        const uint32_t off = ((uint32_t)rowi * (uint32_t)(gk ? ldg : ldx) + (uint32_t)colx[kc]) * 4u;
-        raw[g][kc] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(gk ? rsg : rsx, off, 0, 0));
-      }
-    }
-  };
-  float nxt[NG][KC];
-  int64_t nbi = -1;
-  auto load_bidx = [&](int it) {
-    const int row = part_begin + it * RPI + wave * RPW + q * 16 + j;
-    return (codes && q < NG && row < part_end) ? batch_idx[row] : (int64_t)-1;
-  };
-  if (n_iters > 0) {
-    load_rows(0, nxt);
-    nbi = load_bidx(0);
-  }
-  __syncthreads();
-  float bound_e[W];
-#pragma unroll
-  for (int k = 0; k < W; ++k) {
-    float v = bnd[k];
-#pragma unroll
-    for (int w = 1; w < WV; ++w) v = fmaxf(v, bnd[w * 16 + k]);
-    bound_e[k] = v;
-  }
-  float bound_ee = bnd[W];
-#pragma unroll
-  for (int w = 1; w < WV; ++w) bound_ee = fmaxf(bound_ee, bnd[w * 16 + W]);
-  const uint32_t aoff = (uint32_t)(q * mp + j) * 16u;   // plane q, codeword j of tile 0
-
-  for (int it = 0; it < n_iters; ++it) {
-    const int row0 = part_begin + it * RPI + wave * RPW;
-    float xk[NG][KC];
-#pragma unroll
-    for (int g = 0; g < NG; ++g) {
-#pragma unroll
-      for (int kc = 0; kc < KC; ++kc) {
-        float v = fmaf(__fsub_rn(nxt[g][kc], sh[kc]), al[kc], be[kc]);   // BatchNorm1d (bn_apply)
-        if (isg[kc]) v = __fmul_rn(v, grad_scale);        // vq.py:224
-        xk[g][kc] = v;
-      }
-    }
-    const int64_t cur_bi = nbi;
-    if (it + 1 < n_iters) {
-      load_rows(it + 1, nxt);
-      nbi = load_bidx(it + 1);
-    }
-    // row j of each group, all W values in every q-lane; |x|^2 in order;
-    // the bf16 split B operand; eps
-    float xr[NG][W], sx[NG], eps[NG];
-    bf16x8 bop[NG];
-#pragma unroll
-    for (int g = 0; g < NG; ++g) {
-      float s = 0.f, t = 0.f;
-#pragma unroll
-      for (int k = 0; k < W; ++k) {
-        const float v = __shfl(xk[g][k >> 2], j + 16 * (k & 3));
-        xr[g][k] = v;
-        s = (k == 0) ? __fmul_rn(v, v) : __fadd_rn(s, __fmul_rn(v, v));
-        t = fmaf(fabsf(v), bound_e[k], t);
-      }
-      sx[g] = s;
-      eps[g] = fmaf(t, 0x1p-13f, (bound_ee + s) * 0x1p-18f);
-      // this lane's slots 8q..8q+7 of [-2xh | -2xh | -2xl | 1 1 1 | 0...]:
-      // every non-constant slot i holds x[i % W], high part (-2h, exact) or
-      // low part (bf16(-2(x - h))), so one rounding path per slot:
-      // W = 8: q 0,1 high, q 2 low, q 3 constants;
-      // W = 4: q 0 high, q 1 low (i < 4) / constants, q 2,3 zero
-      const bool lo_lane = W == 8 ? (q == 2) : (q == 1);
-      unsigned short sl[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const float v = xr[g][i % W];
-        const float h = bf_round(v);
-        const float u = lo_lane ? v - h : h;
-        const unsigned short val = (unsigned short)(__float_as_uint(bf_round(-2.f * u)) >> 16);
-        const unsigned short one = i < 3 ? (unsigned short)0x3F80 : (unsigned short)0;
-        unsigned short r;
-        if constexpr (W == 8) {
-          r = q == 3 ? one : val;
-        } else {
-          const unsigned short one4 = (i >= 4 && i < 7) ? (unsigned short)0x3F80 : (unsigned short)0;
-          r = q >= 2 ? (unsigned short)0 : ((q == 1 && i >= 4) ? one4 : val);
-        }
-        sl[i] = r;
-      }
-#pragma unroll
-      for (int i = 0; i < 8; ++i) bop[g][i] = (short)sl[i];
-    }
-
-    // ---- sweep: smallest and second-smallest score per lane, tile of the smallest
-    // Four tiles per iteration (the planes hold kFilterSlack >= 48 codewords
-    // of +inf slack past M rounded to 16), even and odd tiles into two
-    // independent (m1, m2, mark) sets so the min chains overlap.  Each score
-    // is first read by the compiler's v_med3 (the MFMA -> VALU wait states
-    // are only inserted for instructions the compiler emits); the running
-    // minimum is a plain v_min taking the new second-smallest as a dummy
-    // operand, so it is ordered after that read (fmed3(p1, v, -inf) would
-    // add canonicalising v_max on every score).
-    float m1[2][NG], m2[2][NG];
-    int mark[2][NG];
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-      for (int g = 0; g < NG; ++g) {
-        m1[s2][g] = INFINITY;
-        m2[s2][g] = INFINITY;
-        mark[s2][g] = 0;
-      }
-    const char* lds = reinterpret_cast<const char*>(smem);
-    for (int m0 = 0; m0 < m_sweep; m0 += 64) {
-      bf16x8 a[4];
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-        a[t] = *reinterpret_cast<const bf16x8*>(lds + aoff + (uint32_t)(m0 + 16 * t) * 16u);
-      floatx4 d[4][NG];
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int g = 0; g < NG; ++g)
-          d[t][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[t], bop[g], floatx4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const int s2 = t & 1;
-#pragma unroll
-        for (int g = 0; g < NG; ++g) {
-          const float o = m1[s2][g];
-          float p1 = o, p2 = m2[s2][g];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            p2 = __builtin_amdgcn_fmed3f(p1, d[t][g][r], p2);
-            p1 = vmin_after(p1, d[t][g][r], p2);
-          }
-          mark[s2][g] = (p1 < o) ? m0 + 16 * t : mark[s2][g];
-          m1[s2][g] = p1;
-          m2[s2][g] = p2;
-        }
-      }
-    }
-    float m1m[NG], m2m[NG];
-    int markm[NG];
-#pragma unroll
-    for (int g = 0; g < NG; ++g) {
-      // merge the two sets; an equal minimum in both makes the row undecided
-      // (r2 == r1), so either mark serves
-      const bool lo = m1[1][g] < m1[0][g];
-      m1m[g] = lo ? m1[1][g] : m1[0][g];
-      m2m[g] = fminf(fmaxf(m1[0][g], m1[1][g]), fminf(m2[0][g], m2[1][g]));
-      markm[g] = lo ? mark[1][g] : mark[0][g];
-    }
-
-    int bidx[NG];
-    bool ok[NG];
-#pragma unroll
-    for (int g = 0; g < NG; ++g) {
-      // the row's two smallest scores over its 4 q-lanes, and the lowest
-      // (tile, lane) holding the smallest
-      float r1 = m1m[g], r2 = m2m[g];
-      int key = markm[g] + 4 * q;
-#pragma unroll
-      for (int sft = 16; sft <= 32; sft <<= 1) {
-        const float o1 = __shfl_xor(r1, sft), o2 = __shfl_xor(r2, sft);
-        const int ok2 = __shfl_xor(key, sft);
-        r2 = vmin(fmaxf(r1, o1), vmin(r2, o2));
-        key = (o1 < r1 || (o1 == r1 && ok2 < key)) ? ok2 : key;
-        r1 = vmin(r1, o1);
-      }
-      ok[g] = (r2 - r1) > 2.f * eps[g];
-      // exact resolve among the 4 codewords of the winning (tile, lane):
-      // lane q recomputes codeword key + q with the reference's operations
-      const int c = key + q;
-      const bool cv = c < M;
-      const float* er = E + (int64_t)(cv ? c : M - 1) * ldw;
-      float dot = 0.f;
-#pragma unroll
-      for (int k = 0; k < W; ++k) dot = (k == 0) ? __fmul_rn(er[k], xr[g][k]) : fmaf(er[k], xr[g][k], dot);
-      const float dist = fmaf(-2.f, dot, __fadd_rn(sx[g], cv ? se[c] : INFINITY));
-      float dmin = dist;
-      dmin = vmin(dmin, __shfl_xor(dmin, 16));
-      dmin = vmin(dmin, __shfl_xor(dmin, 32));
-      int rr = (dist == dmin) ? q : 4;
-      rr = min(rr, __shfl_xor(rr, 16));
-      rr = min(rr, __shfl_xor(rr, 32));
-      bidx[g] = key + (rr & 3);
-      ok[g] = ok[g] && rr < 4;
-    }
-
-    // ---- outputs: lane (q, j) writes group q's row j; ambiguous rows -> list
-    if (q < NG) {
-      const int row = row0 + q * 16 + j;
-      if (row < part_end) {
-        const int m = pickn<NG>(bidx, q);
-        bool okq = ok[0];
-#pragma unroll
-        for (int g = 1; g < NG; ++g) okq = (q == g) ? ok[g] : okq;
-        if (okq) {
-          if (idx_out) idx_out[(int64_t)b * B + row] = (int64_t)m;
-          if (codes) codes[cur_bi * ldc + b] = (int16_t)m;
-        } else {   // listed in LDS (global atomics only past kLocalList)
-          const int slot = atomicAdd(lcnt, 1);
-          if (slot < kLocalList) {
-            llist[slot] = row;
-          } else {
-            const int gs = atomicAdd(rcnt + b, 1);
-            rlist[(int64_t)b * B + gs] = row;
-          }
-        }
-      }
-    }
-    if constexpr (FUSED) {
-#pragma unroll
-      for (int g = 0; g < NG; ++g) {
-        if (ok[g] && row0 + g * 16 + j < part_end) {
-          unsigned long long* ap = acc + bidx[g] * (W + 1);
-          if (q == 0) atomicAdd(ap, 1ull);
-#pragma unroll
-          for (int kc = 0; kc < KC; ++kc)
-            atomicAdd(ap + 1 + kc * 4 + q, to_fixed(xk[g][kc], isg[kc] ? shift_g : shift_f));
-        }
-      }
-    }
-  }
-  // this workgroup's listed rows: one global reservation, then a copy
-  __syncthreads();
-  const int nl = min(*lcnt, kLocalList);
-  if (nl > 0) {
-    __syncthreads();          // every lane has read lcnt before it is reused
-    if (tid == 0) *lcnt = atomicAdd(rcnt + b, nl);
-    __syncthreads();
-    const int base = *lcnt;
-    for (int i = tid; i < nl; i += NT) rlist[(int64_t)b * B + base + i] = llist[i];
-  }
-  if constexpr (FUSED) {
     __syncthreads();
     unsigned long long* out = partial + (int64_t)b * M * (W + 1);
     for (int i = tid; i < M * (W + 1); i += NT)
@@ -1952,10 +1507,8 @@ extern "C" int32_t vqgnn_vq_ema_parts(int32_t B, int32_t nb, int32_t M, int32_t 
 extern "C" size_t vqgnn_vq_assign_workspace(int32_t B, int32_t nb, int32_t M, int32_t W) {
   if (B <= 0 || nb <= 0 || M <= 0 || W <= 0) return 0;
   const AssignGeom g = assign_geom(B, nb, M, W);
-  const size_t exact = g.fused ? 256 : align_up((size_t)nb * B * sizeof(int), 256);
-  // filtered path: per-branch counters + row lists
-  const size_t filt = align_up((size_t)nb * sizeof(int), 256) + align_up((size_t)nb * B * sizeof(int), 256);
-  return exact > filt ? exact : filt;
+  // the non-fused EMA path's row indices
+  return g.fused ? 256 : align_up((size_t)nb * B * sizeof(int), 256);
 }
 
 // Measurement facility for bench.py: while enabled, every vq_assign_kernel
@@ -1978,75 +1531,6 @@ static void timing_events(hipEvent_t* a, hipEvent_t* b) {
   g_timing_ev.emplace_back(*a, *b);
 }
 
-// filtered path (§3b): D = 4 and W in {4 (features), 8 (features, grads)},
-// one codebook chunk, fused or no EMA statistics.  Opt-in
-// (VQGNN_ASSIGN_FILTER=1): bit-exact, but measured no faster than the exact
-// kernel at arxiv_gcn (filter 155-160 us + 18 us list pass vs 172-184 us;
-// W = 4: 178 vs 117 us), DESIGN.md §4.1
-static std::atomic<int> g_filter_mode{-1};   // -1: VQGNN_ASSIGN_FILTER decides
-
-static bool filter_applies(int D, int W, int M, bool want_ema, bool fused) {
-  static const int env_on = env_int_vq("VQGNN_ASSIGN_FILTER", 0);
-  const int mode = g_filter_mode.load(std::memory_order_relaxed);
-  const int on = mode < 0 ? env_on : mode;
-  if (!on || D != 4 || (W != 4 && W != 8) || (want_ema && !fused)) return false;
-  return filter_lds_bytes(M, W, want_ema) <= kLdsBudget;
-}
-
-template <int W, bool FU>
-static int filter_capacity(size_t lds) {
-  int dev = 0, cus = 0, per_cu = 0;
-  if (hipGetDevice(&dev) != hipSuccess) {
-    (void)hipGetLastError();
-    return 512;
-  }
-  static std::mutex mu;
-  static std::map<std::tuple<int, size_t>, int> cache;
-  std::lock_guard<std::mutex> lk(mu);
-  const auto key = std::make_tuple(dev, lds);
-  auto it = cache.find(key);
-  if (it != cache.end()) return it->second;
-  const void* fn = (const void*)vq_assign_filter_kernel<W, FU>;
-  if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  int cap = 512;
-  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kAsgWaves * 64, lds) ==
-          hipSuccess &&
-      per_cu > 0 && cus > 0)
-    cap = per_cu * cus;
-  (void)hipGetLastError();
-  cache[key] = cap;
-  return cap;
-}
-
-template <int W, bool FU>
-static void launch_filter(const float* X, int64_t ldx, const float* G, int64_t ldg, int B, int nb,
-                          int D, int M, const float* coef, float grad_scale, const float* emb,
-                          int ldw, int64_t emb_bstride, int64_t* idx_out, int16_t* codes,
-                          int64_t ldc, const int64_t* batch_idx, unsigned long long* parts,
-                          int shift_f, int shift_g, int* rlist, int* rcnt, hipEvent_t ev0,
-                          hipStream_t s) {
-  const size_t lds = filter_lds_bytes(M, W, FU);
-  const void* fn = (const void*)vq_assign_filter_kernel<W, FU>;
-  if (lds > 64 * 1024)
-    (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  const int rows_per_iter = kAsgWaves * 16 * kAsgGroups;
-  const int row_blocks = (B + rows_per_iter - 1) / rows_per_iter;
-  int np = env_int_vq("VQGNN_ASG_TARGET", filter_capacity<W, FU>(lds)) / nb;
-  if (np < 1) np = 1;
-  if (np > row_blocks) np = row_blocks;
-  const int rpp = (B + np - 1) / np;
-  // codewords swept: M (VQGNN_FILTER_MSWEEP: a profiling knob that shortens
-  // the sweep and breaks the results; never set outside measurements)
-  static const int msw_env = env_int_vq("VQGNN_FILTER_MSWEEP", -1);
-  const int m_sweep = msw_env >= 0 && msw_env < M ? msw_env : M;
-  hipExtLaunchKernelGGL((vq_assign_filter_kernel<W, FU>), dim3(np * nb), dim3(kAsgWaves * 64),
-                        (uint32_t)lds, s, ev0, nullptr, 0, X, ldx, G, ldg, B, nb, D, M, coef,
-                        grad_scale, emb, ldw, emb_bstride, idx_out, codes, ldc, batch_idx, parts,
-                        rpp, shift_f, shift_g, rlist, rcnt, m_sweep);
-}
-
 template <int KC>
 static int launch_assign(const float* X, int64_t ldx, const float* G, int64_t ldg, int B,
                          int nb, int D, int M, int W, const float* coef, float grad_scale,
@@ -2066,75 +1550,20 @@ static int launch_assign(const float* X, int64_t ldx, const float* G, int64_t ld
     return VQGNN_ERR_UNSUPPORTED;
   }
   const int wgs = g.parts * nb;
-  // the list pass handles the undecided rows (0.4-2%, up to ~10% in one
-  // branch): up to 32 parts per branch of >= 64 rows, empty parts exit early
-  static const int list_parts = env_int_vq("VQGNN_LIST_PARTS", 32);
-  const int wgs_list = std::max(1, std::min(g.parts, list_parts)) * nb;
   const int wm = slot_mode(KC, W, D);
   if (want_ema && !ema_zeroed)
     (void)hipMemsetAsync(parts, 0, (size_t)nb * M * (W + 1) * sizeof(unsigned long long), s);
-  // filtered path: bf16-MFMA scores + exact resolve; the rows it cannot
-  // decide go through the exact kernel below in its row-list mode
-  const int* rlist = nullptr;
-  const int* rcnt = nullptr;
-  // timing (bench): one span from the filter's start to the list pass's end
-  hipEvent_t tev0 = nullptr, tev1 = nullptr;
-  if (workspace && filter_applies(D, W, M, want_ema, fused) &&
-      ((KC == 1 && wm == 1) || (KC == 2 && wm == 2))) {
-    timing_events(&tev0, &tev1);
-    int* cnt = reinterpret_cast<int*>(workspace);
-    int* list = cnt + align_up((size_t)nb * sizeof(int), 256) / sizeof(int);
-    (void)hipMemsetAsync(cnt, 0, (size_t)nb * sizeof(int), s);
-    if (W == 8) {
-      if (want_ema)
-        launch_filter<8, true>(X, ldx, G, ldg, B, nb, D, M, coef, grad_scale, emb, ldw,
-                               emb_bstride, idx_out, codes, ldc, batch_idx, parts, sh.f, sh.g,
-                               list, cnt, tev0, s);
-      else
-        launch_filter<8, false>(X, ldx, G, ldg, B, nb, D, M, coef, grad_scale, emb, ldw,
-                                emb_bstride, idx_out, codes, ldc, batch_idx, parts, sh.f, sh.g,
-                                list, cnt, tev0, s);
-    } else {
-      if (want_ema)
-        launch_filter<4, true>(X, ldx, G, ldg, B, nb, D, M, coef, grad_scale, emb, ldw,
-                               emb_bstride, idx_out, codes, ldc, batch_idx, parts, sh.f, sh.g,
-                               list, cnt, tev0, s);
-      else
-        launch_filter<4, false>(X, ldx, G, ldg, B, nb, D, M, coef, grad_scale, emb, ldw,
-                                emb_bstride, idx_out, codes, ldc, batch_idx, parts, sh.f, sh.g,
-                                list, cnt, tev0, s);
-    }
-    int rc = check_launch("vq_assign_filter");
-    if (rc) return rc;
-    rlist = list;
-    rcnt = cnt;
-  }
-#define VQ_LAUNCH_L(FU, WMV, LI)                                                              \
+#define VQ_LAUNCH(FU, WMV)                                                                    \
   do {                                                                                        \
-    const void* fn = (const void*)vq_assign_kernel<KC, FU, WMV, LI>;                          \
+    const void* fn = (const void*)vq_assign_kernel<KC, FU, WMV>;                              \
     if (lds > 64 * 1024)                                                                      \
       (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);    \
     hipEvent_t ev0 = nullptr, ev1 = nullptr;                                                  \
-    if (!LI) timing_events(&ev0, &ev1);                                                       \
-    else ev1 = tev1;                                                                          \
-    hipExtLaunchKernelGGL((vq_assign_kernel<KC, FU, WMV, LI>), dim3(LI ? wgs_list : wgs),      \
-                          dim3(kAsgWaves * 64),                                               \
+    timing_events(&ev0, &ev1);                                                                \
+    hipExtLaunchKernelGGL((vq_assign_kernel<KC, FU, WMV>), dim3(wgs), dim3(kAsgWaves * 64),     \
                           (uint32_t)lds, s, ev0, ev1, 0, X, ldx, G, ldg, B, nb, D, M, W, coef, \
                           grad_scale, emb, ldw, emb_bstride, idx_out, codes, ldc, batch_idx,   \
-                          idx32, parts, g.rows_per_part, g.chunk, sh.f, sh.g, rlist, rcnt,    \
-                          m_sweep);                                                           \
-  } while (0)
-  // the list pass exists for the filter's shapes only (W = D = 4: KC 1, WM 1;
-  // W = 2D = 8: KC 2, WM 2)
-#define VQ_LAUNCH(FU, WMV)                                                                    \
-  do {                                                                                        \
-    if constexpr ((KC == 1 && WMV == 1) || (KC == 2 && WMV == 2)) {                           \
-      if (rlist) {                                                                            \
-        VQ_LAUNCH_L(FU, WMV, true);                                                           \
-        break;                                                                                \
-      }                                                                                       \
-    }                                                                                         \
-    VQ_LAUNCH_L(FU, WMV, false);                                                              \
+                          idx32, parts, g.rows_per_part, g.chunk, sh.f, sh.g, m_sweep);       \
   } while (0)
 #define VQ_LAUNCH_WM(FU)                                                                      \
   do {                                                                                        \
@@ -2149,7 +1578,6 @@ static int launch_assign(const float* X, int64_t ldx, const float* G, int64_t ld
   if (fused) VQ_LAUNCH_WM(true); else VQ_LAUNCH_WM(false);
 #undef VQ_LAUNCH_WM
 #undef VQ_LAUNCH
-#undef VQ_LAUNCH_L
   int rc = check_launch("vq_assign");
   if (rc || !want_ema || fused) return rc;
   const size_t acc_bytes = (size_t)M * (W + 1) * sizeof(unsigned long long);
@@ -2166,10 +1594,6 @@ static int launch_assign(const float* X, int64_t ldx, const float* G, int64_t ld
                        sh.f, sh.g);
   }
   return check_launch("vq_ema_partial");
-}
-
-extern "C" void vqgnn_assign_filter(int32_t mode) {
-  g_filter_mode.store(mode < 0 ? -1 : (mode ? 1 : 0), std::memory_order_relaxed);
 }
 
 extern "C" int vqgnn_vq_assign(const float* X, int64_t ldx, const float* G, int64_t ldg,

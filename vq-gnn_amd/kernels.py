@@ -144,7 +144,7 @@ def vq_assign(X, G, coef, grad_scale, emb, D, W, idx_out=None, codes=None, batch
     L = lib()
     parts = None
     ws = None
-    # scratch: EMA row ids (non-fused) or the filtered path's row lists
+    # scratch: EMA row ids (non-fused path)
     ws = workspace(L.vqgnn_vq_assign_workspace(B, nb, M, W), X.device)
     if want_stats:
         P = L.vqgnn_vq_ema_parts(B, nb, M, W)
@@ -580,24 +580,6 @@ def gat_edge_grad(rows, col, coef, nnz, X, F, dy, dden, al, ar, params, X2=None,
                                     ptr(dy), _ld(dy), ptr(dden), ptr(al), ptr(ar), ptr(params),
                                     float(negative_slope), ptr(dal), ptr(dar), ptr(dsr),
                                     stream_ptr()), "gat_edge_grad")
-    return dal, dar, dsr
-
-
-def gat_edge_grad_csr(rowptr, col, coef, n_rows, X, F, dy, dden, al, ar, params, X2=None,
-                      B=None, negative_slope=0.2):
-    """Row-parallel coefficient-chain backward over the CSR (include/vqgnn.h
-    §8b): -> (dalpha_l [n], dalpha_r [n], ds_row [n])."""
-    dev = X.device
-    n = al.shape[0]
-    dal = torch.zeros(n, dtype=torch.float32, device=dev)
-    dar = torch.zeros(n, dtype=torch.float32, device=dev)
-    dsr = torch.zeros(n, dtype=torch.float32, device=dev)
-    Bv = int(B) if X2 is not None else X.shape[0]
-    check(lib().vqgnn_gat_edge_grad_csr(ptr(rowptr), int(n_rows), ptr(col), ptr(coef), ptr(X),
-                                        _ld(X), ptr(X2), _ld(X2) if X2 is not None else 0, Bv,
-                                        int(F), ptr(dy), _ld(dy), ptr(dden), ptr(al), ptr(ar),
-                                        ptr(params), float(negative_slope), ptr(dal), ptr(dar),
-                                        ptr(dsr), stream_ptr()), "gat_edge_grad_csr")
     return dal, dar, dsr
 
 
