@@ -58,6 +58,10 @@ def parse():
     # arxiv_gcn, profiles/r01c_*); "codes" = code records + LDS-staged
     # codebooks (x_first_order never materialised) where the codebook fits
     p.add_argument("--spmm-source", default="rows", choices=["codes", "rows"])
+    # run the codeword gather + aggregation on a second stream beside the VQ
+    # update (they read no state the update writes before finish_update):
+    # "after" issues them after the update, "before" ahead of it
+    p.add_argument("--overlap", default="off", choices=["off", "after", "before"])
     return p.parse_args()
 
 
@@ -142,17 +146,42 @@ def main():
     torch.cuda.synchronize()
 
     ev = []
+    side = torch.cuda.Stream() if args.overlap != "off" else None
 
-    def step(record):
-        e = [torch.cuda.Event(enable_timing=True) for _ in range(5)] if record else None
-        if record:
-            e[0].record()
+    def vq_update():
         if W == 2 * D:
             bank.update(Xd, Gd, 0, nb, True, codes=codes, batch_idx=bidx, defer=True)
         else:
             bank.feature_update(Xd, 0, nb, True, codes=codes, batch_idx=bidx)
+
+    def step(record):
+        if side is not None and not record:
+            cur = torch.cuda.current_stream()
+            side.wait_stream(cur)
+            if args.overlap == "after":
+                vq_update()
+            with torch.cuda.stream(side):
+                aggregate(False, None)
+            if args.overlap == "before":
+                vq_update()
+            cur.wait_stream(side)
+            bank.finish_update()
+            bank.sync_codes()
+            return
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(5)] if record else None
+        if record:
+            e[0].record()
+        vq_update()
         if record:
             e[1].record()
+        aggregate(record, e)
+        bank.finish_update()  # EMA finalize (multi-GPU: after the overlapped all-reduce)
+        bank.sync_codes()   # multi-GPU: other ranks' codes, exchanged behind gather + SpMM
+        if record:
+            e[4].record()
+            ev.append(e)
+
+    def aggregate(record, e):
         if fused:               # out-of-batch code records (x_first_order stays virtual)
             _, lcodes = kernels.gather_codewords(subset, B, codes, bank.emb_out, D,
                                                  want_x=False, want_codes=True)
@@ -171,11 +200,6 @@ def main():
                          plan=spmm_plan)
         if record:
             e[3].record()
-        bank.finish_update()  # EMA finalize (multi-GPU: after the overlapped all-reduce)
-        bank.sync_codes()   # multi-GPU: other ranks' codes, exchanged behind gather + SpMM
-        if record:
-            e[4].record()
-            ev.append(e)
 
     def barrier():
         if world > 1:

@@ -57,8 +57,8 @@ def run(name, F=None):
     del os.environ["VQGNN_TASK_SNAP"]
     variants = [("chunk kernel", None, None, None)] + [
         (f"task K={K} G={G} U={U}" + (" fixed" if K < 0 else ""), K, G, U)
-        for (K, G, U) in ((64, 32, 8), (-64, 32, 8), (64, 32, 4), (-64, 32, 4), (128, 32, 8),
-                          (-128, 32, 8), (32, 32, 8), (64, 16, 8))]
+        for (K, G, U) in ((64, 32, 8), (-64, 32, 8), (64, 32, 4), (64, 32, 16), (128, 32, 8),
+                          (128, 32, 16), (32, 32, 8), (64, 16, 8), (64, 16, 16))]
     res = {v[0]: [] for v in variants}
     for rep in range(3):              # interleaved repeats: box drift hits every variant alike
         for tag, K, G, U in variants:

@@ -63,6 +63,7 @@ struct TaskArgs {
   // near path: X and X2 as one 32-bit buffer range from ubase
   const char* ubase;
   uint32_t span, offx, ldxb, offx2, ldx2b;
+  uint32_t ldob;            // near path: ldo in bytes (rows addressed with a 24-bit multiply)
   int dbg;                  // experiments: 1 = no row stores (results invalid)
   int accum;                // 1: out[row] += the row's sum (vqgnn_spmm_task_acc: the
                             // sparse remainder behind the tile kernel); empty rows kept
@@ -154,14 +155,21 @@ __global__ void task_jobs_kernel(const int32_t* __restrict__ rowptr, int n_rows,
 }
 
 // ---- main kernel ---------------------------------------------------------
+// Source of record word x (column j = x & kColMask).  Near path: one 24-bit
+// multiply-add, j * ld + base, with (ld, base) = (ldxb, offx + lane_off) or
+// (ldx2b, offx2 - B * ldx2b + lane_off) (mod 2^32; task_setup guarantees
+// columns, strides and the range below 2^24 / 2^31).  v_mad_u32_u24 reads
+// only bits 0-23 of x, so the flag bits need no mask.
 template <bool FAR>
-__device__ __forceinline__ void row_src(const TaskArgs& a, uint32_t j, uint32_t lane_off,
-                                        uint32_t* off, const char** p) {
+__device__ __forceinline__ void row_src(const TaskArgs& a, uint32_t x, uint32_t b1, uint32_t b2,
+                                        uint32_t lane_off, uint32_t* off, const char** p) {
+  const uint32_t j = x & kColMask;
   if constexpr (FAR) {
     const float* row = (int)j < a.B ? a.X + (int64_t)j * a.ldx : a.X2 + (int64_t)((int)j - a.B) * a.ldx2;
     *p = reinterpret_cast<const char*>(row) + lane_off;
   } else {
-    *off = ((int)j < a.B ? a.offx + j * a.ldxb : a.offx2 + (j - (uint32_t)a.B) * a.ldx2b) + lane_off;
+    const bool s1 = (int)j < a.B;
+    *off = __umul24(x, s1 ? a.ldxb : a.ldx2b) + (s1 ? b1 : b2);
   }
 }
 
@@ -209,10 +217,11 @@ spmm_task_kernel(TaskArgs a) {
 #pragma unroll
   for (int i = 0; i < NC; ++i) pv[i] = c4base + G * i < F4;
   const uint32_t lane_off = (uint32_t)c4base * 16u;
+  const uint32_t b1 = a.offx + lane_off;
+  const uint32_t b2 = a.offx2 - (uint32_t)a.B * a.ldx2b + lane_off;
 
   int r = valid ? a.task_row[t] : 0;
   bool head = valid && a.rowptr[r] < e0;    // first row began in an earlier task
-  bool open = false;                        // acc holds a partial row
 
   const __amdgpu_buffer_rsrc_t rsx =
       __builtin_amdgcn_make_buffer_rsrc((void*)a.ubase, 0, FAR ? 0 : (int)a.span, 0x00020000);
@@ -231,10 +240,14 @@ spmm_task_kernel(TaskArgs a) {
   constexpr int kAnd = 0x1F & ~(G - 1);               // keep the group bits (32-lane swizzle)
   // GAT: the record lane computes its edge's coefficient and broadcasts it as
   // the weight (and, on column tile 0, stores it for the backward)
+  // The load is issued a block ahead and masked only when its block starts,
+  // so no wait for it sits between a block's gathers and the next block's.
   auto load_rec = [&](int e) -> int2 {
+    return __builtin_bit_cast(
+        int2, __builtin_amdgcn_raw_buffer_load_b64(rsr, (uint32_t)(e + k) * 8u, 0, 0));
+  };
+  auto mask_rec = [&](int2 q, int e) -> int2 {
     const int eu = e + k;
-    const int2 q = __builtin_bit_cast(
-        int2, __builtin_amdgcn_raw_buffer_load_b64(rsr, (uint32_t)eu * 8u, 0, 0));
     const bool in = k < U && eu >= e0 && eu < e1;
     if constexpr (GAT) {
       if (!in) return make_int2(0, 0);
@@ -252,23 +265,23 @@ spmm_task_kernel(TaskArgs a) {
 #pragma unroll
   for (int o = G; o < 64; o <<= 1) len = max(len, __shfl_xor(len, o));
 
-  int2 rcur = load_rec(e0);
+  int2 rraw = load_rec(e0);
   // wave-uniform (every lane holds the max): an SGPR loop, not an exec-masked one
   const int nblk = __builtin_amdgcn_readfirstlane((len + U - 1) / U);
   for (int bi = 0; bi < nblk; ++bi) {
     const int e = e0 + bi * U;
-    int2 rnxt = make_int2(0, 0);
-    if (bi + 1 < nblk) rnxt = load_rec(e + U);
+    // next block's records (past the buffer: zeros; outside the task: masked)
+    const int2 rnxt = load_rec(e + U);
+    const int2 rcur = mask_rec(rraw, e);
     int cx[U], cw[U];
     group_bcast<kAnd>(rcur.x, cx, std::make_integer_sequence<int, U>{});
     group_bcast<kAnd>(rcur.y, cw, std::make_integer_sequence<int, U>{});
     float4 v[U][NC];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const uint32_t j = (uint32_t)cx[u] & kColMask;
       uint32_t off = 0;
       const char* p = nullptr;
-      row_src<FAR>(a, j, lane_off, &off, &p);
+      row_src<FAR>(a, (uint32_t)cx[u], b1, b2, lane_off, &off, &p);
 #pragma unroll
       for (int i = 0; i < NC; ++i) {
         if constexpr (FAR) {
@@ -284,7 +297,6 @@ spmm_task_kernel(TaskArgs a) {
     for (int u = 0; u < U; ++u) {
       const float w = __int_as_float(cw[u]);
       const uint32_t x = (uint32_t)cx[u];
-      const bool real = e + u >= e0 && e + u < e1;
 #pragma unroll
       for (int i = 0; i < NC; ++i) {
         acc[i].x = fmaf(w, v[u][i].x, acc[i].x);
@@ -293,9 +305,11 @@ spmm_task_kernel(TaskArgs a) {
         acc[i].w = fmaf(w, v[u][i].w, acc[i].w);
       }
       if constexpr (GAT) den = __fadd_rn(den, w);
-      open = open || real;
       if (x & kEndBit) {                   // the row ends at this edge
-        float* dst = head ? a.carry + (int64_t)t * 2 * a.cf : a.out + (int64_t)r * a.ldo;
+        float* dst = head ? a.carry + (int64_t)t * 2 * a.cf
+                   : FAR  ? a.out + (int64_t)r * a.ldo
+                          : reinterpret_cast<float*>(reinterpret_cast<char*>(a.out) +
+                                                     (uint64_t)(uint32_t)__umul24((uint32_t)r, a.ldob));
         if constexpr (GAT) {
           if (head) {                      // partial: the fixup sums and normalises
             if (k == 0 && blockIdx.y == 0) dst[a.F] = den;
@@ -333,12 +347,15 @@ spmm_task_kernel(TaskArgs a) {
         r = skip == kSkipEsc ? upper_bound_i32(a.rowptr, a.n_rows, e + u + 1) - 1
                              : r + 1 + (int)skip;
         head = false;
-        open = false;
       }
     }
-    rcur = rnxt;
+    rraw = rnxt;
   }
-  if (open) {                              // the last row continues in the next task
+  // the task's last row continues in the next task unless its last edge ends
+  // a row (records outside the task carry no row end)
+  const bool open = valid && !(__builtin_amdgcn_raw_buffer_load_b32(rsr, (uint32_t)(e1 - 1) * 8u, 0, 0) &
+                               (int)kEndBit);
+  if (open) {
     float* dst = a.carry + ((int64_t)t * 2 + 1) * a.cf;
 #pragma unroll
     for (int i = 0; i < NC; ++i)
@@ -552,8 +569,12 @@ static int task_setup(TaskArgs& a, const int32_t* rowptr, int32_t n_rows, int32_
     lo = lo < y0 ? lo : y0;
     hi = hi > y1 ? hi : y1;
   }
-  *near = hi - lo < 0x7FFFFFF0ull && (int64_t)ldx * 4 < 0x7FFFFFFF &&
-          (int64_t)a.ldx2 * 4 < 0x7FFFFFFF && !task_env("VQGNN_SPMM_FAR", 0);
+  // near: 32-bit buffer offsets from one base, and 24-bit row multiplies
+  // (columns, rows and strides below 2^24, the output below 4 GiB)
+  *near = hi - lo < 0x7FFFFFF0ull && (int64_t)ldx * 4 < (1 << 24) &&
+          (int64_t)a.ldx2 * 4 < (1 << 24) && (int64_t)ldo * 4 < (1 << 24) &&
+          n_cols < (1 << 24) && n_rows < (1 << 24) &&
+          (int64_t)n_rows * ldo * 4 < ((int64_t)1 << 32) && !task_env("VQGNN_SPMM_FAR", 0);
   if (*near) {
     a.ubase = reinterpret_cast<const char*>(lo);
     a.span = (uint32_t)(hi - lo);
@@ -561,6 +582,7 @@ static int task_setup(TaskArgs& a, const int32_t* rowptr, int32_t n_rows, int32_
     a.ldxb = (uint32_t)(ldx * 4);
     a.offx2 = nx2 > 0 ? (uint32_t)(y0 - lo) : 0;
     a.ldx2b = (uint32_t)(a.ldx2 * 4);
+    a.ldob = (uint32_t)(ldo * 4);
   }
   a.dbg = task_env("VQGNN_TASK_DBG", 0);
   return VQGNN_OK;
@@ -577,7 +599,7 @@ static void task_launch(const TaskArgs& a, bool near, hipStream_t s) {
     int nc = 1;
     while (nc * G < F4 && nc * G * 4 < 128) nc *= 2;      // 4*G*nc floats <= 128
     const int tiles = (F4 + nc * G - 1) / (nc * G);
-    const int Ue = task_env("VQGNN_TASK_U", 8);
+    const int Ue = task_env("VQGNN_TASK_U", 16);
     const int U = Ue >= 16 ? 16 : (Ue >= 8 ? 8 : (Ue >= 4 ? 4 : 2));
     if (G == 8) {
       if (nc == 1) launch_task_u<8, 1, GAT>(a, tiles, U, near, s);
