@@ -271,3 +271,37 @@ def test_update_eval_mode_stashes_batch_stats():
     torch.testing.assert_close(m.std, torch.sqrt(inputs.var(0, keepdim=True) + 1e-24),
                                rtol=1e-5, atol=1e-7)
     assert torch.equal(m.batch_norm_feat.running_mean, rm)      # eval: running stats untouched
+
+
+@pytest.mark.parametrize("M,W,nb,B", [(4096, 8, 3, 5000), (5000, 4, 2, 3001), (4096, 8, 1, 700)])
+def test_split_ema_statistics_equal_global(M, W, nb, B, monkeypatch):
+    """Codebooks whose int64 EMA slab exceeds the LDS (ppi: M = 4096, W = 8)
+    accumulate per codeword range in LDS (vq_ema_split_kernel); the slab is
+    integer, so it must equal the global-atomics path exactly, and its counts
+    the bincount of the indices."""
+    from vq_gnn_amd import kernels
+    D = 4
+    F = nb * D
+    g = torch.Generator().manual_seed(M + B)
+    X = (torch.randn(B, F, generator=g) * 2).to(DEV)
+    G = (torch.randn(B, F, generator=g) * 1e-3).to(DEV)
+    emb = torch.randn(nb, M, 2 * D, generator=g).to(DEV)
+    coef = torch.zeros(6, F)
+    coef[0] = coef[2] = 1.0
+    coef = coef.to(DEV)
+    out = {}
+    for mode in ("split", "global"):
+        if mode == "global":
+            monkeypatch.setenv("VQGNN_EMA_GLOBAL", "1")
+        idx = torch.empty(nb, B, dtype=torch.long, device=DEV)
+        st = kernels.vq_assign(X, G if W == 2 * D else None, coef, 1.0, emb, D, W, idx_out=idx,
+                               want_stats=True, stat_count=B)
+        out[mode] = (idx.clone(), kernels.vq_ema_reduce(st).clone())
+    monkeypatch.delenv("VQGNN_EMA_GLOBAL", raising=False)
+    torch.cuda.synchronize()
+    assert torch.equal(out["split"][0], out["global"][0])
+    assert torch.equal(out["split"][1], out["global"][1])
+    stats = out["split"][1].view(nb, M, W + 1)
+    for b in range(nb):
+        assert torch.equal(stats[b, :, 0].cpu(),
+                           torch.bincount(out["split"][0][b].cpu(), minlength=M)), b

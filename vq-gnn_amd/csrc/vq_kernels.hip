@@ -1175,6 +1175,64 @@ vq_ema_partial_kernel(const float* __restrict__ X, int64_t ldx,
   }
 }
 
+// Split EMA statistics for a slab larger than the LDS (ppi: M = 4096, W = 8:
+// 295 KB per branch).  Workgroup = (branch, codeword range h of M / H, row
+// part): the range's slab sits in LDS; a thread takes one row per pass,
+// reads its index and, when it falls in the range, the row's W values, then
+// adds the count and the fixed-point values with ds_add_u64.  Indices are read
+// by every range (B ints per branch per range), row values once overall.  The
+// LDS slab is folded into the global one with int64 atomics: integer, exact,
+// order-free, so the result equals vq_ema_partial_kernel's.
+constexpr int kSplitThreads = 1024;
+constexpr size_t kSplitSlab = 80 * 1024;      // two workgroups per CU
+
+__global__ void __launch_bounds__(kSplitThreads)
+vq_ema_split_kernel(const float* __restrict__ X, int64_t ldx,
+                    const float* __restrict__ Gr, int64_t ldg,
+                    int B, int nb, int D, int M, int W,
+                    const float* __restrict__ coef, float grad_scale,
+                    const int* __restrict__ idx32, unsigned long long* __restrict__ partial,
+                    int H, int mrange, int rows_per_part, int shift_f, int shift_g) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long smem64[];
+  const int F = nb * D;
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int b = wg % nb;
+  const int h = (wg / nb) % H;
+  const int part = wg / (nb * H);
+  const int tid = threadIdx.x;
+  const int slots = W + 1;
+  const int m0 = h * mrange, m1 = min(M, m0 + mrange);
+  for (int i = tid; i < (m1 - m0) * slots; i += kSplitThreads) smem64[i] = 0ull;
+  __syncthreads();
+  const int row_begin = part * rows_per_part;
+  const int row_end = min(B, row_begin + rows_per_part);
+  const int* idx = idx32 + (int64_t)b * B;
+  int r = row_begin + tid;
+  int m = r < row_end ? idx[r] : -1;
+  for (; r < row_end; r += kSplitThreads) {
+    const int rn = r + kSplitThreads;
+    const int mn = rn < row_end ? idx[rn] : -1;       // next pass's index, in flight
+    if (m >= m0 && m < m1) {
+      unsigned long long* a = smem64 + (m - m0) * slots;
+      atomicAdd(a, 1ull);
+      for (int k = 0; k < W; ++k) {
+        const bool g = k >= D;
+        const int c = g ? b * D + (k - D) : b * D + k;
+        const float raw = g ? Gr[(int64_t)r * ldg + c] : X[(int64_t)r * ldx + c];
+        float v = fmaf(__fsub_rn(raw, coef[(g ? 5 * F : 4 * F) + c]), coef[(g ? 2 * F : 0) + c],
+                       coef[(g ? 3 * F : F) + c]);
+        if (g) v = __fmul_rn(v, grad_scale);
+        atomicAdd(a + 1 + k, to_fixed(v, g ? shift_g : shift_f));
+      }
+    }
+    m = mn;
+  }
+  __syncthreads();
+  unsigned long long* out = partial + ((int64_t)b * M + m0) * slots;
+  for (int i = tid; i < (m1 - m0) * slots; i += kSplitThreads)
+    if (smem64[i]) atomicAdd(out + i, smem64[i]);
+}
+
 // out[i] = sum over parts of parts[p][i] (integer: exact, order-free)
 __global__ void vq_ema_reduce_kernel(const long long* __restrict__ parts, int nparts,
                                      int64_t per_part, long long* __restrict__ out) {
@@ -1588,7 +1646,27 @@ static int launch_assign(const float* X, int64_t ldx, const float* G, int64_t ld
     hipLaunchKernelGGL(vq_ema_partial_kernel, dim3(wgs), dim3(kAssignThreads), acc_bytes, s, X,
                        ldx, G, ldg, B, nb, D, M, W, coef, grad_scale, idx32, parts,
                        g.rows_per_part, 1, sh.f, sh.g);
-  } else {  // global atomics
+  } else if (!env_int_vq("VQGNN_EMA_GLOBAL", 0)) {
+    // codeword ranges whose slab fits kSplitSlab; enough row parts for
+    // about two workgroups per CU
+    const size_t slot_bytes = (size_t)(W + 1) * sizeof(unsigned long long);
+    const int mrange = (int)std::max<size_t>(1, kSplitSlab / slot_bytes);
+    const int H = (M + mrange - 1) / mrange;
+    int dev = 0, ncu = 256;
+    if (hipGetDevice(&dev) == hipSuccess)
+      (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    const int want = 2 * ncu;
+    int rparts = std::max(1, (want + nb * H - 1) / (nb * H));
+    rparts = std::min(rparts, std::max(1, B / kSplitThreads));
+    const int rpp = (B + rparts - 1) / rparts;
+    const size_t slab = (size_t)mrange * slot_bytes;
+    if (slab > 64 * 1024)
+      (void)hipFuncSetAttribute((const void*)vq_ema_split_kernel,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)slab);
+    hipLaunchKernelGGL(vq_ema_split_kernel, dim3(nb * H * rparts), dim3(kSplitThreads), slab, s,
+                       X, ldx, G, ldg, B, nb, D, M, W, coef, grad_scale, idx32, parts, H, mrange,
+                       rpp, sh.f, sh.g);
+  } else {  // global atomics (measurement reference: VQGNN_EMA_GLOBAL=1)
     hipLaunchKernelGGL(vq_ema_partial_kernel, dim3(wgs), dim3(kAssignThreads), 0, s, X, ldx, G,
                        ldg, B, nb, D, M, W, coef, grad_scale, idx32, parts, g.rows_per_part, 0,
                        sh.f, sh.g);
