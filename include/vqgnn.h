@@ -141,7 +141,10 @@ int vqgnn_bn_stats_finalize(const float* X, int64_t ldx, const float* G, int64_t
  *      ema_parts [P][nb][M][W+1] int64 — P = vqgnn_vq_ema_parts(B, nb, M, W)
  *                (currently 1): (count, sum of normalised x) per codeword in
  *                fixed point; the workgroups' partials are added into it with
- *                int64 atomics.  ema_zeroed = 0: the call zeroes it first;
+ *                int64 atomics (from the assign's LDS slab when the codebook
+ *                and the slab share the LDS; else from a second kernel that
+ *                holds one codeword range's slab in LDS per workgroup).
+ *                ema_zeroed = 0: the call zeroes it first;
  *                1: the caller guarantees it is zero (e.g. left so by
  *                vqgnn_vq_ema_finalize with zero_after = 1).
  *    stat_count: rows the BatchNorm batch statistics were taken over (all
