@@ -166,7 +166,6 @@ def main():
                 vq_update()
             cur.wait_stream(side)
             bank.finish_update()
-            bank.sync_codes()
             return
         e = [torch.cuda.Event(enable_timing=True) for _ in range(5)] if record else None
         if record:
@@ -176,7 +175,8 @@ def main():
             e[1].record()
         aggregate(record, e)
         bank.finish_update()  # EMA finalize (multi-GPU: after the overlapped all-reduce)
-        bank.sync_codes()   # multi-GPU: other ranks' codes, exchanged behind gather + SpMM
+        # multi-GPU: the other ranks' codes land in the next update, after its
+        # assign (VQBank.update): the exchange overlaps gather + SpMM + BN + assign
         if record:
             e[4].record()
             ev.append(e)

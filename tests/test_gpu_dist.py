@@ -83,3 +83,38 @@ def test_rccl_world1_deferred_update(tmp_path):
     for tag in ("cap", "nocap"):
         for k in ("emb", "emb_out", "ema_w", "cs", "rm_f", "rv_f", "rm_g", "rv_g", "codes"):
             np.testing.assert_array_equal(r[f"{tag}_{k}"], r["ref_" + k], err_msg=f"{tag} {k}")
+
+
+@pytest.mark.parametrize("nb,M", [(32, 256), (8, 200), (6, 64), (16, 1024), (40, 256)])
+def test_wire_pack_scatter_last_record_wins(nb, M):
+    """The packed code exchange without RCCL: three 'ranks' pack their rows
+    (own codes scattered at once), the records are concatenated in rank order
+    (what all_gather_into_tensor delivers) and scattered: every node takes the
+    codes of its LAST record, the winner table returns to -1, and the
+    8-codes-per-thread kernels (uint8 wire, 8 | nb) agree with the
+    one-thread-per-record ones."""
+    from vq_gnn_amd import kernels
+    dev = torch.device("cuda:0")
+    rng = np.random.default_rng(nb * 7 + M)
+    N, max_B, world = 5000, 700, 3
+    rec = kernels.codes_wire_record(nb, M)
+    recv = torch.zeros(world * max_B * rec, dtype=torch.uint8, device=dev)
+    ref = np.zeros((N, nb), np.int64)
+    codes_own = torch.zeros(N, nb, dtype=torch.int16, device=dev)
+    for rk in range(world):
+        B = 600 + 30 * rk
+        ids = rng.choice(2000, size=B, replace=False)       # ranks overlap in [0, 2000)
+        loc = rng.integers(0, M, size=(B, nb))
+        send = torch.empty(max_B * rec, dtype=torch.uint8, device=dev)
+        kernels.pack_codes(torch.from_numpy(ids).to(dev), torch.from_numpy(loc).to(torch.int16).to(dev),
+                           M, max_B, send, codes=codes_own)
+        recv[rk * max_B * rec:(rk + 1) * max_B * rec] = send
+        ref[ids] = loc                                      # later ranks overwrite
+    winner = torch.full((N,), -1, dtype=torch.int32, device=dev)
+    codes = torch.zeros(N, nb, dtype=torch.int16, device=dev)
+    kernels.scatter_wire(recv, world * max_B, nb, M, winner, codes)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(codes.cpu().numpy(), ref)
+    assert bool((winner == -1).all())
+    # own-codes scatter of the pack: the last packing rank's codes for shared nodes
+    np.testing.assert_array_equal(codes_own.cpu().numpy(), ref)

@@ -59,6 +59,34 @@ __global__ void pack_codes_kernel(const int64_t* __restrict__ batch_idx, int B,
     for (int b = 0; b < nb; ++b) c[b] = l[b];
 }
 
+// Eight codes per thread (uint8 wire, 8 | nb, 16-byte aligned code rows):
+// thread (row, chunk) reads one 16-byte piece of the row's int16 codes,
+// writes 8 wire bytes and (own rows) the 16-byte piece of c_indices.
+__global__ void pack_codes8_kernel(const int64_t* __restrict__ batch_idx, int B,
+                                   const int16_t* __restrict__ local, int nb, int max_B,
+                                   uint8_t* __restrict__ send, int16_t* __restrict__ codes,
+                                   int64_t ldc) {
+  const int ch = nb >> 3;
+  const int64_t tix = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (tix >= (int64_t)max_B * ch) return;
+  const int r = (int)(tix / ch), c = (int)(tix % ch);
+  const int rec = wire_record_bytes(nb, 256);
+  uint8_t* p = send + (int64_t)r * rec;
+  if (r >= B) {
+    if (c == 0) *reinterpret_cast<int32_t*>(p) = -1;
+    return;
+  }
+  const int64_t node = batch_idx[r];
+  if (c == 0) *reinterpret_cast<int32_t*>(p) = (int32_t)node;
+  const uint4 t = *reinterpret_cast<const uint4*>(local + (int64_t)r * nb + 8 * c);
+  uint32_t* pw = reinterpret_cast<uint32_t*>(p + 4 + 8 * c);
+  pw[0] = (t.x & 0xFFu) | ((t.x >> 16 & 0xFFu) << 8) | ((t.y & 0xFFu) << 16) |
+          ((t.y >> 16 & 0xFFu) << 24);
+  pw[1] = (t.z & 0xFFu) | ((t.z >> 16 & 0xFFu) << 8) | ((t.w & 0xFFu) << 16) |
+          ((t.w >> 16 & 0xFFu) << 24);
+  if (codes && node >= 0) *reinterpret_cast<uint4*>(codes + node * ldc + 8 * c) = t;
+}
+
 __global__ void wire_winner_kernel(const uint8_t* __restrict__ recv, int64_t n, int rec,
                                    int64_t N, int32_t* __restrict__ winner) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -92,6 +120,28 @@ __global__ void wire_scatter_kernel(const uint8_t* __restrict__ recv, int64_t n,
   winner[node] = -1;   // only the winner clears: the losers compare against any other value
 }
 
+// Thread (record, chunk of 8 codes).  The lanes of one record sit in one
+// wave and all read winner[node] before chunk 0's lane (after its compare)
+// returns the entry to -1.
+__global__ void wire_scatter8_kernel(const uint8_t* __restrict__ recv, int64_t n, int rec,
+                                     int nb, int64_t N, int32_t* __restrict__ winner,
+                                     int16_t* __restrict__ codes, int64_t ldc) {
+  const int ch = nb >> 3;
+  const int64_t tix = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (tix >= n * ch) return;
+  const int64_t i = tix / ch;
+  const int c = (int)(tix % ch);
+  const uint8_t* p = recv + i * rec;
+  const int32_t node = *reinterpret_cast<const int32_t*>(p);
+  if (node < 0 || node >= N || winner[node] != (int32_t)i) return;
+  const uint32_t* pw = reinterpret_cast<const uint32_t*>(p + 4 + 8 * c);
+  const uint32_t w0 = pw[0], w1 = pw[1];
+  *reinterpret_cast<uint4*>(codes + (int64_t)node * ldc + 8 * c) =
+      make_uint4((w0 & 0xFFu) | ((w0 >> 8 & 0xFFu) << 16), (w0 >> 16 & 0xFFu) | ((w0 >> 24) << 16),
+                 (w1 & 0xFFu) | ((w1 >> 8 & 0xFFu) << 16), (w1 >> 16 & 0xFFu) | ((w1 >> 24) << 16));
+  if (c == 0) winner[node] = -1;
+}
+
 }  // namespace vqgnn
 
 using namespace vqgnn;
@@ -111,8 +161,17 @@ extern "C" int vqgnn_pack_codes(const int64_t* batch_idx, int32_t B, const int16
   // word-wise path: uint8 wire, 4 | nb, 8-byte aligned local rows and codes rows
   const int vec = M <= 256 && nb % 4 == 0 && ((uintptr_t)local & 7) == 0 &&
                   (!codes || (((uintptr_t)codes & 7) == 0 && ldc % 4 == 0));
-  hipLaunchKernelGGL(pack_codes_kernel, dim3((max_B + 255) / 256), dim3(256), 0,
-                     as_stream(stream), batch_idx, B, local, nb, M, max_B, send, codes, ldc, vec);
+  const bool vec8 = M <= 256 && nb % 8 == 0 && ((uintptr_t)local & 15) == 0 &&
+                    (!codes || (((uintptr_t)codes & 15) == 0 && ldc % 8 == 0));
+  if (vec8) {
+    const int64_t nt = (int64_t)max_B * (nb / 8);
+    hipLaunchKernelGGL(pack_codes8_kernel, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0,
+                       as_stream(stream), batch_idx, B, local, nb, max_B, send, codes, ldc);
+  } else {
+    hipLaunchKernelGGL(pack_codes_kernel, dim3((max_B + 255) / 256), dim3(256), 0,
+                       as_stream(stream), batch_idx, B, local, nb, M, max_B, send, codes, ldc,
+                       vec);
+  }
   return check_launch("pack_codes");
 }
 
@@ -127,6 +186,12 @@ extern "C" int vqgnn_scatter_wire(const uint8_t* recv, int64_t n_records, int32_
   const dim3 grid((unsigned)((n_records + 255) / 256));
   hipLaunchKernelGGL(wire_winner_kernel, grid, dim3(256), 0, as_stream(stream), recv, n_records,
                      rec, N, winner);
+  if (M <= 256 && nb % 8 == 0 && ((uintptr_t)codes & 15) == 0 && ldc % 8 == 0) {
+    const int64_t nt = n_records * (nb / 8);
+    hipLaunchKernelGGL(wire_scatter8_kernel, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0,
+                       as_stream(stream), recv, n_records, rec, nb, N, winner, codes, ldc);
+    return check_launch("scatter_wire");
+  }
   const int vec = M <= 256 && nb % 4 == 0 && ((uintptr_t)codes & 7) == 0 && ldc % 4 == 0;
   hipLaunchKernelGGL(wire_scatter_kernel, grid, dim3(256), 0, as_stream(stream), recv, n_records,
                      rec, nb, M, N, winner, codes, ldc, vec);

@@ -188,7 +188,9 @@ class VQBank(nn.Module):
     def feature_update(self, X, b0, nbr, training, idx_out=None, codes=None, batch_idx=None):
         """vq.py:160-202 for branches [b0, b0+nbr): X is [B, nbr*D] (a row-major view)."""
         self.finish_update()
-        self.sync_codes()
+        exchanging = training and self.comm is not None and codes is not None
+        if not exchanging:
+            self.sync_codes()
         D, F = self.D, nbr * self.D
         sl = self._sel(b0, nbr)
         B = X.shape[0]
@@ -228,6 +230,7 @@ class VQBank(nn.Module):
             stats = kernels.vq_ema_reduce(stats)
             comm.allreduce_(stats)
             if local is not None:
+                self.sync_codes()           # the previous exchange lands before ours
                 self._exchange_codes(batch_idx, local, codes, max_B)
         if training:
             kernels.vq_ema_finalize(stats, D, D, self.decay, self.warm_up_flag, 1.0, self.epsilon,
@@ -260,9 +263,16 @@ class VQBank(nn.Module):
         statistics is then asynchronous and overlaps what the caller queues
         before finish_update().  Until then emb / emb_out hold the codebook
         from before this update, as the reference's forward sees it (the
-        hook's update runs after the aggregation, models.py:181-185)."""
+        hook's update runs after the aggregation, models.py:181-185).
+
+        Multi-GPU, the previous update's code exchange is landed after this
+        update's assign, just before its own codes are scattered (the assign
+        reads no codes): the all_gather then overlaps the caller's gather +
+        SpMM and this update's statistics and assign."""
         self.finish_update()
-        self.sync_codes()
+        exchanging = training and self.comm is not None and codes is not None
+        if not exchanging:
+            self.sync_codes()
         D, F = self.D, nbr * self.D
         sl = self._sel(b0, nbr)
         B = X.shape[0]
@@ -312,6 +322,8 @@ class VQBank(nn.Module):
         work = None
         if comm is not None:
             stats = kernels.vq_ema_reduce(stats)
+            if local is not None:
+                self.sync_codes()           # the previous exchange lands before ours
             if defer:
                 if local is not None:      # codes first: the all-reduce is waited on later
                     self._exchange_codes(batch_idx, local, codes, max_B)
