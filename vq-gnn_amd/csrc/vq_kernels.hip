@@ -714,6 +714,10 @@ static AssignGeom assign_geom(int B, int nb, int M, int W) {
   } else {
     int c = g.mpad;
     while (c > 16 && cb_lds_bytes(g.kc, c) > kLdsBudget) c = (c / 2 + 15) / 16 * 16;
+    // measurement knob: a smaller staged chunk (more resident workgroups,
+    // the codebook restaged once per chunk and row block)
+    const int cenv = env_int_vq("VQGNN_ASG_CHUNK", 0);
+    if (cenv >= 32 && cenv < c) c = cenv / 32 * 32;
     g.chunk = c;
   }
   const int rows_per_iter = kAsgWaves * 16 * kAsgGroups;
