@@ -193,7 +193,10 @@ __device__ __forceinline__ float gat_edge_coef(const TaskArgs& a, int e, uint32_
   return __fmul_rn(expf(x), w);
 }
 
-template <int G, int NC, int U, bool FAR, bool GAT = false>
+// PART (near path): the last column tile is partial (F/4 not a multiple of
+// G*NC): its lanes past F load nothing (an offset past the buffer range
+// returns 0 without a memory access) instead of reading the next row
+template <int G, int NC, int U, bool FAR, bool GAT = false, bool PART = false>
 __global__ void __launch_bounds__(kTaskThreads)
 spmm_task_kernel(TaskArgs a) {
   constexpr int TPW = 64 / G;
@@ -217,6 +220,9 @@ spmm_task_kernel(TaskArgs a) {
 #pragma unroll
   for (int i = 0; i < NC; ++i) pv[i] = c4base + G * i < F4;
   const uint32_t lane_off = (uint32_t)c4base * 16u;
+  uint32_t kill[NC];                        // PART: 2^31 (> the range) for pieces past F
+#pragma unroll
+  for (int i = 0; i < NC; ++i) kill[i] = PART && !pv[i] ? 0x80000000u : 0u;
   const uint32_t b1 = a.offx + lane_off;
   const uint32_t b2 = a.offx2 - (uint32_t)a.B * a.ldx2b + lane_off;
 
@@ -288,8 +294,8 @@ spmm_task_kernel(TaskArgs a) {
           v[u][i] = pv[i] ? *reinterpret_cast<const float4*>(p + 16 * G * i)
                           : make_float4(0.f, 0.f, 0.f, 0.f);
         } else {   // pieces past F read the next row (or 0 past the range): never stored
-          v[u][i] = __builtin_bit_cast(
-              float4, __builtin_amdgcn_raw_buffer_load_b128(rsx, off + 16u * G * i, 0, 0));
+          const uint32_t o = PART ? ((off + 16u * G * i) | kill[i]) : off + 16u * G * i;
+          v[u][i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsx, o, 0, 0));
         }
       }
     }
@@ -432,11 +438,11 @@ spmm_task_fixup_kernel(TaskArgs a) {
   }
 }
 
-template <int G, int NC, int U, bool FAR, bool GAT>
+template <int G, int NC, int U, bool FAR, bool GAT, bool PART = false>
 static void launch_task(const TaskArgs& a, int tiles, hipStream_t s) {
   const int waves = (a.ntasks + 64 / G - 1) / (64 / G);
   const int blocks = (waves + 3) / 4;
-  hipLaunchKernelGGL((spmm_task_kernel<G, NC, U, FAR, GAT>), dim3(blocks, tiles),
+  hipLaunchKernelGGL((spmm_task_kernel<G, NC, U, FAR, GAT, PART>), dim3(blocks, tiles),
                      dim3(kTaskThreads), 0, s, a);
 }
 
@@ -446,7 +452,12 @@ static void launch_task_u(const TaskArgs& a, int tiles, int U, bool near, hipStr
   if (U > G) U = G;
   if (near) {
     if constexpr (G >= 16) {
-      if (U == 16) return launch_task<G, NC, 16, false, GAT>(a, tiles, s);
+      if (U == 16) {
+        if constexpr (!GAT && NC == 1) {   // the default shape: a partial last tile
+          if ((a.F >> 2) % (G * NC) != 0) return launch_task<G, NC, 16, false, GAT, true>(a, tiles, s);
+        }
+        return launch_task<G, NC, 16, false, GAT>(a, tiles, s);
+      }
     }
     if (U == 8) return launch_task<G, NC, 8, false, GAT>(a, tiles, s);
     if (U == 4) return launch_task<G, NC, 4, false, GAT>(a, tiles, s);
