@@ -380,9 +380,12 @@ spmm_task_kernel(TaskArgs a) {
 template <bool GAT>
 __global__ void __launch_bounds__(256)
 spmm_task_fixup_kernel(TaskArgs a) {
-  const int lane = threadIdx.x & 63;
-  const int w = blockIdx.x * 4 + (threadIdx.x >> 6);
+  // L lanes per job: 32 when a row (plus the GAT slot) fits 32 float4 pieces,
+  // so a wave finishes two rows
   const int F4 = a.F >> 2;
+  const int L = (GAT ? F4 + 1 : F4) <= 32 ? 32 : 64;
+  const int lane = threadIdx.x & (L - 1);
+  const int w = (blockIdx.x * 256 + threadIdx.x) / L;
   const int C4 = a.cf >> 2;                 // carry row stride in float4
   if (w < a.n_jobs) {
     const int r = a.jobs[3 * w], ts = a.jobs[3 * w + 1], t = a.jobs[3 * w + 2];
@@ -404,7 +407,7 @@ spmm_task_fixup_kernel(TaskArgs a) {
       norm = r < a.norm_B;
       q = __fadd_rn(d, 1e-16f);
     }
-    for (int c = lane; c < ncol; c += 64) {
+    for (int c = lane; c < ncol; c += L) {
       if (GAT && c == F4) continue;
       float4 sum = c4[((int64_t)ts * 2 + 1) * C4 + c];
       int u = ts + 1;
@@ -434,7 +437,7 @@ spmm_task_fixup_kernel(TaskArgs a) {
     const int r = a.jobs[3 * a.ntasks + (w - a.n_jobs)];    // the empty-row list
     if (r < 0 || r >= a.n_rows || a.accum) return;
     float4* o = reinterpret_cast<float4*>(a.out + (int64_t)r * a.ldo);
-    for (int c = lane; c < F4; c += 64) o[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int c = lane; c < F4; c += L) o[c] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
 }
 
@@ -625,7 +628,11 @@ static void task_launch(const TaskArgs& a, bool near, hipStream_t s) {
   }
   const int nfix = a.n_jobs + a.n_empty;
   if (nfix > 0)
-    hipLaunchKernelGGL(spmm_task_fixup_kernel<GAT>, dim3((nfix + 3) / 4), dim3(256), 0, s, a);
+  {
+    const int jobs_per_block = ((GAT ? a.F / 4 + 1 : a.F / 4) <= 32) ? 8 : 4;
+    hipLaunchKernelGGL(spmm_task_fixup_kernel<GAT>, dim3((nfix + jobs_per_block - 1) / jobs_per_block),
+                       dim3(256), 0, s, a);
+  }
 }
 
 extern "C" int vqgnn_spmm_task(const int32_t* rowptr, int32_t n_rows, int32_t n_cols, int64_t nnz,
