@@ -28,6 +28,84 @@ constexpr int kGatRowsPerWave = 4;
 
 // alpha_l / alpha_r of n rows (one wave per kGatRowsPerWave rows, lanes over
 // columns, fixed butterfly) and one (max_l, max_r) pair per block.
+// Vector form (F % 4 == 0, 16-byte rows): half a wave per row, float4
+// pieces, every row of the wave loaded before any sum (4 rows per wave);
+// a 5-step butterfly inside each half.  Same per-block maxima.
+__global__ void __launch_bounds__(kGatThreads)
+gat_alpha4_kernel(const float* __restrict__ X, int64_t ldx, const float* __restrict__ X2,
+                  int64_t ldx2, int B, int n, int F, int ones, const float* __restrict__ att_l,
+                  const float* __restrict__ att_r, float* __restrict__ al, float* __restrict__ ar,
+                  float* __restrict__ block_max) {
+  __shared__ float red[2][kGatThreads / 64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int half = lane >> 5, l32 = lane & 31;
+  const int F4 = F >> 2;
+  const int base = (blockIdx.x * (kGatThreads / 64) + wave) * kGatRowsPerWave;
+  float ml = -INFINITY, mr = -INFINITY;
+  float sl[kGatRowsPerWave / 2], sr[kGatRowsPerWave / 2];
+#pragma unroll
+  for (int k = 0; k < kGatRowsPerWave / 2; ++k) {
+    sl[k] = 0.f;
+    sr[k] = 0.f;
+  }
+  for (int c4 = l32; c4 < F4; c4 += 32) {
+    const float4 wl = reinterpret_cast<const float4*>(att_l)[c4];
+    const float4 wr = reinterpret_cast<const float4*>(att_r)[c4];
+    float4 v[kGatRowsPerWave / 2];
+#pragma unroll
+    for (int k = 0; k < kGatRowsPerWave / 2; ++k) {
+      const int i = base + 2 * k + half;
+      v[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (i < n) {
+        const float* row = i < B ? X + (int64_t)i * ldx : X2 + (int64_t)(i - B) * ldx2;
+        v[k] = reinterpret_cast<const float4*>(row)[c4];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kGatRowsPerWave / 2; ++k) {
+      sl[k] = fmaf(v[k].w, wl.w, fmaf(v[k].z, wl.z, fmaf(v[k].y, wl.y, fmaf(v[k].x, wl.x, sl[k]))));
+      sr[k] = fmaf(v[k].w, wr.w, fmaf(v[k].z, wr.z, fmaf(v[k].y, wr.y, fmaf(v[k].x, wr.x, sr[k]))));
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < kGatRowsPerWave / 2; ++k) {
+#pragma unroll
+    for (int off = 16; off > 0; off >>= 1) {
+      sl[k] = __fadd_rn(sl[k], __shfl_xor(sl[k], off));
+      sr[k] = __fadd_rn(sr[k], __shfl_xor(sr[k], off));
+    }
+    const int i = base + 2 * k + half;
+    if (i < n) {
+      if (ones) {  // the appended ones column is the last term of the sum
+        sl[k] = __fadd_rn(sl[k], att_l[F]);
+        sr[k] = __fadd_rn(sr[k], att_r[F]);
+      }
+      if (l32 == 0) {
+        al[i] = sl[k];
+        ar[i] = sr[k];
+      }
+      ml = fmaxf(ml, sl[k]);
+      mr = fmaxf(mr, sr[k]);
+    }
+  }
+  ml = fmaxf(ml, __shfl_xor(ml, 32));
+  mr = fmaxf(mr, __shfl_xor(mr, 32));
+  if (lane == 0) {
+    red[0][wave] = ml;
+    red[1][wave] = mr;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float a = red[0][0], b = red[1][0];
+    for (int w = 1; w < kGatThreads / 64; ++w) {
+      a = fmaxf(a, red[0][w]);
+      b = fmaxf(b, red[1][w]);
+    }
+    block_max[2 * blockIdx.x] = a;
+    block_max[2 * blockIdx.x + 1] = b;
+  }
+}
+
 __global__ void __launch_bounds__(kGatThreads)
 gat_alpha_kernel(const float* __restrict__ X, int64_t ldx, const float* __restrict__ X2,
                  int64_t ldx2, int B, int n, int F, int ones, const float* __restrict__ att_l,
@@ -393,8 +471,15 @@ extern "C" int vqgnn_gat_alpha(const float* X, int64_t ldx, const float* X2, int
   const int rows_per_block = (kGatThreads / 64) * kGatRowsPerWave;
   const int nblocks = (n + rows_per_block - 1) / rows_per_block;
   float* bm = reinterpret_cast<float*>(workspace);
-  hipLaunchKernelGGL(gat_alpha_kernel, dim3(nblocks), dim3(kGatThreads), 0, s, X, ldx, X2, ldx2,
-                     B, n, F, ones, att_l, att_r, alpha_l, alpha_r, bm);
+  const bool vec = F % 4 == 0 && ldx % 4 == 0 && ((uintptr_t)X & 15) == 0 &&
+                   (!X2 || (ldx2 % 4 == 0 && ((uintptr_t)X2 & 15) == 0)) &&
+                   ((uintptr_t)att_l & 15) == 0 && ((uintptr_t)att_r & 15) == 0;
+  if (vec)
+    hipLaunchKernelGGL(gat_alpha4_kernel, dim3(nblocks), dim3(kGatThreads), 0, s, X, ldx, X2,
+                       ldx2, B, n, F, ones, att_l, att_r, alpha_l, alpha_r, bm);
+  else
+    hipLaunchKernelGGL(gat_alpha_kernel, dim3(nblocks), dim3(kGatThreads), 0, s, X, ldx, X2,
+                       ldx2, B, n, F, ones, att_l, att_r, alpha_l, alpha_r, bm);
   hipLaunchKernelGGL(gat_scale_kernel, dim3(1), dim3(1024), 0, s, bm, nblocks, params);
   return check_launch("gat_alpha");
 }

@@ -383,7 +383,7 @@ spmm_task_fixup_kernel(TaskArgs a) {
   // L lanes per job: 32 when a row (plus the GAT slot) fits 32 float4 pieces,
   // so a wave finishes two rows
   const int F4 = a.F >> 2;
-  const int L = (GAT ? F4 + 1 : F4) <= 32 ? 32 : 64;
+  const int L = F4 <= 32 ? 32 : 64;          // (GAT's slot column F4 is skipped below)
   const int lane = threadIdx.x & (L - 1);
   const int w = (blockIdx.x * 256 + threadIdx.x) / L;
   const int C4 = a.cf >> 2;                 // carry row stride in float4
@@ -401,7 +401,15 @@ spmm_task_fixup_kernel(TaskArgs a) {
     bool norm = false;
     if constexpr (GAT) {                   // every lane needs the row's coefficient sum
       float d = a.carry[((int64_t)ts * 2 + 1) * a.cf + a.F];
-      for (int u = ts + 1; u < t; ++u) d = __fadd_rn(d, a.carry[((int64_t)u * 2 + 1) * a.cf + a.F]);
+      int u = ts + 1;
+      for (; u + 8 <= t; u += 8) {         // loads 8 tasks ahead of the in-order adds
+        float dv[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) dv[i] = a.carry[((int64_t)(u + i) * 2 + 1) * a.cf + a.F];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) d = __fadd_rn(d, dv[i]);
+      }
+      for (; u < t; ++u) d = __fadd_rn(d, a.carry[((int64_t)u * 2 + 1) * a.cf + a.F]);
       d = __fadd_rn(d, a.carry[(int64_t)t * 2 * a.cf + a.F]);
       if (a.den && lane == 0) a.den[r] = d;
       norm = r < a.norm_B;
@@ -629,7 +637,7 @@ static void task_launch(const TaskArgs& a, bool near, hipStream_t s) {
   const int nfix = a.n_jobs + a.n_empty;
   if (nfix > 0)
   {
-    const int jobs_per_block = ((GAT ? a.F / 4 + 1 : a.F / 4) <= 32) ? 8 : 4;
+    const int jobs_per_block = a.F / 4 <= 32 ? 8 : 4;
     hipLaunchKernelGGL(spmm_task_fixup_kernel<GAT>, dim3((nfix + jobs_per_block - 1) / jobs_per_block),
                        dim3(256), 0, s, a);
   }
