@@ -1211,6 +1211,9 @@ vq_ema_split_kernel(const float* __restrict__ X, int64_t ldx,
   const int row_begin = part * rows_per_part;
   const int row_end = min(B, row_begin + rows_per_part);
   const int* idx = idx32 + (int64_t)b * B;
+  const bool vec4 = D == 4 && (W == 4 || W == 8) && (ldx & 3) == 0 &&
+                    ((uintptr_t)X & 15) == 0 &&
+                    (W == 4 || ((ldg & 3) == 0 && ((uintptr_t)Gr & 15) == 0));
   int r = row_begin + tid;
   int m = r < row_end ? idx[r] : -1;
   for (; r < row_end; r += kSplitThreads) {
@@ -1219,6 +1222,27 @@ vq_ema_split_kernel(const float* __restrict__ X, int64_t ldx,
     if (m >= m0 && m < m1) {
       unsigned long long* a = smem64 + (m - m0) * slots;
       atomicAdd(a, 1ull);
+      if (vec4) {                          // D = 4: both halves as one float4 load each
+        float v[8];
+        const float4 xv = *reinterpret_cast<const float4*>(X + (int64_t)r * ldx + b * 4);
+        v[0] = xv.x; v[1] = xv.y; v[2] = xv.z; v[3] = xv.w;
+        if (W == 8) {
+          const float4 gv = *reinterpret_cast<const float4*>(Gr + (int64_t)r * ldg + b * 4);
+          v[4] = gv.x; v[5] = gv.y; v[6] = gv.z; v[7] = gv.w;
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          if (k >= W) break;
+          const bool g = k >= 4;
+          const int c = b * 4 + (k & 3);
+          float t = fmaf(__fsub_rn(v[k], coef[(g ? 5 * F : 4 * F) + c]), coef[(g ? 2 * F : 0) + c],
+                         coef[(g ? 3 * F : F) + c]);
+          if (g) t = __fmul_rn(t, grad_scale);
+          atomicAdd(a + 1 + k, to_fixed(t, g ? shift_g : shift_f));
+        }
+        m = mn;
+        continue;
+      }
       for (int k = 0; k < W; ++k) {
         const bool g = k >= D;
         const int c = g ? b * D + (k - D) : b * D + k;
@@ -1293,6 +1317,7 @@ vq_ema_finalize_kernel(long long* __restrict__ stats, int nparts, int64_t part_s
   if (tid == 0) bad = 0;
 
   // cs = cs*decay + (1-decay)*counts  (vq.py:177-178; fp32 tensor ops)
+#pragma unroll 4
   for (int m = tid; m < M; m += kFinThreads)
     cs_s[m] = __fadd_rn(__fmul_rn(cs[m], decay), __fmul_rn(one_m_decay, stat((int64_t)m * (W + 1), 0)));
   __syncthreads();
@@ -1332,7 +1357,9 @@ vq_ema_finalize_kernel(long long* __restrict__ stats, int nparts, int64_t part_s
   }
 
   // ema_w = ema_w*decay + (1-decay)*dw ; embedding = ema_w / cs ; output
+  // (unrolled: the loads of four elements per thread in flight together)
   const int nw = M * W;
+#pragma unroll 4
   for (int i = tid; i < nw; i += kFinThreads) {
     const int m = i / W, k = i % W;
     const int64_t o = (int64_t)m * ldw + k;
