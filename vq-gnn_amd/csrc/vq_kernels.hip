@@ -1288,7 +1288,7 @@ vq_ema_finalize_kernel(long long* __restrict__ stats, int nparts, int64_t part_s
                        float* __restrict__ emb_out, int64_t emb_bstride,
                        const float* __restrict__ rm_f, const float* __restrict__ rv_f,
                        const float* __restrict__ rm_g, const float* __restrict__ rv_g,
-                       int* __restrict__ bad_init) {
+                       int* __restrict__ bad_init, int split) {
   extern __shared__ float cs_s[];            // [M]
   __shared__ float wred[kFinWaves];
   __shared__ int bad;
@@ -1355,6 +1355,7 @@ vq_ema_finalize_kernel(long long* __restrict__ stats, int nparts, int64_t part_s
           st[(int64_t)p * part_stride + (int64_t)(i / W) * (W + 1) + 1 + i % W] = 0;
     return;
   }
+  if (split) return;                         // vq_ema_apply_kernel takes the rest
 
   // ema_w = ema_w*decay + (1-decay)*dw ; embedding = ema_w / cs ; output
   // (unrolled: the loads of four elements per thread in flight together)
@@ -1378,6 +1379,67 @@ vq_ema_finalize_kernel(long long* __restrict__ stats, int nparts, int64_t part_s
       const float sd = sqrtf(__fadd_rn(rv_g[b * D + kg], epsilon));
       out = __fadd_rn(__fmul_rn(__fdiv_rn(ev, div), sd), rm_g[b * D + kg]);
       if (grad_scale == 0.f) out = __fmul_rn(out, 0.f);  // vq.py:274-275
+    }
+    eo[o] = out;
+  }
+}
+
+// Large codebooks (M >= 1024): the per-codeword half of the finalize spread
+// over (branch, 256-codeword slice) workgroups once vq_ema_finalize_kernel
+// (split = 1) has written the branch's cluster sizes.  A branch with an
+// empty cluster is skipped (the finalize flagged it and cleared its slab).
+// Same operations per element as the single-kernel form.
+constexpr int kApplyThreads = 256;
+constexpr int kApplySlice = 256;
+
+__global__ void __launch_bounds__(kApplyThreads)
+vq_ema_apply_kernel(long long* __restrict__ stats, int nparts, int64_t part_stride,
+                    int zero_after, int shift_f, int shift_g, int M, int D, int W, int ldw,
+                    float decay, float grad_scale, float epsilon,
+                    const float* __restrict__ cluster_size, int64_t cs_bstride,
+                    float* __restrict__ ema_w, float* __restrict__ emb,
+                    float* __restrict__ emb_out, int64_t emb_bstride,
+                    const float* __restrict__ rm_f, const float* __restrict__ rv_f,
+                    const float* __restrict__ rm_g, const float* __restrict__ rv_g) {
+  const int b = blockIdx.y;
+  const int tid = threadIdx.x;
+  const float* cs = cluster_size + (int64_t)b * cs_bstride;
+  int zero = 0;
+  for (int m = tid; m < M; m += kApplyThreads) zero |= cs[m] == 0.f;
+  if (__syncthreads_or(zero)) return;
+  long long* st = stats + (int64_t)b * M * (W + 1);
+  auto stat = [&](int64_t i, int shift) {
+    long long v = st[i];
+    if (zero_after) st[i] = 0;
+    for (int p = 1; p < nparts; ++p) {
+      v += st[(int64_t)p * part_stride + i];
+      if (zero_after) st[(int64_t)p * part_stride + i] = 0;
+    }
+    return (float)ldexp((double)v, -shift);
+  };
+  float* ew = ema_w + (int64_t)b * emb_bstride;
+  float* e = emb + (int64_t)b * emb_bstride;
+  float* eo = emb_out + (int64_t)b * emb_bstride;
+  const float one_m_decay = (float)(1.0 - (double)decay);
+  const int m0 = blockIdx.x * kApplySlice, m1 = min(M, m0 + kApplySlice);
+  for (int i = m0 * W + tid; i < m1 * W; i += kApplyThreads) {
+    const int m = i / W, k = i % W;
+    const int64_t o = (int64_t)m * ldw + k;
+    const float dw = stat((int64_t)m * (W + 1) + 1 + k, k < D ? shift_f : shift_g);
+    const float w = __fadd_rn(__fmul_rn(ew[o], decay), __fmul_rn(one_m_decay, dw));
+    ew[o] = w;
+    const float ev = __fdiv_rn(w, cs[m]);
+    e[o] = ev;
+    float out;
+    if (k < D) {
+      const float sd = sqrtf(__fadd_rn(rv_f[b * D + k], 1e-5f));
+      out = __fadd_rn(__fmul_rn(ev, sd), rm_f[b * D + k]);
+    } else {
+      const int kg = k - D;
+      const float div = (float)((double)grad_scale + (double)epsilon);
+      const float sd = sqrtf(__fadd_rn(rv_g[b * D + kg], epsilon));
+      out = __fadd_rn(__fmul_rn(__fdiv_rn(ev, div), sd), rm_g[b * D + kg]);
+      if (grad_scale == 0.f) out = __fmul_rn(out, 0.f);
     }
     eo[o] = out;
   }
@@ -1786,12 +1848,21 @@ extern "C" int vqgnn_vq_ema_finalize(int64_t* ema_parts, int32_t nparts, int32_t
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 136 * 1024);
     });
   }
+  // M >= 1024: the per-codeword half runs in a second, wider launch
+  const int split = M >= 1024 && !env_int_vq("VQGNN_EMA_FIN_ONE", 0);
   hipLaunchKernelGGL(vq_ema_finalize_kernel, dim3(nb), dim3(kFinThreads), lds, as_stream(stream),
                      reinterpret_cast<long long*>(ema_parts), nparts,
                      (int64_t)nb * M * (W + 1), zero_after, sh.f, sh.g, M, D, W, ldw, decay,
                      laplace,
                      grad_scale, epsilon, cluster_size, cs_bstride, ema_w, embedding,
-                     embedding_output, emb_bstride, rm_f, rv_f, rm_g, rv_g, bad_init);
+                     embedding_output, emb_bstride, rm_f, rv_f, rm_g, rv_g, bad_init, split);
+  if (split)
+    hipLaunchKernelGGL(vq_ema_apply_kernel, dim3((M + kApplySlice - 1) / kApplySlice, nb),
+                       dim3(kApplyThreads), 0, as_stream(stream),
+                       reinterpret_cast<long long*>(ema_parts), nparts, (int64_t)nb * M * (W + 1),
+                       zero_after, sh.f, sh.g, M, D, W, ldw, decay, grad_scale, epsilon,
+                       cluster_size, cs_bstride, ema_w, embedding, embedding_output, emb_bstride,
+                       rm_f, rv_f, rm_g, rv_g);
   return check_launch("ema_finalize");
 }
 
