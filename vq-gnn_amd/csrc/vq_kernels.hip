@@ -585,6 +585,7 @@ struct AssignGeom {
   int chunk;          // codewords per LDS chunk (multiple of 16)
   int kc;             // k-chunks of 4 (W padded to 4*kc)
   bool fused;         // EMA statistics accumulated in the assign kernel
+  int wv;             // waves per workgroup (8 or 16)
 };
 
 template <int KC>
@@ -639,11 +640,13 @@ static int env_int_vq(const char* name, int dflt) {
   return v && *v ? atoi(v) : dflt;
 }
 
-constexpr int kAsgWaves = 8;    // waves per workgroup
+// Waves per workgroup: 8, or 16 where the LDS footprint (a large codebook,
+// or the fused EMA slab of M = 1024) leaves one workgroup per CU — the
+// choice with more resident waves per CU (assign_geom).
 constexpr int kAsgGroups = 2;   // 16-row groups per wave and iteration
 
-template <int KC, bool FUSED, int WM>
-__global__ void __launch_bounds__(kAsgWaves * 64)
+template <int KC, bool FUSED, int WM, int WV>
+__global__ void __launch_bounds__(WV * 64)
 vq_assign_kernel(const float* __restrict__ X, int64_t ldx,
                  const float* __restrict__ Gr, int64_t ldg,
                  int B, int nb, int D, int M, int W,
@@ -661,22 +664,25 @@ static int slot_mode(int kc, int W, int D) {
   return W == D ? 1 : 2;
 }
 
+template <int KC, int WV>
+static const void* assign_fn_wv(bool fused, int wm) {
+  if (fused) return wm == 1 ? (const void*)vq_assign_kernel<KC, true, 1, WV>
+                  : wm == 2 ? (const void*)vq_assign_kernel<KC, true, 2, WV>
+                            : (const void*)vq_assign_kernel<KC, true, 0, WV>;
+  return wm == 1 ? (const void*)vq_assign_kernel<KC, false, 1, WV>
+       : wm == 2 ? (const void*)vq_assign_kernel<KC, false, 2, WV>
+                 : (const void*)vq_assign_kernel<KC, false, 0, WV>;
+}
 template <int KC>
-static const void* assign_fn(bool fused, int wm) {
-  if (fused) return wm == 1 ? (const void*)vq_assign_kernel<KC, true, 1>
-                  : wm == 2 ? (const void*)vq_assign_kernel<KC, true, 2>
-                            : (const void*)vq_assign_kernel<KC, true, 0>;
-  return wm == 1 ? (const void*)vq_assign_kernel<KC, false, 1>
-       : wm == 2 ? (const void*)vq_assign_kernel<KC, false, 2>
-                 : (const void*)vq_assign_kernel<KC, false, 0>;
+static const void* assign_fn(bool fused, int wm, int wv) {
+  return wv == 16 ? assign_fn_wv<KC, 16>(fused, wm) : assign_fn_wv<KC, 8>(fused, wm);
 }
 
 // Workgroups of the assign kernel the current device holds at once (register
 // and LDS limited), cached per configuration.  Without a device (host-only
 // queries) a static estimate is returned; the value only sizes the grid.
-static int assign_capacity(int kc, bool fused, int wm, size_t lds) {
-  constexpr int wv = kAsgWaves;
-  const int fallback = 512;
+static int assign_capacity(int kc, bool fused, int wm, size_t lds, int wv) {
+  const int fallback = 512 * 8 / wv;
   int dev = 0, cus = 0, per_cu = 0;
   if (hipGetDevice(&dev) != hipSuccess) {
     (void)hipGetLastError();
@@ -684,12 +690,12 @@ static int assign_capacity(int kc, bool fused, int wm, size_t lds) {
   }
   static std::mutex mu;
   static std::map<std::tuple<int, int, bool, size_t>, int> cache;
-  const auto key = std::make_tuple(dev, kc * 4 + wm, fused, lds);
+  const auto key = std::make_tuple(dev, (kc * 4 + wm) * 32 + wv, fused, lds);
   std::lock_guard<std::mutex> lk(mu);
   auto it = cache.find(key);
   if (it != cache.end()) return it->second;
-  const void* fn = kc == 1 ? assign_fn<1>(fused, wm)
-                 : kc == 2 ? assign_fn<2>(fused, wm) : assign_fn<4>(fused, wm);
+  const void* fn = kc == 1 ? assign_fn<1>(fused, wm, wv)
+                 : kc == 2 ? assign_fn<2>(fused, wm, wv) : assign_fn<4>(fused, wm, wv);
   if (lds > 64 * 1024)
     (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   int cap = fallback;
@@ -720,13 +726,20 @@ static AssignGeom assign_geom(int B, int nb, int M, int W) {
     if (cenv >= 32 && cenv < c) c = cenv / 32 * 32;
     g.chunk = c;
   }
-  const int rows_per_iter = kAsgWaves * 16 * kAsgGroups;
+  size_t lds = cb_lds_bytes(g.kc, g.chunk);
+  if (g.fused) lds += acc;
+  const int wm = W == 4 * g.kc ? 2 : 0;
+  // waves per workgroup: the choice with more resident waves per CU (ties: 8)
+  const int cap8 = assign_capacity(g.kc, g.fused, wm, lds, 8);
+  const int cap16 = assign_capacity(g.kc, g.fused, wm, lds, 16);
+  g.wv = cap16 * 16 > cap8 * 8 ? 16 : 8;
+  const int wenv = env_int_vq("VQGNN_ASG_WAVES", 0);
+  if (wenv == 8 || wenv == 16) g.wv = wenv;
+  const int rows_per_iter = g.wv * 16 * kAsgGroups;
   const int row_blocks = (B + rows_per_iter - 1) / rows_per_iter;
   // one full round of resident workgroups: parts x nb <= what the device
   // holds at once (every part has the same row count, so no tail round)
-  size_t lds = cb_lds_bytes(g.kc, g.chunk);
-  if (g.fused) lds += acc;
-  const int target = env_int_vq("VQGNN_ASG_TARGET", assign_capacity(g.kc, g.fused, W == 4 * g.kc ? 2 : 0, lds));
+  const int target = env_int_vq("VQGNN_ASG_TARGET", g.wv == 16 ? cap16 : cap8);
   int parts = target / nb;
   if (parts < 1) parts = 1;
   if (parts > row_blocks) parts = row_blocks;
@@ -812,8 +825,8 @@ __device__ __forceinline__ void stage_chunk(const float* __restrict__ E, int ldw
   }
 }
 
-template <int KC, bool FUSED, int WM>
-__global__ void __launch_bounds__(kAsgWaves * 64)
+template <int KC, bool FUSED, int WM, int WV>
+__global__ void __launch_bounds__(WV * 64)
 vq_assign_kernel(const float* __restrict__ X, int64_t ldx,
                  const float* __restrict__ Gr, int64_t ldg,
                  int B, int nb, int D, int M, int W,
@@ -824,7 +837,7 @@ vq_assign_kernel(const float* __restrict__ X, int64_t ldx,
                  int* __restrict__ idx32, unsigned long long* __restrict__ partial,
                  int rows_per_part, int chunk, int shift_f, int shift_g, int m_sweep) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  constexpr int NG = kAsgGroups, WV = kAsgWaves, NT = WV * 64, K4 = 4 * KC;
+  constexpr int NG = kAsgGroups, NT = WV * 64, K4 = 4 * KC;
   const int F = nb * D;
   const int wg = xcd_remap(blockIdx.x, gridDim.x);
   const int b = wg % nb;
@@ -1704,23 +1717,28 @@ static int launch_assign(const float* X, int64_t ldx, const float* G, int64_t ld
   const int wm = slot_mode(KC, W, D);
   if (want_ema && !ema_zeroed)
     (void)hipMemsetAsync(parts, 0, (size_t)nb * M * (W + 1) * sizeof(unsigned long long), s);
-#define VQ_LAUNCH(FU, WMV)                                                                    \
+#define VQ_LAUNCH(FU, WMV, WVV)                                                               \
   do {                                                                                        \
-    const void* fn = (const void*)vq_assign_kernel<KC, FU, WMV>;                              \
+    const void* fn = (const void*)vq_assign_kernel<KC, FU, WMV, WVV>;                         \
     if (lds > 64 * 1024)                                                                      \
       (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);    \
     hipEvent_t ev0 = nullptr, ev1 = nullptr;                                                  \
     timing_events(&ev0, &ev1);                                                                \
-    hipExtLaunchKernelGGL((vq_assign_kernel<KC, FU, WMV>), dim3(wgs), dim3(kAsgWaves * 64),     \
+    hipExtLaunchKernelGGL((vq_assign_kernel<KC, FU, WMV, WVV>), dim3(wgs), dim3(WVV * 64),      \
                           (uint32_t)lds, s, ev0, ev1, 0, X, ldx, G, ldg, B, nb, D, M, W, coef, \
                           grad_scale, emb, ldw, emb_bstride, idx_out, codes, ldc, batch_idx,   \
                           idx32, parts, g.rows_per_part, g.chunk, sh.f, sh.g, m_sweep);       \
   } while (0)
+#define VQ_LAUNCH_WV(FU, WMV)                                                                 \
+  do {                                                                                        \
+    if (g.wv == 16) VQ_LAUNCH(FU, WMV, 16);                                                   \
+    else VQ_LAUNCH(FU, WMV, 8);                                                               \
+  } while (0)
 #define VQ_LAUNCH_WM(FU)                                                                      \
   do {                                                                                        \
-    if (wm == 1) VQ_LAUNCH(FU, 1);                                                            \
-    else if (wm == 2) VQ_LAUNCH(FU, 2);                                                       \
-    else VQ_LAUNCH(FU, 0);                                                                    \
+    if (wm == 1) VQ_LAUNCH_WV(FU, 1);                                                         \
+    else if (wm == 2) VQ_LAUNCH_WV(FU, 2);                                                    \
+    else VQ_LAUNCH_WV(FU, 0);                                                                 \
   } while (0)
   // codewords swept per chunk: all (VQGNN_ASSIGN_MSWEEP: a profiling knob that
   // shortens the sweep and breaks the results; never set outside measurements)
@@ -1728,6 +1746,7 @@ static int launch_assign(const float* X, int64_t ldx, const float* G, int64_t ld
   const int m_sweep = msw_env >= 0 ? msw_env : (1 << 30);
   if (fused) VQ_LAUNCH_WM(true); else VQ_LAUNCH_WM(false);
 #undef VQ_LAUNCH_WM
+#undef VQ_LAUNCH_WV
 #undef VQ_LAUNCH
   int rc = check_launch("vq_assign");
   if (rc || !want_ema || fused) return rc;
