@@ -136,8 +136,13 @@ def main():
         gat = OurGATConv(F + 1, F + 1, bias=False, add_self_loops=False).to(dev)
     # per-batch adjacency preparation (like the reference's SparseTensor build
     # in the data loader): the SpMM chunk plan, computed once per batch
-    fused = gat is None and args.spmm_source == "codes" and kernels.spmm_codes_supported(F, nb, M, D)
-    spmm_plan = adj.plan(F, B=B, kind="chunk" if fused else None)
+    # --spmm-source codes: the task-split code tiles (§6g) where they apply,
+    # else the round-1 chunk kernel with every codebook in LDS (§6c)
+    task_codes = gat is None and args.spmm_source == "codes" and \
+        kernels.spmm_task_codes_supported(F, nb, M, D) and os.environ.get("VQGNN_SPMM", "task") == "task"
+    fused = task_codes or (gat is None and args.spmm_source == "codes" and
+                           kernels.spmm_codes_supported(F, nb, M, D))
+    spmm_plan = adj.plan(F, B=B, kind="chunk" if fused and not task_codes else None)
     task = isinstance(spmm_plan, kernels.TaskPlan)
     if args.spmm_source == "codes" and not fused:
         raise SystemExit(f"--spmm-source codes: F={F} M={M} does not fit the LDS codebook path")
@@ -307,10 +312,11 @@ def main():
         except (OSError, ValueError):
             pmc = {}
     agg_name = ("gat aggregation (alpha+coef+spmm+normalize)" if gat is not None
+                else "spmm_task_codes_kernel+spmm_task_fixup_kernel" if task_codes
                 else "spmm_codes_kernel+spmm_fixup_kernel" if fused
                 else "spmm_task_kernel+spmm_task_fixup_kernel" if task
                 else "spmm_wave_kernel+spmm_fixup_kernel")
-    agg_pmc = ("spmm_codes_kernel" if fused else "spmm_task_kernel" if task
+    agg_pmc = ("spmm_task_codes_kernel" if task_codes else "spmm_codes_kernel" if fused else "spmm_task_kernel" if task
                else "spmm_wave_kernel")
     rl_spmm = dict(kernel=agg_name, bound="hbm",
                    achieved=spmm_bytes / (spmm_ms * 1e-3) / 1e9, peak=8000.0, unit="GB/s",

@@ -370,6 +370,26 @@ int vqgnn_spmm_tile(int32_t n_rows, int32_t n_cols, int32_t B, const float* X, i
                     const int32_t* blocks, int32_t n_dense, const int32_t* rowptr_b,
                     const int32_t* boff, const int64_t* drec, vqgnn_stream_t stream);
 
+/* 6g. Task-split code-source SpMM (opt-in; large codebooks, e.g. reddit's
+ *     M = 1024): vqgnn_spmm_task with the columns j >= B read as codewords,
+ *     xin[j][b*4 + k] = emb[b*emb_bstride + code*ldw + col_offset + k],
+ *     code = lcodes[(j - B)*ldlc + b] (models.py:168-174 without
+ *     materialising x_first_order).  Workgroups own column tiles of 8
+ *     branches and stage those branches' codebook entries (8*M float4) in
+ *     LDS; an out-of-batch edge reads one 2-byte code per branch.  Same task
+ *     plan, workspace, summation order and bits as vqgnn_spmm_task on the
+ *     gathered rows.  Applies when vqgnn_spmm_task_codes_supported(F, nb, M,
+ *     D): D == 4, F == 4*nb, M <= 1280; else VQGNN_ERR_UNSUPPORTED.  X may be
+ *     NULL when B == 0.                                                      */
+int vqgnn_spmm_task_codes_supported(int32_t F, int32_t nb, int32_t M, int32_t D);
+int vqgnn_spmm_task_codes(const int32_t* rowptr, int32_t n_rows, int32_t n_cols, int64_t nnz,
+                          int32_t B, const float* X, int64_t ldx, const int16_t* lcodes,
+                          int64_t ldlc, int32_t nb, const float* emb, int32_t M, int32_t D,
+                          int32_t ldw, int64_t emb_bstride, int32_t col_offset, int32_t F,
+                          float* out, int64_t ldo, const int32_t* plan, const int64_t* records,
+                          int32_t K, int32_t n_jobs, int32_t n_empty, void* workspace,
+                          vqgnn_stream_t stream);
+
 /* 7. CSR transpose (structure + values) for the backward product
  *    dX = A^T dOut (torch_sparse matmul autograd, convs.py:95).  Output CSR of
  *    A^T with rows sorted by column of A; within a row, entries ordered by

@@ -291,6 +291,51 @@ def test_spmm_codes_unsorted_rows_hubs_and_edges():
     assert not kernels.spmm_codes_supported(128, 32, 1024, 4)   # 512 KiB of codebook
 
 
+@pytest.mark.parametrize("nb,M,B", [(32, 1024, 1700), (151, 1024, 1700), (12, 300, 1700),
+                                    (32, 1024, 0), (32, 1024, 3000)])
+def test_spmm_task_codes_vs_task_two_source(nb, M, B):
+    """Task-split code-source SpMM (include/vqgnn.h §6g; reddit's M = 1024 and
+    F = 604's partial last tile): bit-identical to the task SpMM over the
+    gathered rows (same records, order, fix-up), within 1e-5 of fp64; rows
+    interleaving X and code columns, hub rows cut across tasks, empty rows,
+    B = 0 (codes only) and B = n_cols (no codes)."""
+    D = 4
+    F = nb * D
+    assert kernels.spmm_task_codes_supported(F, nb, M, D)
+    rng = np.random.default_rng(nb * 7 + M + B)
+    n_rows, n_cols = 2500, 3000
+    rowptr, col, val = _random_csr(n_rows, n_cols, 40, rng, hub_rows=(3, 1200), hub_deg=2900)
+    for i in range(n_rows):
+        s, e = rowptr[i], rowptr[i + 1]
+        col[s:e] = rng.permutation(col[s:e])
+    X = rng.standard_normal((max(B, 1), F)).astype(np.float32)
+    emb_out = rng.standard_normal((nb, M, 2 * D)).astype(np.float32)
+    lc = rng.integers(0, M, size=(n_cols - B, nb)).astype(np.int16)
+    a = _dev_csr(rowptr, col, val, n_rows, n_cols)
+    xd = torch.from_numpy(X).to(DEV)
+    emb_d = torch.from_numpy(emb_out).to(DEV)
+    lcd = torch.from_numpy(lc).to(DEV)
+    plan = a.plan(F, kind="task")
+    for off in (0, D):
+        out = kernels.spmm_codes(a.rowptr, a.col, a.value, n_rows, a.nnz(), xd, F, lcd, emb_d, D,
+                                 B, plan=plan, col_offset=off)
+        xt = emb_out[np.arange(nb)[None, :], lc.astype(np.int64), off:off + D].reshape(-1, F)
+        xtd = torch.from_numpy(np.ascontiguousarray(xt)).to(DEV)
+        if B == 0:
+            two = kernels.spmm(a.rowptr, a.col, a.value, n_rows, a.nnz(), xtd, F, plan=plan)
+        elif B == n_cols:
+            two = kernels.spmm(a.rowptr, a.col, a.value, n_rows, a.nnz(), xd, F, plan=plan)
+        else:
+            two = kernels.spmm(a.rowptr, a.col, a.value, n_rows, a.nnz(), xd, F, X2=xtd, B=B,
+                               plan=plan)
+        assert torch.equal(out, two), f"col_offset={off}"
+        xin = np.concatenate([X[:B], xt]) if B < n_cols else X
+        ref64 = conv_ref.spmm_fp64(rowptr, col, val, xin)
+        scale = conv_ref.spmm_fp64(rowptr, col, np.abs(val), np.abs(xin)) + 1e-6
+        assert np.max(np.abs(out.cpu().numpy() - ref64) / scale) < 1e-5
+    assert not kernels.spmm_task_codes_supported(F, nb, 2048, D)
+
+
 # --- segment-pair SpMM (include/vqgnn.h §6d): bit-identical to vqgnn_spmm ---
 
 def _pair_vs_chunk(rowptr, col, val, n_rows, n_cols, F, B=None, x2_rows=0, seed=0):

@@ -77,6 +77,11 @@ SIGNATURES = {
     "vqgnn_spmm_task": (ctypes.c_int, [_c_void_p, _i32, _i32, _i64, _i32, _c_void_p, _i64,
                                        _c_void_p, _i64, _i32, _c_void_p, _i64, _c_void_p,
                                        _c_void_p, _i32, _i32, _i32, _c_void_p, _c_void_p]),
+    "vqgnn_spmm_task_codes_supported": (ctypes.c_int, [_i32, _i32, _i32, _i32]),
+    "vqgnn_spmm_task_codes": (ctypes.c_int, [_c_void_p, _i32, _i32, _i64, _i32, _c_void_p, _i64,
+                                             _c_void_p, _i64, _i32, _c_void_p, _i32, _i32, _i32,
+                                             _i64, _i32, _i32, _c_void_p, _i64, _c_void_p,
+                                             _c_void_p, _i32, _i32, _i32, _c_void_p, _c_void_p]),
     "vqgnn_spmm_task_acc": (ctypes.c_int, [_c_void_p, _i32, _i32, _i64, _i32, _c_void_p, _i64,
                                            _c_void_p, _i64, _i32, _c_void_p, _i64, _c_void_p,
                                            _c_void_p, _i32, _i32, _i32, _c_void_p, _c_void_p]),

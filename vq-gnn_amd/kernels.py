@@ -451,6 +451,9 @@ def spmm_codes(rowptr, col, val, n_rows, nnz, X, F, lcodes, emb_out, D, B, out=N
     (j >= B) — x_input = cat([x, x_first_order]) of models.py:168-174 without
     materialising x_first_order.  lcodes: gather_codewords(..., want_x=False,
     want_codes=True)."""
+    if isinstance(plan, TaskPlan):
+        return spmm_task_codes(plan, n_rows, X, F, lcodes, emb_out, D, B, out=out,
+                               col_offset=col_offset, rowptr=rowptr, nnz=nnz, val=val)
     if isinstance(plan, PairPlan):   # the code-source kernel walks chunks
         plan = plan.chunk
     require_gpu(X, "spmm_codes")
@@ -473,6 +476,51 @@ def spmm_codes(rowptr, col, val, n_rows, nnz, X, F, lcodes, emb_out, D, B, out=N
                              ptr(emb_out), M, int(D), emb_out.shape[2], emb_out.stride(0),
                              int(col_offset), int(F), ptr(out), _ld(out), ptr(plan), ptr(ws),
                              stream_ptr()), "spmm_codes")
+    return out
+
+
+def spmm_task_codes_supported(F, nb, M, D) -> bool:
+    """True when vqgnn_spmm_task_codes applies (include/vqgnn.h §6g)."""
+    return bool(lib().vqgnn_spmm_task_codes_supported(int(F), int(nb), int(M), int(D)))
+
+
+def spmm_task_codes(plan, n_rows, X, F, lcodes, emb_out, D, B, out=None, col_offset=0,
+                    rowptr=None, nnz=None, val=None):
+    """The task-split SpMM (plan: TaskPlan) with the out-of-batch columns read
+    as codes: xin[j] = X[j] (j < B), concat_b emb_out[b, lcodes[j-B, b],
+    col_offset:col_offset+D] (j >= B); codebook column tiles of 8 branches
+    staged in LDS (any M <= 1280).  Same records, order and bits as
+    vqgnn_spmm_task on the gathered x_first_order."""
+    require_gpu(X, "spmm_task_codes")
+    dev = X.device
+    nb, M = emb_out.shape[0], emb_out.shape[1]
+    if not spmm_task_codes_supported(F, nb, M, D):
+        raise ValueError(f"spmm_task_codes: F={F} nb={nb} M={M} D={D} unsupported")
+    if lcodes.dtype != torch.int16 or lcodes.dim() != 2 or lcodes.shape[1] != nb or \
+            (lcodes.shape[0] > 0 and lcodes.stride(1) != 1):
+        raise ValueError("spmm_task_codes: lcodes must be int16 [n-B, nb], row-major")
+    if emb_out.stride(2) != 1 or emb_out.stride(1) != emb_out.shape[2]:
+        raise ValueError("spmm_task_codes: emb_out must be [nb, M, W] with contiguous rows")
+    if X.shape[0] < int(B):
+        raise ValueError(f"spmm_task_codes: X has {X.shape[0]} rows < B={B}")
+    if val is not None and val.data_ptr() != plan.val_ptr:
+        raise ValueError("spmm_task_codes: the task plan's records hold other values than val")
+    if nnz is not None and int(nnz) != plan.nnz or int(n_rows) > plan.n_rows:
+        raise ValueError(f"spmm_task_codes: task plan for nnz={plan.nnz}, rows={plan.n_rows}")
+    if rowptr is None:
+        raise ValueError("spmm_task_codes: rowptr is required")
+    if out is None:
+        out = torch.empty(n_rows, F, dtype=torch.float32, device=dev)
+    L = lib()
+    ws = workspace(L.vqgnn_spmm_task_workspace(plan.nnz, plan.K, F), dev)
+    n_cols = int(B) + lcodes.shape[0]
+    check(L.vqgnn_spmm_task_codes(ptr(rowptr), int(n_rows), n_cols, plan.nnz, int(B),
+                                  ptr(X) if int(B) > 0 else None, _ld(X), ptr(lcodes),
+                                  max(lcodes.stride(0), nb), nb, ptr(emb_out), M, int(D),
+                                  emb_out.shape[2], emb_out.stride(0), int(col_offset), int(F),
+                                  ptr(out), _ld(out), ptr(plan.plan), ptr(plan.records), plan.K,
+                                  plan.n_jobs, plan.n_empty, ptr(ws), stream_ptr()),
+          "spmm_task_codes")
     return out
 
 
