@@ -53,20 +53,44 @@ def parse():
     # kernel events inside the timed region (the roofline kernel's launches);
     # off only to measure what they cost
     p.add_argument("--no-kernel-events", action="store_true")
-    # aggregation source for the out-of-batch rows: "rows" = gathered
-    # x_first_order rows (default: measured faster, 99+7 us vs 171+7 us at
-    # arxiv_gcn, profiles/r01c_*); "codes" = code records + LDS-staged
-    # codebooks (x_first_order never materialised) where the codebook fits
-    p.add_argument("--spmm-source", default="rows", choices=["codes", "rows"])
-    # run the codeword gather + aggregation on a second stream beside the VQ
-    # update (they read no state the update writes before finish_update):
-    # "after" issues them after the update, "before" ahead of it
-    p.add_argument("--overlap", default="off", choices=["off", "after", "before"])
     return p.parse_args()
+
+
+def launcher_cmd(argv, gpus, port):
+    """The torch.distributed.run command bench.py starts as a child process
+    when called as ``python bench.py --gpus N`` (N > 1) outside a launcher:
+    one rank per GPU on this node, rendezvous on 127.0.0.1."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+            f"--nproc-per-node={gpus}", "--master-addr", "127.0.0.1",
+            "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def relay_ranks(args):
+    """--gpus N > 1 without WORLD_SIZE: run N ranks under torch.distributed.run
+    as a CHILD process (no exec, and nothing here has touched the GPU), relay
+    its output (rank 0 prints the JSON line) and exit with its return code."""
+    import subprocess
+    cmd = launcher_cmd(sys.argv[1:], args.gpus, free_port())
+    env = dict(os.environ)
+    env.setdefault("MASTER_ADDR", "127.0.0.1")
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    proc = subprocess.run(cmd, env=env)
+    sys.exit(proc.returncode)
 
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        relay_ranks(args)
+    if "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={os.environ['WORLD_SIZE']} but --gpus {args.gpus}")
     import torch.distributed as dist
     import vqgnn_pkg
     vqgnn_pkg.load()
@@ -135,23 +159,15 @@ def main():
         torch.manual_seed(4)
         gat = OurGATConv(F + 1, F + 1, bias=False, add_self_loops=False).to(dev)
     # per-batch adjacency preparation (like the reference's SparseTensor build
-    # in the data loader): the SpMM chunk plan, computed once per batch
-    # --spmm-source codes: the task-split code tiles (§6g) where they apply,
-    # else the round-1 chunk kernel with every codebook in LDS (§6c)
-    task_codes = gat is None and args.spmm_source == "codes" and \
-        kernels.spmm_task_codes_supported(F, nb, M, D) and os.environ.get("VQGNN_SPMM", "task") == "task"
-    fused = task_codes or (gat is None and args.spmm_source == "codes" and
-                           kernels.spmm_codes_supported(F, nb, M, D))
-    spmm_plan = adj.plan(F, B=B, kind="chunk" if fused and not task_codes else None)
-    task = isinstance(spmm_plan, kernels.TaskPlan)
-    if args.spmm_source == "codes" and not fused:
-        raise SystemExit(f"--spmm-source codes: F={F} M={M} does not fit the LDS codebook path")
+    # in the data loader): the SpMM task plan, built once per batch before the
+    # timed region; its cost is reported as plan_ms
+    spmm_plan = adj.plan(F, B=B)
+    plan_ms = time_plan(adj, n, nnz)
     # codebook state = one feature_update warm pass
     bank.feature_update(Xd, 0, nb, True, codes=codes, batch_idx=bidx)
     torch.cuda.synchronize()
 
     ev = []
-    side = torch.cuda.Stream() if args.overlap != "off" else None
 
     def vq_update():
         if W == 2 * D:
@@ -160,18 +176,6 @@ def main():
             bank.feature_update(Xd, 0, nb, True, codes=codes, batch_idx=bidx)
 
     def step(record):
-        if side is not None and not record:
-            cur = torch.cuda.current_stream()
-            side.wait_stream(cur)
-            if args.overlap == "after":
-                vq_update()
-            with torch.cuda.stream(side):
-                aggregate(False, None)
-            if args.overlap == "before":
-                vq_update()
-            cur.wait_stream(side)
-            bank.finish_update()
-            return
         e = [torch.cuda.Event(enable_timing=True) for _ in range(5)] if record else None
         if record:
             e[0].record()
@@ -187,17 +191,10 @@ def main():
             ev.append(e)
 
     def aggregate(record, e):
-        if fused:               # out-of-batch code records (x_first_order stays virtual)
-            _, lcodes = kernels.gather_codewords(subset, B, codes, bank.emb_out, D,
-                                                 want_x=False, want_codes=True)
-        else:
-            x_first, _ = kernels.gather_codewords(subset, B, codes, bank.emb_out, D)
+        x_first, _ = kernels.gather_codewords(subset, B, codes, bank.emb_out, D)
         if record:
             e[2].record()
-        if fused:
-            kernels.spmm_codes(adj.rowptr, adj.col, adj.value, n, nnz, Xd, F, lcodes,
-                               bank.emb_out, D, B, plan=spmm_plan)
-        elif gat is not None:     # attention aggregation (alpha, coef, SpMM, normalise)
+        if gat is not None:     # attention aggregation (alpha, coefficients, SpMM, normalise)
             with torch.no_grad():
                 gat.fused_forward(Xd, adj, x_first, B)
         else:
@@ -294,35 +291,24 @@ def main():
     # Algorithmic work per launch:
     #  vq_assign_kernel: 2*B*M*W flops per branch (the distance contraction);
     #  SpMM (spmm_task_kernel + spmm_task_fixup_kernel): rowptr + (col, val) + every
-    #  input row once (x and x_first_order) + the output rows.
-    #  fused (spmm_codes_kernel): X rows once, the B' code records and the
-    #  codebooks' feature halves instead of x_first_order.
-    if fused:
-        spmm_bytes = 4 * (n + 1) + 8 * nnz + 4 * B * F + 2 * (n - B) * nb + 4 * nb * M * D \
-            + 4 * n * F
-    else:
-        spmm_bytes = 4 * (n + 1) + 8 * nnz + 4 * n * F + 4 * n * F
+    #  input row once (x and x_first_order) + the output rows (SURVEY.md §8d).
+    spmm_bytes = 4 * (n + 1) + 8 * nnz + 4 * n * F + 4 * n * F
     vq_flops = 2.0 * B * M * W * nb
-    pmc = {}
-    if os.path.exists(args.pmc_json):
-        try:
-            pm = json.load(open(args.pmc_json))
-            if pm.get("config") == args.config and pm.get("semantics", "update") == args.semantics:
-                pmc = pm.get("hbm_bytes_per_launch", {})
-        except (OSError, ValueError):
-            pmc = {}
-    agg_name = ("gat aggregation (alpha+coef+spmm+normalize)" if gat is not None
-                else "spmm_task_codes_kernel+spmm_task_fixup_kernel" if task_codes
-                else "spmm_codes_kernel+spmm_fixup_kernel" if fused
-                else "spmm_task_kernel+spmm_task_fixup_kernel" if task
-                else "spmm_wave_kernel+spmm_fixup_kernel")
-    agg_pmc = ("spmm_task_codes_kernel" if task_codes else "spmm_codes_kernel" if fused else "spmm_task_kernel" if task
-               else "spmm_wave_kernel")
+    pmc, pmc_note = load_pmc(args)
+    agg_name = ("gat aggregation (alpha + fused coefficient/SpMM/normalise walker)"
+                if gat is not None else "spmm_task_kernel+spmm_task_fixup_kernel")
+    agg_pmc = "spmm_task_kernel"
     rl_spmm = dict(kernel=agg_name, bound="hbm",
                    achieved=spmm_bytes / (spmm_ms * 1e-3) / 1e9, peak=8000.0, unit="GB/s",
                    bytes_per_launch=spmm_bytes, ms_per_launch=spmm_ms,
                    traffic=pmc.get(agg_pmc))
     rl_spmm["frac"] = rl_spmm["achieved"] / rl_spmm["peak"]
+    if rl_spmm["traffic"]:
+        rl_spmm["traffic_over_algorithmic"] = rl_spmm["traffic"] / spmm_bytes
+    if gat is None:
+        # the kernel's own floor: the same plan shape with every column folded
+        # onto 1,024 hot rows (all gathers hit L2), DESIGN.md §4.2
+        rl_spmm["floor_ms"], rl_spmm["floor_note"] = spmm_floor(kernels, adj, Xd, B, n, nnz, F)
     rl_vq = dict(kernel="vq_assign_kernel", bound="mfma",
                  achieved=vq_flops / (assign_ms * 1e-3) / 1e12, peak=157.3, unit="TFLOP/s",
                  flops_per_launch=vq_flops, ms_per_launch=assign_ms,
@@ -331,7 +317,7 @@ def main():
     dominant = rl_spmm if spmm_ms >= assign_ms else rl_vq
     roofline = dict(bound=dominant["bound"], achieved=dominant["achieved"], peak=dominant["peak"],
                     unit=dominant["unit"], frac=dominant["frac"], traffic=dominant["traffic"],
-                    kernel=dominant["kernel"])
+                    kernel=dominant["kernel"], traffic_source=pmc_note)
 
     # measured device copy rate beside the 8 TB/s spec (a 1 GiB HBM -> HBM
     # copy, read + write bytes), after the timed region
@@ -362,19 +348,90 @@ def main():
             dtype="f32", data="synthetic (seeded arxiv-shaped graph, random features)",
             config=dict(workload=f"{args.config}: one layer step (VQ {args.semantics} + EMA for "
                                  f"{nb} branches, "
-                                 f"{'out-of-batch code gather' if fused else 'codeword gather'}, "
+                                 f"codeword gather, "
                                  f"{'GAT attention aggregation' if gat is not None else 'SpMM'})",
                         B=B, B_prime=n - B, nnz=nnz, F=F, M=M, D=D, W=W,
-                        parallelism=f"dp{world}"),
+                        parallelism=f"dp{world}", world=world,
+                        backend=(args.backend if comm is not None else None),
+                        rccl_ranks=(world if comm is not None and args.backend == "nccl" else 0),
+                        devices=(1 if os.environ.get("VQGNN_BENCH_ONE_DEVICE") == "1" else world)),
             roofline=roofline,
             kernels=dict(vq_update_ms=vq_ms, codeword_gather_ms=gather_ms, spmm_ms=spmm_ms,
                          spmm=rl_spmm, vq_assign=rl_vq),
             cpu_baseline=cpu,
             host_issue_ms_per_step=t_issue / args.steps * 1e3,
+            plan_ms=plan_ms,
         )
         print(json.dumps(out))
     if dist.is_initialized():
         dist.destroy_process_group()
+
+
+def lib_digest():
+    """sha256 of the libvqgnn.so this process loaded: ties PMC traffic to the
+    build it was measured on."""
+    import hashlib
+    from vq_gnn_amd._lib import LIB_PATH
+    h = hashlib.sha256()
+    with open(LIB_PATH, "rb") as f:
+        for blk in iter(lambda: f.read(1 << 20), b""):
+            h.update(blk)
+    return h.hexdigest()
+
+
+def load_pmc(args):
+    """Per-launch HBM bytes from profiles/pmc_latest.json (scripts/pmc_to_json.py)
+    -- only when it was captured on this config AND on the library this process
+    runs (its lib_sha256); otherwise traffic is null with the reason."""
+    if not os.path.exists(args.pmc_json):
+        return {}, "no PMC file"
+    try:
+        pm = json.load(open(args.pmc_json))
+    except (OSError, ValueError) as exc:
+        return {}, f"unreadable PMC file ({exc})"
+    if pm.get("config") != args.config or pm.get("semantics", "update") != args.semantics:
+        return {}, f"PMC file is for {pm.get('config')}/{pm.get('semantics')}"
+    lib_hash = lib_digest()
+    if pm.get("lib_sha256") != lib_hash:
+        return {}, (f"PMC file from another build (lib {str(pm.get('lib_sha256'))[:12]}, "
+                    f"running {lib_hash[:12]}): traffic withheld")
+    return pm.get("hbm_bytes_per_launch", {}), (
+        f"{os.path.relpath(args.pmc_json, ROOT)} (lib {lib_hash[:12]}, git {pm.get('git_head')})")
+
+
+def time_plan(adj, n, nnz, reps=5):
+    """Device time of one task-plan build (records, task starts, fix-up jobs and
+    the job-count readback), the per-batch preparation outside the timed step."""
+    from vq_gnn_amd import kernels
+    ts = []
+    for _ in range(reps + 1):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        kernels.spmm_task_plan(adj.rowptr, adj.col, adj.value, n, nnz)
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t0)
+    return float(np.median(ts[1:])) * 1e3
+
+
+def spmm_floor(kernels, adj, Xd, B, n, nnz, F, hot=1024, reps=10):
+    """SpMM over the same rows and row lengths with every column folded onto
+    `hot` rows of X (all gathers L2 hits): the per-edge gather issue floor of
+    the kernel, no memory system behind it."""
+    if B < hot:
+        return None, "batch smaller than the hot set"
+    col = torch.remainder(adj.col, hot).to(torch.int32)
+    plan = kernels.spmm_task_plan(adj.rowptr, col, adj.value, n, nnz)
+    out = torch.empty(n, F, dtype=torch.float32, device=Xd.device)
+    run = lambda: kernels.spmm(adj.rowptr, col, adj.value, n, nnz, Xd[:hot], F,  # noqa: E731
+                               out=out, plan=plan)
+    run()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        run()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps, f"columns folded onto {hot} hot rows, same plan shape"
 
 
 def cpu_leg(args, X, G, batch, bidx, subset, adj, codes0, M, D, B, nnz, nb, gat):
@@ -393,9 +450,11 @@ def cpu_leg(args, X, G, batch, bidx, subset, adj, codes0, M, D, B, nnz, nb, gat)
                                 val=vl.cpu().numpy(), n=int(subset.numel()))
     host = host_topology()
     threads = host["affinity"]
+    cap_source = f"sched_getaffinity ({threads} CPUs)"
     omp = os.environ.get("OMP_NUM_THREADS")
-    if omp and omp.isdigit() and int(omp) > 0:
-        threads = min(threads, int(omp))
+    if omp and omp.isdigit() and int(omp) > 0 and int(omp) < threads:
+        threads = int(omp)
+        cap_source = f"OMP_NUM_THREADS={omp} (the box's CPU share; affinity {host['affinity']})"
     att = None
     if gat is not None:
         att = (gat.att_l.detach().cpu().view(-1).numpy(), gat.att_r.detach().cpu().view(-1).numpy())
@@ -419,6 +478,7 @@ def cpu_leg(args, X, G, batch, bidx, subset, adj, codes0, M, D, B, nnz, nb, gat)
                 sample=f"{args.config} layer step ({sem}, {nb} branches, B={B}, nnz={nnz}): "
                        f"{desc_all}; median of {n_all} steps after 1 warm-up; "
                        f"oracle/cpu_baseline.py, torch {torch.__version__} CPU",
+                thread_cap=cap_source,
                 value_1thread=nnz / t_one,
                 sample_1thread=f"{desc_one}; median of {n_one} steps",
                 host=host)

@@ -217,99 +217,46 @@ int vqgnn_gather_codewords(const int64_t* subset, int32_t B, int32_t n,
 int vqgnn_scatter_codes(const int64_t* batch_idx, int32_t B, const int16_t* local,
                         int32_t nb, int16_t* codes, int64_t ldc, vqgnn_stream_t stream);
 
-/* 6. Two-source CSR SpMM (sum), the aggregation of OurGCNConv (convs.py:95 ->
- *    torch_sparse spmm_sum):
+/* 6. Task-split two-source CSR SpMM (sum), the aggregation of OurGCNConv
+ *    (convs.py:95 -> torch_sparse.matmul(adj, x_input, reduce='add')):
  *      out[i][:] = sum_{e in row i} val[e] * xin[col[e]][:]
  *    with xin[j] = X[j] for j < B and X2[j - B] for j >= B, i.e.
  *    x_input = cat([x, x_first_order]) (models.py:174) without the copy.
- *    X2 == NULL: xin = X (plain SpMM; B ignored) — also the transpose product
+ *    X2 == NULL: xin = X (plain SpMM; B ignored) -- also the transpose product
  *    of the backward pass.  n_cols = rows of xin (X rows, or B + X2 rows);
- *    every col[e] must be < n_cols.  Rows of at most L edges (L >= 128) are summed in CSR
- *    order with separate mul and add, bit-identical to spmm_sum's loop; longer
- *    rows are split into edge chunks whose partials are added in chunk order.
- *    F must be a multiple of 4; X/X2/out 16-byte aligned; out [n_rows][ldo]. */
-size_t vqgnn_spmm_workspace(int32_t n_rows, int64_t nnz, int32_t F);
-int vqgnn_spmm(const int32_t* rowptr, const int32_t* col, const float* val,
-               int32_t n_rows, int32_t n_cols, int64_t nnz, int32_t B,
-               const float* X, int64_t ldx, const float* X2, int64_t ldx2,
-               int32_t F, float* out, int64_t ldo, const int32_t* plan,
-               void* workspace, vqgnn_stream_t stream);
-/* 6b. Optional SpMM plan of a CSR (computed once per batch adjacency and F,
- *     like the transpose): the first row of every edge chunk, so the kernel's
- *     waves skip the row search.  plan: vqgnn_spmm_plan_size(nnz, F) int32;
- *     pass it to vqgnn_spmm (NULL = search in-kernel).                       */
-int64_t vqgnn_spmm_plan_size(int64_t nnz, int32_t F);
-int vqgnn_spmm_plan(const int32_t* rowptr, int32_t n_rows, int64_t nnz, int32_t F,
-                    int32_t* plan, vqgnn_stream_t stream);
-
-/* 6c. Code-source SpMM: vqgnn_spmm with xin[j] = X[j] for j < B and, for
- *     j >= B, xin[j][b*D + k] = emb[b*emb_bstride + code*ldw + col_offset + k]
- *     with code = lcodes[(j - B)*ldlc + b] — x_first_order (models.py:168-174)
- *     is never materialised: the codebooks' feature halves are staged in LDS
- *     and an out-of-batch edge reads its 2*nb-byte code record instead of a
- *     4*F-byte row.  Same summation order and bits as vqgnn_spmm.
- *     Applies when vqgnn_spmm_codes_supported(F, nb, M, D) (F in {64, 128,
- *     256}, nb*D == F, nb*M*D <= 32768 floats); else VQGNN_ERR_UNSUPPORTED.
- *     lcodes: vqgnn_gather_codewords(..., xt = NULL, lcodes); workspace and
- *     plan as vqgnn_spmm.                                                    */
-int vqgnn_spmm_codes_supported(int32_t F, int32_t nb, int32_t M, int32_t D);
-int vqgnn_spmm_codes(const int32_t* rowptr, const int32_t* col, const float* val,
-                     int32_t n_rows, int32_t n_cols, int64_t nnz, int32_t B,
-                     const float* X, int64_t ldx, const int16_t* lcodes, int64_t ldlc,
-                     int32_t nb, const float* emb, int32_t M, int32_t D, int32_t ldw,
-                     int64_t emb_bstride, int32_t col_offset, int32_t F, float* out,
-                     int64_t ldo, const int32_t* plan, void* workspace,
-                     vqgnn_stream_t stream);
-
-/* 6d. Segment-pair SpMM (F = 128): vqgnn_spmm with the same arguments, the
- *     same row semantics and bit-identical output, on a segment plan: rows
- *     (long rows: their S-aligned pieces) sorted by length inside 2048-row
- *     windows and XCD ranges, two segments per wave (one per half-wave), so
- *     one dwordx4 wave-instruction gathers two 512-B input rows.
- *     plan: vqgnn_spmm_pair_plan_size(n_rows, nnz, F) int32, built once per
- *     batch adjacency, F and B by vqgnn_spmm_pair_plan (scratch:
- *     vqgnn_spmm_pair_plan_workspace bytes); B splits the rows into batch
- *     and out-of-batch ranges for the XCD placement only.  workspace:
- *     vqgnn_spmm_workspace(n_rows, nnz, F).  The plan covers rows
- *     [0, n_rows) exactly as passed here.  When X and X2 lie more than 4 GiB
- *     apart the call runs vqgnn_spmm with chunk_plan (6b, may be NULL).
- *     Replaces convs.py:95 -> torch_sparse spmm_sum like 6.                  */
-int vqgnn_spmm_pair_supported(int32_t F);
-int64_t vqgnn_spmm_pair_plan_size(int32_t n_rows, int64_t nnz, int32_t F);
-size_t vqgnn_spmm_pair_plan_workspace(int32_t n_rows, int64_t nnz, int32_t F);
-int vqgnn_spmm_pair_plan(const int32_t* rowptr, int32_t n_rows, int64_t nnz, int32_t F,
-                         int32_t B, int32_t* plan, void* workspace, vqgnn_stream_t stream);
-int vqgnn_spmm_pair(const int32_t* rowptr, const int32_t* col, const float* val,
-                    int32_t n_rows, int32_t n_cols, int64_t nnz, int32_t B,
-                    const float* X, int64_t ldx, const float* X2, int64_t ldx2,
-                    int32_t F, float* out, int64_t ldo, const int32_t* plan,
-                    const int32_t* chunk_plan, void* workspace, vqgnn_stream_t stream);
-
-/* 6e. Task-split SpMM (the default aggregation): out = A * xin as in 6, for
- *     any F that is a multiple of 4 (column tiles of 128).  The nnz range is
- *     cut into tasks of K edges; 8 lanes walk one task (a wave: 8 tasks in
- *     lock-step, balanced whatever the row lengths), gathering each source
- *     row as 128-byte lines (dwordx4) and accumulating with fma; rows that
- *     span tasks are finished by a fix-up in task order, empty rows written
- *     as zeros.  Each row is a sequential fma chain over its edges in CSR
- *     order: deterministic, within 1e-5 relative of the fp64 sum (north_star
- *     tolerance; not spmm_sum's separate multiply/add bit pattern).
- *     Plan (once per batch adjacency, any F): vqgnn_spmm_task_plan fills
- *     plan [vqgnn_spmm_task_size(nnz, K, n_rows)] int32 (each task's first
- *     edge and row — a row of at most K/2 edges is never cut, so tasks hold
- *     K/2..3K/2 edges — then the fix-up jobs: cut rows and empty rows),
- *     records [nnz] int64 (source column, row-end flag, weight) and
- *     counts[2] (device int32: cut rows, empty rows), which the caller reads
- *     once per plan and passes to every vqgnn_spmm_task call as n_jobs /
- *     n_empty.  K = 64 (multiple of 4 in [8, 4096]).  A call may cover the
- *     first n_rows rows of the planned CSR (edges [0, rowptr[n_rows])), e.g.
- *     the backward's batch rows.  n_cols < 2^26.  Workspace:
- *     vqgnn_spmm_task_workspace(nnz, K, F) bytes.
- *     Replaces convs.py:95 -> torch_sparse spmm_sum like 6.                  */
+ *    every col[e] must be < n_cols < 2^26.  F a multiple of 4 (column tiles of
+ *    128 floats; a partial last tile loads nothing past F); X/X2/out 16-byte
+ *    aligned; out [n_rows][ldo].
+ *    The nnz range is cut into tasks of K edges; 32 lanes walk one task (a
+ *    wave: two tasks in lock-step, balanced whatever the row lengths),
+ *    gathering each source row as 512-byte lines (dwordx4 per lane, 16 edges
+ *    in flight per task) and accumulating with fma; rows that span tasks are
+ *    finished by a fix-up in task order, empty rows written as zeros.  Each
+ *    row is a sequential fma chain over its edges in CSR order: deterministic,
+ *    independent of the launch geometry, within 1e-5 relative of the fp64 sum
+ *    (north_star tolerance; not spmm_sum's separate multiply/add bit pattern).
+ *    Plan (once per batch adjacency, any F): vqgnn_spmm_task_plan fills
+ *    plan [vqgnn_spmm_task_size(nnz, K, n_rows)] int32 (each task's first
+ *    edge and row -- a row of at most K/2 edges is never cut, so tasks hold
+ *    K/2..3K/2 edges -- then the fix-up jobs: cut rows and empty rows),
+ *    records [nnz] int64 (source column, row-end flag, weight) and
+ *    counts[2] (device int32: cut rows, empty rows), which the caller reads
+ *    once per plan and passes to every vqgnn_spmm_task call as n_jobs /
+ *    n_empty.  K = 64 (multiple of 4 in [8, 4096]); nnz < 2^31.  A call may
+ *    cover the first n_rows rows of the planned CSR (edges
+ *    [0, rowptr[n_rows])), e.g. the backward's batch rows.  Workspace:
+ *    vqgnn_spmm_task_workspace(nnz, K, F) bytes.
+ *    vqgnn_spmm_task_records rewrites only the records for other values on
+ *    the same structure (the plan's task starts and fix-up jobs depend on
+ *    rowptr alone), e.g. GAT's coefficients on the transposed CSR in the
+ *    backward, without a new plan or a host read.                            */
 int64_t vqgnn_spmm_task_size(int64_t nnz, int32_t K, int32_t n_rows);
 int vqgnn_spmm_task_plan(const int32_t* rowptr, const int32_t* col, const float* val,
                          int32_t n_rows, int64_t nnz, int32_t K, int32_t* plan,
                          int64_t* records, int32_t* counts, vqgnn_stream_t stream);
+int vqgnn_spmm_task_records(const int32_t* rowptr, const int32_t* col, const float* val,
+                            int32_t n_rows, int64_t nnz, int64_t* records,
+                            vqgnn_stream_t stream);
 size_t vqgnn_spmm_task_workspace(int64_t nnz, int32_t K, int32_t F);
 int vqgnn_spmm_task(const int32_t* rowptr, int32_t n_rows, int32_t n_cols, int64_t nnz,
                     int32_t B, const float* X, int64_t ldx, const float* X2, int64_t ldx2,
@@ -370,26 +317,6 @@ int vqgnn_spmm_tile(int32_t n_rows, int32_t n_cols, int32_t B, const float* X, i
                     const int32_t* blocks, int32_t n_dense, const int32_t* rowptr_b,
                     const int32_t* boff, const int64_t* drec, vqgnn_stream_t stream);
 
-/* 6g. Task-split code-source SpMM (opt-in; large codebooks, e.g. reddit's
- *     M = 1024): vqgnn_spmm_task with the columns j >= B read as codewords,
- *     xin[j][b*4 + k] = emb[b*emb_bstride + code*ldw + col_offset + k],
- *     code = lcodes[(j - B)*ldlc + b] (models.py:168-174 without
- *     materialising x_first_order).  Workgroups own column tiles of 8
- *     branches and stage those branches' codebook entries (8*M float4) in
- *     LDS; an out-of-batch edge reads one 2-byte code per branch.  Same task
- *     plan, workspace, summation order and bits as vqgnn_spmm_task on the
- *     gathered rows.  Applies when vqgnn_spmm_task_codes_supported(F, nb, M,
- *     D): D == 4, F == 4*nb, M <= 1280; else VQGNN_ERR_UNSUPPORTED.  X may be
- *     NULL when B == 0.                                                      */
-int vqgnn_spmm_task_codes_supported(int32_t F, int32_t nb, int32_t M, int32_t D);
-int vqgnn_spmm_task_codes(const int32_t* rowptr, int32_t n_rows, int32_t n_cols, int64_t nnz,
-                          int32_t B, const float* X, int64_t ldx, const int16_t* lcodes,
-                          int64_t ldlc, int32_t nb, const float* emb, int32_t M, int32_t D,
-                          int32_t ldw, int64_t emb_bstride, int32_t col_offset, int32_t F,
-                          float* out, int64_t ldo, const int32_t* plan, const int64_t* records,
-                          int32_t K, int32_t n_jobs, int32_t n_empty, void* workspace,
-                          vqgnn_stream_t stream);
-
 /* 7. CSR transpose (structure + values) for the backward product
  *    dX = A^T dOut (torch_sparse matmul autograd, convs.py:95).  Output CSR of
  *    A^T with rows sorted by column of A; within a row, entries ordered by
@@ -415,7 +342,8 @@ int vqgnn_csr_expand_rows(const int32_t* rowptr, int32_t n_rows, int64_t nnz,
  *    gat_coef: coef[e] = exp(leaky(alpha_l[col]/s + alpha_r[row]/s)) * val[e]
  *      (no max shift, no softmax normalisation), den[i] = sum_e coef[e] in
  *      CSR order (the ones column of the aggregation)         (convs.py:249-266)
- *    The aggregation itself is vqgnn_spmm with val = coef.
+ *    (gat_coef + vqgnn_spmm_task on records of coef + gat_normalize is the
+ *    unfused form of vqgnn_gat_spmm_task, 8b, kept as its test reference.)
  *    gat_normalize: rows < B: out[i][:F] /= den[i] + eps       (models.py:188)
  *    gat_edge_grad: backward of the coefficient chain for every edge:
  *      dcoef = dy[row] . x_in[col][:F] + dden[row];  da = dcoef*coef*leaky'(a);
@@ -595,14 +523,16 @@ int32_t vqgnn_assign_timing_read(float* ms, int32_t cap);
  *     vqgnn_scatter_wire: all ranks' records (rank-major, as
  *     all_gather_into_tensor lays them out) into codes; a node held by
  *     several records takes the LAST record's codes (deterministic: a
- *     per-node atomicMax of the record index, then only the winner writes).
- *     winner: int32 [N], all -1 on entry, all -1 again on exit.              */
+ *     per-node atomicMax of (epoch << 32 | record index), then only the
+ *     winner writes).  winner: int64 [N], zero-initialised once and never
+ *     reset; epoch: 1, 2, 3, ... per call on the same table (< 2^31), so
+ *     earlier stamps always lose.  n_records < 2^32.                          */
 int32_t vqgnn_codes_wire_record(int32_t nb, int32_t M);
 int vqgnn_pack_codes(const int64_t* batch_idx, int32_t B, const int16_t* local, int32_t nb,
                      int32_t M, int32_t max_B, uint8_t* send, int16_t* codes, int64_t ldc,
                      vqgnn_stream_t stream);
 int vqgnn_scatter_wire(const uint8_t* recv, int64_t n_records, int32_t nb, int32_t M,
-                       int32_t* winner, int64_t N, int16_t* codes, int64_t ldc,
+                       int64_t* winner, int64_t epoch, int64_t N, int16_t* codes, int64_t ldc,
                        vqgnn_stream_t stream);
 
 /* ------------------------------------------------------------------------ *

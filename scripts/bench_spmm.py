@@ -1,6 +1,7 @@
 """SpMM kernel comparison on the bench batches (GPU): the task-split kernel
-(include/vqgnn.h §6e) at several K / unroll settings against the chunk
-kernel (§6b), with the algorithmic-byte roofline fraction of SURVEY §8(d).
+(include/vqgnn.h §6) at several K / G / U settings, with the algorithmic-byte
+roofline fraction of SURVEY §8(d), and bound probes (same plan shape,
+columns rewritten).
 Usage: python scripts/bench_spmm.py [arxiv_gcn|reddit_gcn|ppi_sage ...]"""
 import os
 import sys
@@ -48,38 +49,28 @@ def run(name, F=None):
         print(f"  {tag:28s} {t:9.1f} us  {alg / t / 1e3:7.1f} GB/s alg  frac {alg / t / 8e6:.3f}"
               f"  {b.nnz * 4 * F / t / 1e6:6.2f} TB/s gathered", flush=True)
 
-    chunk = adj.plan(F, B=b.B, kind="chunk")
     plans = {K: kernels.spmm_task_plan(adj.rowptr, adj.col, adj.value, b.n, b.nnz, K)
              for K in (32, 64, 128)}
     os.environ["VQGNN_TASK_SNAP"] = "0"     # fixed K-edge tasks (rows cut anywhere)
     plans.update({-K: kernels.spmm_task_plan(adj.rowptr, adj.col, adj.value, b.n, b.nnz, K)
                   for K in (64, 128)})
     del os.environ["VQGNN_TASK_SNAP"]
-    variants = [("chunk kernel", None, None, None)] + [
+    variants = [
         (f"task K={K} G={G} U={U}" + (" fixed" if K < 0 else ""), K, G, U)
         for (K, G, U) in ((64, 32, 8), (-64, 32, 8), (64, 32, 4), (64, 32, 16), (128, 32, 8),
                           (128, 32, 16), (32, 32, 8), (64, 16, 8), (64, 16, 16))]
     res = {v[0]: [] for v in variants}
     for rep in range(3):              # interleaved repeats: box drift hits every variant alike
         for tag, K, G, U in variants:
-            if K is None:
-                fn = lambda: kernels.spmm(adj.rowptr, adj.col, adj.value, b.n, b.nnz, X, F,  # noqa
-                                          X2=X2, B=b.B, out=out, plan=chunk)
-            else:
-                os.environ["VQGNN_TASK_U"], os.environ["VQGNN_TASK_G"] = str(U), str(G)
-                pl = plans[K]
-                fn = lambda: kernels.spmm(adj.rowptr, adj.col, adj.value, b.n, b.nnz, X, F,  # noqa
-                                          X2=X2, B=b.B, out=out, plan=pl)
+            os.environ["VQGNN_TASK_U"], os.environ["VQGNN_TASK_G"] = str(U), str(G)
+            pl = plans[K]
+            fn = lambda: kernels.spmm(adj.rowptr, adj.col, adj.value, b.n, b.nnz, X, F,  # noqa
+                                      X2=X2, B=b.B, out=out, plan=pl)
             res[tag].append(timeit(fn))
     for tag, ts in res.items():
         line(tag + " (min of 3)", min(ts))
     os.environ.pop("VQGNN_TASK_U", None)
     os.environ.pop("VQGNN_TASK_G", None)
-    ref = out.clone()
-    kernels.spmm(adj.rowptr, adj.col, adj.value, b.n, b.nnz, X, F, X2=X2, B=b.B, out=out,
-                 plan=chunk)
-    d = (out - ref).abs().max().item()
-    print(f"  max |task - chunk| = {d:.3e}", flush=True)
     tp = timeit(lambda: kernels.spmm_task_plan(adj.rowptr, adj.col, adj.value, b.n, b.nnz, 64))
     print(f"  task plan build            {tp:9.1f} us", flush=True)
     # bound probes: same CSR shape and task split, columns rewritten

@@ -1,4 +1,6 @@
-"""Run one hot-path kernel a few times on arxiv-shaped data (PMC target)."""
+"""Run one hot-path kernel a few times on a bench config's batch (PMC target).
+CONFIG=<bench config> (reddit configs build graph and batch on the device);
+argv[1]: step | vq | spmm | spmm_tile (the opt-in tiled SpMM's plan)."""
 import os
 import sys
 
@@ -18,8 +20,16 @@ dev = torch.device("cuda:0")
 what = sys.argv[1] if len(sys.argv) > 1 else "step"
 reps = int(os.environ.get("REPS", "5"))
 cfg = CONFIGS[os.environ.get("CONFIG", "arxiv_gcn")]
-g, _, b = make_batch(cfg)
-bidx, subset, adj = batch_to_device(b, dev)
+if cfg.get("device_build"):
+    from types import SimpleNamespace
+    from vq_gnn_amd.graph import make_batch_device
+    dg, (bidx, subset, adj) = make_batch_device(cfg, device=dev)
+    g = SimpleNamespace(N=dg.N)
+    b = SimpleNamespace(B=int(bidx.numel()), n=int(subset.numel()), nnz=adj.nnz())
+    del dg
+else:
+    g, _, b = make_batch(cfg)
+    bidx, subset, adj = batch_to_device(b, dev)
 F, M, D = cfg["F"], cfg["M"], 4
 nb = F // D
 X = torch.randn(b.B, F, device=dev)
@@ -31,12 +41,12 @@ for i in range(nb):
 bank = bank.to(dev)
 bank.feature_update(X, 0, nb, True, codes=codes, batch_idx=bidx)
 xt, _ = kernels.gather_codewords(subset, b.B, codes, bank.emb_out, D)
-plan = adj.plan(F, B=b.B)          # the default task plan (as the bench)
+plan = adj.plan(F, B=b.B, kind="tile" if what == "spmm_tile" else None)
 torch.cuda.synchronize()
 for _ in range(reps):
     if what in ("vq", "step"):
         bank.update(X, G, 0, nb, True, codes=codes, batch_idx=bidx)
-    if what in ("spmm", "step"):
+    if what in ("spmm", "step", "spmm_tile"):
         xt, _ = kernels.gather_codewords(subset, b.B, codes, bank.emb_out, D)
         kernels.spmm(adj.rowptr, adj.col, adj.value, b.n, b.nnz, X, F, X2=xt, B=b.B, plan=plan)
 torch.cuda.synchronize()

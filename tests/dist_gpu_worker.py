@@ -103,6 +103,34 @@ def main(out_dir):
     torch.cuda.synchronize()
     res["two_a"] = ca[:24].cpu().numpy()
     res["two_b"] = cb[:24].cpu().numpy()
+    # staleness contract of the deferred exchange, with a
+    # capacity (no host collective) as bench.py runs it: three consecutive
+    # update(defer=True) steps on disjoint node sets S[rank][step]; after step
+    # k a rank's codes hold its own step-k codes and the other rank's
+    # step-(k-1) codes, the other rank's step-k rows still hold their old
+    # codes; after sync_codes() the replicas are identical
+    sb = fresh_bank()
+    sb.comm = CodebookSync(count_group=sync.count_group, capacity=700)
+    sc = codes0.to(dev)
+    perm = torch.randperm(N, generator=torch.Generator().manual_seed(3))
+    sets = [[perm[(2 * k + r) * 600:(2 * k + r) * 600 + 600 - 50 * r] for k in range(3)]
+            for r in range(world)]
+    for k in range(3):
+        gk = torch.Generator().manual_seed(100 + 10 * k + rank)
+        nodes = sets[rank][k]
+        Xk = torch.randn(nodes.numel(), F, generator=gk).to(dev)
+        Gk = (torch.randn(nodes.numel(), F, generator=gk) * 1e-3).to(dev)
+        sb.update(Xk, Gk, 0, nb, True, codes=sc, batch_idx=nodes.to(dev), defer=True)
+        sb.finish_update()
+        torch.cuda.synchronize()
+        res[f"stale_{k}"] = sc.cpu().numpy()
+    sb.sync_codes()
+    torch.cuda.synchronize()
+    res["stale_final"] = sc.cpu().numpy()
+    res["stale_codes0"] = codes0.numpy()
+    for r in range(world):
+        for k in range(3):
+            res[f"set_{r}_{k}"] = sets[r][k].numpy()
     np.savez(os.path.join(out_dir, f"r{rank}.npz"), **res)
     dist.barrier()
     dist.destroy_process_group()

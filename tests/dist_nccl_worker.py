@@ -40,7 +40,10 @@ def main(out_dir):
         return bank.to(dev)
 
     res = {}
-    for tag, capacity in (("cap", B), ("nocap", None)):
+    # "cap4x": capacity above B -> a coarser fixed-point grid of the EMA
+    # statistic (dist.CodebookSync docstring): not bit-exact, within the EMA
+    # tolerance
+    for tag, capacity in (("cap", B), ("nocap", None), ("cap4x", 4 * B)):
         bank = fresh_bank()
         bank.comm = CodebookSync(count_group=dist.new_group(backend="gloo"), capacity=capacity)
         codes = codes0.clone()

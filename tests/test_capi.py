@@ -43,7 +43,8 @@ def test_host_only_workspace_queries():
     assert (sf.value, sg.value) == (21, 21)
     h.vqgnn_vq_stat_shifts(84670, 2.0 ** -10, ctypes.byref(sf), ctypes.byref(sg))
     assert (sf.value, sg.value) == (21, 31)
-    assert h.vqgnn_spmm_workspace(128000, 2_000_000, 128) > 0
+    assert h.vqgnn_spmm_task_workspace(2_000_000, 64, 128) > 0
+    assert h.vqgnn_spmm_task_size(2_000_000, 64, 128000) == 5 * 31250 + 1 + 128000
 
 
 def test_invalid_arguments_rejected_without_device():
@@ -54,7 +55,15 @@ def test_invalid_arguments_rejected_without_device():
     assert rc == 1
     assert b"null" in h.vqgnn_last_error() or b"W" in h.vqgnn_last_error()
     # dummy non-null addresses: validation rejects F before any pointer is used
-    rc = h.vqgnn_spmm(16, None, None, 4, 4, 0, 0, None, 4, None, 0, 6, 16, 4, None, None, None)
+    rc = h.vqgnn_spmm_task(16, 4, 4, 0, 0, None, 4, None, 0, 6, 16, 4, 16, None, 64, 0, 0,
+                           None, None)
     assert rc == 1 and b"multiple of 4" in h.vqgnn_last_error()
-    rc = h.vqgnn_spmm(None, None, None, 4, 4, 0, 0, None, 4, None, 0, 8, None, 8, None, None, None)
+    rc = h.vqgnn_spmm_task(None, 4, 4, 0, 0, None, 4, None, 0, 8, None, 8, None, None, 64, 0, 0,
+                           None, None)
     assert rc == 1 and b"null" in h.vqgnn_last_error()
+    # the plan's edge count is bounded by its int32 task starts
+    rc = h.vqgnn_spmm_task_plan(16, 16, None, 4, 1 << 31, 64, 16, 16, 16, None)
+    assert rc == 1 and b"bad arguments" in h.vqgnn_last_error()
+    # the code exchange's stamp epochs start at 1
+    rc = h.vqgnn_scatter_wire(16, 4, 8, 256, 16, 0, 10, 16, 8, None)
+    assert rc == 1 and b"epoch" in h.vqgnn_last_error()

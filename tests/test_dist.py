@@ -30,10 +30,11 @@ def _worker(rank, world, port, out_dir):
     # per-rank batch sizes that change between calls: without a capacity,
     # every call agrees on this call's max(B)
     res["max_seq"] = np.array([sync.rows_per_rank(b) for b in ([5, 2, 9], [3, 7, 1])[rank]])
-    # the update path's BatchNorm all-reduce carries the row count: [4F + 1]
-    # fp64 sums with B last (bn_stats(with_count=True))
+    # the update path's BatchNorm all-reduce carries the row count: [4F + 2]
+    # fp64 sums with B at 4F and the over-capacity flag last
+    # (bn_stats(with_count=True))
     for b in ([5, 2, 9], [3, 7, 1])[rank]:
-        flat = torch.zeros(4 * 2 + 1, dtype=torch.float64)
+        flat = torch.zeros(4 * 2 + 2, dtype=torch.float64)
         flat[:8] = torch.arange(8, dtype=torch.float64) * (rank + 1)
         flat[8] = b
         sync.allreduce_stats_(flat, b)
@@ -50,15 +51,24 @@ def _worker(rank, world, port, out_dir):
 
     dist.all_reduce = no_host_collective
     try:
-        flat = torch.zeros(9, dtype=torch.float64)
+        flat = torch.zeros(10, dtype=torch.float64)
         flat[8] = B
         res["capped_bound"] = capped.allreduce_stats_(flat, B)
         res["capped_count"] = float(flat[8])
+        res["over_none"] = int(capped.take_overflow())
         try:
             capped.rows_per_rank(10)
             res["over"] = 0
         except ValueError:
             res["over"] = 1
+        # one rank over capacity: no raise inside the collective (the other
+        # rank would hang in it); both ranks see the flag afterwards
+        flat = torch.zeros(10, dtype=torch.float64)
+        b_over = [12, 4][rank]
+        flat[8] = b_over
+        res["over_bound"] = capped.allreduce_stats_(flat, b_over)
+        res["over_flag"] = int(capped.take_overflow())
+        res["over_flag_after"] = int(capped.take_overflow())
     finally:
         dist.all_reduce = real
     # BN sums (fp64) and EMA statistic (int64) all-reduce
@@ -94,7 +104,9 @@ def test_codebook_sync_gloo_world2(tmp_path):
         np.testing.assert_array_equal(r[k]["max_seq"], [5, 7, 9])
         np.testing.assert_array_equal(r[k]["counts_seq"], [8.0, 9.0, 10.0])
         assert int(r[k]["capped_bound"]) == 9 and float(r[k]["capped_count"]) == 8.0
-        assert int(r[k]["over"]) == 1
+        assert int(r[k]["over"]) == 1 and int(r[k]["over_none"]) == 0
+        assert int(r[k]["over_bound"]) == 9
+        assert int(r[k]["over_flag"]) == 1 and int(r[k]["over_flag_after"]) == 0
         np.testing.assert_array_equal(r[k]["sums"], np.arange(8).reshape(4, 2) * 3.0)
         st = r[k]["stats"]
         assert st[0, 0, 0, 0] == 3 and st[0, 1, 2, 4] == 3 * (1 << 40)

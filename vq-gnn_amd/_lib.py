@@ -53,35 +53,15 @@ SIGNATURES = {
                                               _i64, _c_void_p, _c_void_p]),
     "vqgnn_scatter_codes": (ctypes.c_int, [_c_void_p, _i32, _c_void_p, _i32, _c_void_p, _i64,
                                            _c_void_p]),
-    "vqgnn_spmm_workspace": (_size, [_i32, _i64, _i32]),
-    "vqgnn_spmm": (ctypes.c_int, [_c_void_p, _c_void_p, _c_void_p, _i32, _i32, _i64, _i32,
-                                  _c_void_p, _i64, _c_void_p, _i64, _i32, _c_void_p, _i64,
-                                  _c_void_p, _c_void_p, _c_void_p]),
-    "vqgnn_spmm_codes_supported": (ctypes.c_int, [_i32, _i32, _i32, _i32]),
-    "vqgnn_spmm_codes": (ctypes.c_int, [_c_void_p, _c_void_p, _c_void_p, _i32, _i32, _i64, _i32,
-                                        _c_void_p, _i64, _c_void_p, _i64, _i32, _c_void_p, _i32,
-                                        _i32, _i32, _i64, _i32, _i32, _c_void_p, _i64,
-                                        _c_void_p, _c_void_p, _c_void_p]),
-    "vqgnn_spmm_pair_supported": (ctypes.c_int, [_i32]),
-    "vqgnn_spmm_pair_plan_size": (_i64, [_i32, _i64, _i32]),
-    "vqgnn_spmm_pair_plan_workspace": (_size, [_i32, _i64, _i32]),
-    "vqgnn_spmm_pair_plan": (ctypes.c_int, [_c_void_p, _i32, _i64, _i32, _i32, _c_void_p,
-                                            _c_void_p, _c_void_p]),
-    "vqgnn_spmm_pair": (ctypes.c_int, [_c_void_p, _c_void_p, _c_void_p, _i32, _i32, _i64, _i32,
-                                       _c_void_p, _i64, _c_void_p, _i64, _i32, _c_void_p, _i64,
-                                       _c_void_p, _c_void_p, _c_void_p, _c_void_p]),
     "vqgnn_spmm_task_size": (_i64, [_i64, _i32, _i32]),
     "vqgnn_spmm_task_plan": (ctypes.c_int, [_c_void_p, _c_void_p, _c_void_p, _i32, _i64, _i32,
                                             _c_void_p, _c_void_p, _c_void_p, _c_void_p]),
+    "vqgnn_spmm_task_records": (ctypes.c_int, [_c_void_p, _c_void_p, _c_void_p, _i32, _i64,
+                                               _c_void_p, _c_void_p]),
     "vqgnn_spmm_task_workspace": (_size, [_i64, _i32, _i32]),
     "vqgnn_spmm_task": (ctypes.c_int, [_c_void_p, _i32, _i32, _i64, _i32, _c_void_p, _i64,
                                        _c_void_p, _i64, _i32, _c_void_p, _i64, _c_void_p,
                                        _c_void_p, _i32, _i32, _i32, _c_void_p, _c_void_p]),
-    "vqgnn_spmm_task_codes_supported": (ctypes.c_int, [_i32, _i32, _i32, _i32]),
-    "vqgnn_spmm_task_codes": (ctypes.c_int, [_c_void_p, _i32, _i32, _i64, _i32, _c_void_p, _i64,
-                                             _c_void_p, _i64, _i32, _c_void_p, _i32, _i32, _i32,
-                                             _i64, _i32, _i32, _c_void_p, _i64, _c_void_p,
-                                             _c_void_p, _i32, _i32, _i32, _c_void_p, _c_void_p]),
     "vqgnn_spmm_task_acc": (ctypes.c_int, [_c_void_p, _i32, _i32, _i64, _i32, _c_void_p, _i64,
                                            _c_void_p, _i64, _i32, _c_void_p, _i64, _c_void_p,
                                            _c_void_p, _i32, _i32, _i32, _c_void_p, _c_void_p]),
@@ -106,8 +86,6 @@ SIGNATURES = {
                                            _c_void_p, _i32, _i32, _i32, _c_void_p, _c_void_p,
                                            _c_void_p, _c_void_p, _f32, _i32, _c_void_p,
                                            _c_void_p, _c_void_p, _c_void_p]),
-    "vqgnn_spmm_plan_size": (_i64, [_i64, _i32]),
-    "vqgnn_spmm_plan": (ctypes.c_int, [_c_void_p, _i32, _i64, _i32, _c_void_p, _c_void_p]),
     "vqgnn_csr_transpose_workspace": (_size, [_i32, _i32, _i64]),
     "vqgnn_csr_transpose": (ctypes.c_int, [_c_void_p, _c_void_p, _c_void_p, _i32, _i32, _i64,
                                            _c_void_p, _c_void_p, _c_void_p, _c_void_p,
@@ -162,8 +140,8 @@ SIGNATURES = {
     "vqgnn_codes_wire_record": (_i32, [_i32, _i32]),
     "vqgnn_pack_codes": (ctypes.c_int, [_c_void_p, _i32, _c_void_p, _i32, _i32, _i32, _c_void_p,
                                         _c_void_p, _i64, _c_void_p]),
-    "vqgnn_scatter_wire": (ctypes.c_int, [_c_void_p, _i64, _i32, _i32, _c_void_p, _i64, _c_void_p,
-                                          _i64, _c_void_p]),
+    "vqgnn_scatter_wire": (ctypes.c_int, [_c_void_p, _i64, _i32, _i32, _c_void_p, _i64, _i64,
+                                          _c_void_p, _i64, _c_void_p]),
     # §11 v1 compressed adjacency
     "vqgnn_mapper_capacity": (_i64, [_i64, _i64, _i32, _i32, _i32, _i32]),
     "vqgnn_mapper_workspace": (_size, [_i64, _i64, _i32, _i32, _i32]),

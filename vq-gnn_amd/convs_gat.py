@@ -12,7 +12,6 @@ The arithmetic runs in HIP (include/vqgnn.h §8):
   out       = sum_e coef_e * x_in[j]                       } fused kernel; the
   rows < B  : out /= sum_e coef_e + 1e-16                  } coefficients stay in
                                                               registers)
-(VQGNN_SPMM=chunk: vqgnn_gat_coef + vqgnn_spmm + vqgnn_gat_normalize.)
 
 The backward (dX for the batch rows, d att_l, d att_r) differentiates the same
 chain: the transposed-coefficient SpMM, vqgnn_gat_edge_grad for the
@@ -22,7 +21,6 @@ gradient, and the x_in^T d alpha reductions.
 from __future__ import annotations
 
 import math
-import os
 
 import torch
 from torch import nn
@@ -52,28 +50,17 @@ class GATFunction(torch.autograd.Function):
         al, ar, params = kernels.gat_alpha(xc, att_l, att_r, F, X2=x_first, B=B, ones=ones)
         # the fused attention path runs on the task plan (coefficients computed
         # per edge record), also for dense-block adjacencies
-        plan = adj.plan(F, B=B if x_first is not None else None,
-                        kind=None if os.environ.get("VQGNN_SPMM") == "chunk" else "task")
-        if isinstance(plan, kernels.TaskPlan):
-            # fused: coefficients, ones-column sums and the normalisation in the
-            # aggregation kernel; coef / den kept only when a backward follows
-            # (grad mode is off inside forward: ask the context what the
-            # backward will need)
-            grad = any(ctx.needs_input_grad[:4])
-            out, den, coef = kernels.gat_spmm(
-                adj.rowptr, adj.col, adj.value, n, nnz, xc, F, al, ar, params, plan, adj.rows(),
-                X2=x_first, B=B if x_first is not None else None,
-                norm_B=B if normalize else 0, negative_slope=slope, want_den=grad,
-                want_coef=grad)
-        else:                     # VQGNN_SPMM=chunk: coefficient pass + SpMM + normalise
-            coef, den = kernels.gat_coef(adj.rowptr, adj.col, adj.value, n, nnz, al, ar, params,
-                                         slope)
-            out = kernels.spmm(adj.rowptr, adj.col, coef, n, nnz, xc, F, X2=x_first,
-                               B=B if x_first is not None else None,
-                               plan=adj.plan(F, B=B if x_first is not None else None,
-                                             kind="chunk"))
-            if normalize:
-                kernels.gat_normalize(out, B, F, den, 1e-16)
+        plan = adj.plan(F, kind="task")
+        # fused: coefficients, ones-column sums and the normalisation in the
+        # aggregation kernel; coef / den kept only when a backward follows
+        # (grad mode is off inside forward: ask the context what the backward
+        # will need)
+        grad = any(ctx.needs_input_grad[:4])
+        out, den, coef = kernels.gat_spmm(
+            adj.rowptr, adj.col, adj.value, n, nnz, xc, F, al, ar, params, plan, adj.rows(),
+            X2=x_first, B=B if x_first is not None else None,
+            norm_B=B if normalize else 0, negative_slope=slope, want_den=grad,
+            want_coef=grad)
         ctx.save_for_backward(xc, x_first if x_first is not None else xc, att_l, att_r, al, ar,
                               params, coef, den, out)
         ctx.has_first = x_first is not None
@@ -138,8 +125,10 @@ class GATFunction(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             t = adj.transposed()
             tcoef = coef[adj.t_perm.long()]
-            # rows [0, B) of A_coef^T dy (the merge kernel bounds the walk by nnz)
-            dx = kernels.spmm(t.rowptr, t.col, tcoef, B, nnz, dy, F, plan=t.plan(F, n_rows=B, kind="chunk"))
+            # rows [0, B) of A_coef^T dy: the transpose's task plan with the
+            # coefficients as record weights (no new plan, no host read)
+            cplan = t.plan(F, kind="task").with_values(t.col, tcoef)
+            dx = kernels.spmm(t.rowptr, t.col, tcoef, B, nnz, dy, F, plan=cplan)
             dx += dal[:B, None] * att_l.view(-1)[:F] + dar[:B, None] * att_r.view(-1)[:F]
         return dx, None, d_att_l, d_att_r, None, None, None, None, None, None, None
 

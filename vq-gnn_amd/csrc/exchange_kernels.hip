@@ -8,9 +8,12 @@
 // them with "the last record wins" for a node several ranks hold — the order
 // of the union batch on one GPU (index_put with repeated indices writes in
 // order on the CPU).  The winner is chosen deterministically (an atomicMax of
-// the record index per node, then only the winner writes), so every replica
-// resolves repeats the same way; the per-node winner table returns to -1
-// after each scatter, so it needs one initialisation only.
+// the stamp epoch << 32 | record index per node, then only the winner
+// writes), so every replica resolves repeats the same way.  The epoch grows
+// with every exchange, so stamps of earlier exchanges are smaller than any of
+// this one and the table is never reset: no pass, no lane, no wave ever
+// writes it except the atomicMax (a reset by the winner lane raced with the
+// other lanes of the same record when they sat in another wave).
 
 #include "common.h"
 
@@ -87,22 +90,28 @@ __global__ void pack_codes8_kernel(const int64_t* __restrict__ batch_idx, int B,
   if (codes && node >= 0) *reinterpret_cast<uint4*>(codes + node * ldc + 8 * c) = t;
 }
 
+__device__ __forceinline__ unsigned long long wire_stamp(int64_t epoch, int64_t i) {
+  return ((unsigned long long)epoch << 32) | (unsigned long long)(uint32_t)i;
+}
+
 __global__ void wire_winner_kernel(const uint8_t* __restrict__ recv, int64_t n, int rec,
-                                   int64_t N, int32_t* __restrict__ winner) {
+                                   int64_t N, int64_t epoch,
+                                   unsigned long long* __restrict__ winner) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int32_t node = *reinterpret_cast<const int32_t*>(recv + i * rec);
-  if (node >= 0 && node < N) atomicMax(winner + node, (int32_t)i);
+  if (node >= 0 && node < N) atomicMax(winner + node, wire_stamp(epoch, i));
 }
 
 __global__ void wire_scatter_kernel(const uint8_t* __restrict__ recv, int64_t n, int rec, int nb,
-                                    int M, int64_t N, int32_t* __restrict__ winner,
+                                    int M, int64_t N, int64_t epoch,
+                                    const unsigned long long* __restrict__ winner,
                                     int16_t* __restrict__ codes, int64_t ldc, int vec) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint8_t* p = recv + i * rec;
   const int32_t node = *reinterpret_cast<const int32_t*>(p);
-  if (node < 0 || node >= N || winner[node] != (int32_t)i) return;
+  if (node < 0 || node >= N || winner[node] != wire_stamp(epoch, i)) return;
   int16_t* c = codes + (int64_t)node * ldc;
   if (vec) {
     const uint32_t* pw = reinterpret_cast<const uint32_t*>(p + 4);
@@ -117,14 +126,13 @@ __global__ void wire_scatter_kernel(const uint8_t* __restrict__ recv, int64_t n,
     const int16_t* q = reinterpret_cast<const int16_t*>(p + 4);
     for (int b = 0; b < nb; ++b) c[b] = q[b];
   }
-  winner[node] = -1;   // only the winner clears: the losers compare against any other value
 }
 
-// Thread (record, chunk of 8 codes).  The lanes of one record sit in one
-// wave and all read winner[node] before chunk 0's lane (after its compare)
-// returns the entry to -1.
+// Thread (record, chunk of 8 codes): the table is read-only here, so the
+// lanes of one record may sit in any wave or workgroup.
 __global__ void wire_scatter8_kernel(const uint8_t* __restrict__ recv, int64_t n, int rec,
-                                     int nb, int64_t N, int32_t* __restrict__ winner,
+                                     int nb, int64_t N, int64_t epoch,
+                                     const unsigned long long* __restrict__ winner,
                                      int16_t* __restrict__ codes, int64_t ldc) {
   const int ch = nb >> 3;
   const int64_t tix = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -133,13 +141,12 @@ __global__ void wire_scatter8_kernel(const uint8_t* __restrict__ recv, int64_t n
   const int c = (int)(tix % ch);
   const uint8_t* p = recv + i * rec;
   const int32_t node = *reinterpret_cast<const int32_t*>(p);
-  if (node < 0 || node >= N || winner[node] != (int32_t)i) return;
+  if (node < 0 || node >= N || winner[node] != wire_stamp(epoch, i)) return;
   const uint32_t* pw = reinterpret_cast<const uint32_t*>(p + 4 + 8 * c);
   const uint32_t w0 = pw[0], w1 = pw[1];
   *reinterpret_cast<uint4*>(codes + (int64_t)node * ldc + 8 * c) =
       make_uint4((w0 & 0xFFu) | ((w0 >> 8 & 0xFFu) << 16), (w0 >> 16 & 0xFFu) | ((w0 >> 24) << 16),
                  (w1 & 0xFFu) | ((w1 >> 8 & 0xFFu) << 16), (w1 >> 16 & 0xFFu) | ((w1 >> 24) << 16));
-  if (c == 0) winner[node] = -1;
 }
 
 }  // namespace vqgnn
@@ -176,24 +183,28 @@ extern "C" int vqgnn_pack_codes(const int64_t* batch_idx, int32_t B, const int16
 }
 
 extern "C" int vqgnn_scatter_wire(const uint8_t* recv, int64_t n_records, int32_t nb, int32_t M,
-                                  int32_t* winner, int64_t N, int16_t* codes, int64_t ldc,
-                                  vqgnn_stream_t stream) {
+                                  int64_t* winner, int64_t epoch, int64_t N, int16_t* codes,
+                                  int64_t ldc, vqgnn_stream_t stream) {
   clear_error();
-  VQGNN_REQUIRE(n_records >= 0 && nb > 0 && M > 0 && N >= 0, "scatter_wire: bad shape");
+  VQGNN_REQUIRE(n_records >= 0 && n_records < ((int64_t)1 << 32) && nb > 0 && M > 0 && N >= 0,
+                "scatter_wire: bad shape");
+  VQGNN_REQUIRE(epoch >= 1 && epoch < ((int64_t)1 << 31), "scatter_wire: epoch %lld outside [1, 2^31)",
+                (long long)epoch);
   if (n_records == 0) return VQGNN_OK;
   VQGNN_REQUIRE(recv && winner && codes, "scatter_wire: null pointer");
   const int rec = wire_record_bytes(nb, M);
+  unsigned long long* win = reinterpret_cast<unsigned long long*>(winner);
   const dim3 grid((unsigned)((n_records + 255) / 256));
   hipLaunchKernelGGL(wire_winner_kernel, grid, dim3(256), 0, as_stream(stream), recv, n_records,
-                     rec, N, winner);
+                     rec, N, epoch, win);
   if (M <= 256 && nb % 8 == 0 && ((uintptr_t)codes & 15) == 0 && ldc % 8 == 0) {
     const int64_t nt = n_records * (nb / 8);
     hipLaunchKernelGGL(wire_scatter8_kernel, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0,
-                       as_stream(stream), recv, n_records, rec, nb, N, winner, codes, ldc);
+                       as_stream(stream), recv, n_records, rec, nb, N, epoch, win, codes, ldc);
     return check_launch("scatter_wire");
   }
   const int vec = M <= 256 && nb % 4 == 0 && ((uintptr_t)codes & 7) == 0 && ldc % 4 == 0;
   hipLaunchKernelGGL(wire_scatter_kernel, grid, dim3(256), 0, as_stream(stream), recv, n_records,
-                     rec, nb, M, N, winner, codes, ldc, vec);
+                     rec, nb, M, N, epoch, win, codes, ldc, vec);
   return check_launch("scatter_wire");
 }

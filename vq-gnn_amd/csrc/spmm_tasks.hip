@@ -80,17 +80,6 @@ struct TaskArgs {
   float* coef;              // [nnz] optional: the coefficients (for the backward)
 };
 
-// Code-source column tiles (vqgnn_spmm_task_codes): a column j >= B is the
-// codeword row concat_b emb[b][lcodes[j - B][b]][off .. off + 4), read as one
-// 2-byte code per branch plus the tile's codebook entries staged in LDS
-struct CodeTile {
-  const int16_t* lcodes;    // [n_cols - B][ldlc]
-  uint32_t ldlcb, lcspan;   // bytes per lcodes row, bytes of lcodes
-  const float* emb;         // [nb][M][ldw] (branch stride bstride floats)
-  int64_t bstride;
-  int ldw, off, M, nb;
-};
-
 __device__ __forceinline__ int upper_bound_i32(const int32_t* __restrict__ a, int n, int key) {
   // first i in [0, n] with a[i] > key  (a non-decreasing, n + 1 entries read)
   int lo = 0, hi = n + 1;
@@ -207,12 +196,8 @@ __device__ __forceinline__ float gat_edge_coef(const TaskArgs& a, int e, uint32_
 // PART (near path): the last column tile is partial (F/4 not a multiple of
 // G*NC): its lanes past F load nothing (an offset past the buffer range
 // returns 0 without a memory access) instead of reading the next row
-// CODES (near, NC = 1, G = one lane per branch): columns >= B read a code
-// and the LDS codebook entry `cbs` of the lane's branch instead of a row
-template <int G, int NC, int U, bool FAR, bool GAT, bool PART, bool CODES>
-__device__ __forceinline__ void task_walk(const TaskArgs& a, const CodeTile& ct,
-                                          const float* __restrict__ cbs, int wv, int nwaves) {
-  static_assert(!CODES || (NC == 1 && !FAR && !GAT && !PART), "code tiles: near, one piece");
+template <int G, int NC, int U, bool FAR, bool GAT, bool PART>
+__device__ __forceinline__ void task_walk(const TaskArgs& a, int wv, int nwaves) {
   constexpr int TPW = 64 / G;
   const int lane = threadIdx.x & 63;
   const int g = lane / G, k = lane % G;
@@ -220,7 +205,11 @@ __device__ __forceinline__ void task_walk(const TaskArgs& a, const CodeTile& ct,
   // a call over the first n_rows rows of a larger CSR (the backward's
   // transpose restricted to batch rows) covers edges [0, rowptr[n_rows])
   const int nnz = min(a.nnz, a.rowptr[a.n_rows]);
-  if (wv >= nwaves || wv * TPW >= a.ntasks || a.task_start[wv * TPW] >= nnz) return;
+  if (wv >= nwaves || wv * TPW >= a.ntasks) return;
+  // the wave's records are addressed from its first task's first edge: 32-bit
+  // buffer offsets cover any nnz < 2^31 (a wave spans at most 64 tasks)
+  const int wbase = a.task_start[wv * TPW];
+  if (wbase >= nnz) return;
   const bool tv = t < a.ntasks;
   const int e0 = tv ? min(a.task_start[t], nnz) : nnz;
   const bool valid = e0 < nnz;
@@ -244,10 +233,8 @@ __device__ __forceinline__ void task_walk(const TaskArgs& a, const CodeTile& ct,
   const __amdgpu_buffer_rsrc_t rsx =
       __builtin_amdgcn_make_buffer_rsrc((void*)a.ubase, 0, FAR ? 0 : (int)a.span, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsr = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)a.rec, 0, (int)(uint32_t)min((int64_t)a.nnz * 8, (int64_t)0x7FFFFFFF), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rsc =
-      __builtin_amdgcn_make_buffer_rsrc((void*)ct.lcodes, 0, (int)ct.lcspan, 0x00020000);
-  const uint32_t coff = (uint32_t)c4base * 2u;          // CODES: this lane's branch
+      (void*)(a.rec + wbase), 0,
+      (int)(uint32_t)min((int64_t)(a.nnz - wbase) * 8, (int64_t)0x7FFFFFFF), 0x00020000);
 
   float4 acc[NC];
 #pragma unroll
@@ -265,7 +252,7 @@ __device__ __forceinline__ void task_walk(const TaskArgs& a, const CodeTile& ct,
   // so no wait for it sits between a block's gathers and the next block's.
   auto load_rec = [&](int e) -> int2 {
     return __builtin_bit_cast(
-        int2, __builtin_amdgcn_raw_buffer_load_b64(rsr, (uint32_t)(e + k) * 8u, 0, 0));
+        int2, __builtin_amdgcn_raw_buffer_load_b64(rsr, (uint32_t)(e - wbase + k) * 8u, 0, 0));
   };
   auto mask_rec = [&](int2 q, int e) -> int2 {
     const int eu = e + k;
@@ -298,32 +285,6 @@ __device__ __forceinline__ void task_walk(const TaskArgs& a, const CodeTile& ct,
     group_bcast<kAnd>(rcur.x, cx, std::make_integer_sequence<int, U>{});
     group_bcast<kAnd>(rcur.y, cw, std::make_integer_sequence<int, U>{});
     float4 v[U][NC];
-    if constexpr (CODES) {
-      // codes first (the LDS reads wait only for them), then the X rows of
-      // columns < B; each source's offset is pushed past its range (a load
-      // of 0 without a memory access) for the other kind of column
-      uint32_t cd[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const uint32_t j = (uint32_t)cx[u] & kColMask;
-        const uint32_t o = (int)j < a.B ? 0x80000000u : __umul24(j - (uint32_t)a.B, ct.ldlcb) + coff;
-        cd[u] = __builtin_amdgcn_raw_buffer_load_b16(rsc, o, 0, 0);
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {   // exec-masked: most steps have no X column at all
-        const uint32_t x = (uint32_t)cx[u];
-        v[u][0] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if ((int)(x & kColMask) < a.B)
-          v[u][0] = __builtin_bit_cast(
-              float4, __builtin_amdgcn_raw_buffer_load_b128(rsx, __umul24(x, a.ldxb) + b1, 0, 0));
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const uint32_t m = min(cd[u], (uint32_t)ct.M - 1u);
-        const float4 q = *reinterpret_cast<const float4*>(cbs + 4 * (k * ct.M + (int)m));
-        if ((int)((uint32_t)cx[u] & kColMask) >= a.B) v[u][0] = q;
-      }
-    } else {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       uint32_t off = 0;
@@ -339,7 +300,6 @@ __device__ __forceinline__ void task_walk(const TaskArgs& a, const CodeTile& ct,
           v[u][i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsx, o, 0, 0));
         }
       }
-    }
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -401,8 +361,8 @@ __device__ __forceinline__ void task_walk(const TaskArgs& a, const CodeTile& ct,
   }
   // the task's last row continues in the next task unless its last edge ends
   // a row (records outside the task carry no row end)
-  const bool open = valid && !(__builtin_amdgcn_raw_buffer_load_b32(rsr, (uint32_t)(e1 - 1) * 8u, 0, 0) &
-                               (int)kEndBit);
+  const bool open = valid && !(__builtin_amdgcn_raw_buffer_load_b32(rsr, (uint32_t)(e1 - 1 - wbase) * 8u,
+                                                                    0, 0) & (int)kEndBit);
   if (open) {
     float* dst = a.carry + ((int64_t)t * 2 + 1) * a.cf;
 #pragma unroll
@@ -419,34 +379,7 @@ __global__ void __launch_bounds__(kTaskThreads)
 spmm_task_kernel(TaskArgs a) {
   const int nwaves = (int)gridDim.x * (kTaskThreads / 64);
   const int wv = xcd_remap(blockIdx.x, gridDim.x) * (kTaskThreads / 64) + (threadIdx.x >> 6);
-  task_walk<G, NC, U, FAR, GAT, PART, false>(a, CodeTile{}, nullptr, wv, nwaves);
-}
-
-// Code-source tiles: a workgroup per (CU, column tile of kCodeBranches
-// branches) stages the tile's codebook entries (kCodeBranches x M float4)
-// once, then its waves walk a contiguous range of task waves
-constexpr int kCodeThreads = 1024;
-constexpr int kCodeBranches = 8;
-template <int U>
-__global__ void __launch_bounds__(kCodeThreads)
-spmm_task_codes_kernel(TaskArgs a, CodeTile ct) {
-  extern __shared__ float4 cb4[];
-  const int tile = blockIdx.y;
-  for (int i = threadIdx.x; i < kCodeBranches * ct.M; i += kCodeThreads) {
-    const int bl = i / ct.M, m = i - bl * ct.M;
-    const int b = tile * kCodeBranches + bl;
-    cb4[i] = b < ct.nb ? *reinterpret_cast<const float4*>(ct.emb + b * ct.bstride +
-                                                          (int64_t)m * ct.ldw + ct.off)
-                       : make_float4(0.f, 0.f, 0.f, 0.f);
-  }
-  __syncthreads();
-  constexpr int TPW = 64 / kCodeBranches;
-  const int nw = (a.ntasks + TPW - 1) / TPW;
-  const int per = (nw + (int)gridDim.x - 1) / (int)gridDim.x;
-  const int w0 = (int)blockIdx.x * per, w1 = min(nw, w0 + per);
-  for (int wv = w0 + (int)(threadIdx.x >> 6); wv < w1; wv += kCodeThreads / 64)
-    task_walk<kCodeBranches, 1, U, false, false, false, true>(
-        a, ct, reinterpret_cast<const float*>(cb4), wv, nw);
+  task_walk<G, NC, U, FAR, GAT, PART>(a, wv, nwaves);
 }
 
 // One wave per fix-up job.  A cut row: out[row] = tail[ts] + ... + tail[t-1]
@@ -576,6 +509,27 @@ extern "C" int64_t vqgnn_spmm_task_size(int64_t nnz, int32_t K, int32_t n_rows) 
   return 5 * (int64_t)task_count(nnz, K) + 1 + (n_rows > 0 ? n_rows : 0);
 }
 
+static void task_records(const int32_t* rowptr, const int32_t* col, const float* val,
+                         int32_t n_rows, int64_t nnz, int2* rec, hipStream_t s) {
+  if (nnz <= 0) return;
+  hipLaunchKernelGGL(task_records_kernel, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s,
+                     col, val, (int)nnz, rec);
+  if (n_rows > 0)
+    hipLaunchKernelGGL(task_row_ends_kernel, dim3((n_rows + 255) / 256), dim3(256), 0, s, rowptr,
+                       n_rows, rec);
+}
+
+extern "C" int vqgnn_spmm_task_records(const int32_t* rowptr, const int32_t* col, const float* val,
+                                       int32_t n_rows, int64_t nnz, int64_t* records,
+                                       vqgnn_stream_t stream) {
+  clear_error();
+  VQGNN_REQUIRE(rowptr && n_rows >= 0 && nnz >= 0 && nnz < (int64_t)1 << 31,
+                "spmm_task_records: bad arguments");
+  VQGNN_REQUIRE(nnz == 0 || (col && records), "spmm_task_records: null pointer");
+  task_records(rowptr, col, val, n_rows, nnz, reinterpret_cast<int2*>(records), as_stream(stream));
+  return check_launch("spmm_task_records");
+}
+
 extern "C" int vqgnn_spmm_task_plan(const int32_t* rowptr, const int32_t* col, const float* val,
                                     int32_t n_rows, int64_t nnz, int32_t K, int32_t* plan,
                                     int64_t* records, int32_t* counts, vqgnn_stream_t stream) {
@@ -593,14 +547,7 @@ extern "C" int vqgnn_spmm_task_plan(const int32_t* rowptr, const int32_t* col, c
   int32_t* empties = jobs + 3 * ntasks;
   if (hipMemsetAsync(counts, 0, 2 * sizeof(int32_t), s) != hipSuccess)
     return check_launch("spmm_task_plan memset");
-  int2* rec = reinterpret_cast<int2*>(records);
-  if (nnz > 0) {
-    hipLaunchKernelGGL(task_records_kernel, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0, s,
-                       col, val, (int)nnz, rec);
-    if (n_rows > 0)
-      hipLaunchKernelGGL(task_row_ends_kernel, dim3((n_rows + 255) / 256), dim3(256), 0, s,
-                         rowptr, n_rows, rec);
-  }
+  task_records(rowptr, col, val, n_rows, nnz, reinterpret_cast<int2*>(records), s);
   hipLaunchKernelGGL(task_first_row_kernel, dim3((ntasks + 256) / 256), dim3(256), 0, s, rowptr,
                      n_rows, (int)nnz, K, task_env("VQGNN_TASK_SNAP", 1) ? K / 2 : 0, ntasks,
                      task_start, task_row);
@@ -784,75 +731,4 @@ extern "C" int vqgnn_gat_spmm_task(const int32_t* rowptr, int32_t n_rows, int32_
   a.coef = coef;
   task_launch<true>(a, near, as_stream(stream));
   return check_launch("gat_spmm_task");
-}
-
-extern "C" int vqgnn_spmm_task_codes_supported(int32_t F, int32_t nb, int32_t M, int32_t D) {
-  return D == 4 && nb > 0 && F == nb * D && M > 0 &&
-         (size_t)kCodeBranches * M * 16 <= 160 * 1024;
-}
-
-extern "C" int vqgnn_spmm_task_codes(const int32_t* rowptr, int32_t n_rows, int32_t n_cols,
-                                     int64_t nnz, int32_t B, const float* X, int64_t ldx,
-                                     const int16_t* lcodes, int64_t ldlc, int32_t nb,
-                                     const float* emb, int32_t M, int32_t D, int32_t ldw,
-                                     int64_t emb_bstride, int32_t col_offset, int32_t F,
-                                     float* out, int64_t ldo, const int32_t* plan,
-                                     const int64_t* records, int32_t K, int32_t n_jobs,
-                                     int32_t n_empty, void* workspace, vqgnn_stream_t stream) {
-  clear_error();
-  if (!vqgnn_spmm_task_codes_supported(F, nb, M, D)) {
-    set_error("spmm_task_codes: F=%d nb=%d M=%d D=%d: needs D = 4, F = 4 nb, M <= 1280", F, nb,
-              M, D);
-    return VQGNN_ERR_UNSUPPORTED;
-  }
-  VQGNN_REQUIRE(B >= 0 && B <= n_cols && n_cols < (1 << 24), "spmm_task_codes: B=%d, n_cols=%d",
-                B, n_cols);
-  VQGNN_REQUIRE(nnz == 0 || B == n_cols || (lcodes && emb), "spmm_task_codes: null pointer");
-  VQGNN_REQUIRE(ldlc >= nb && (int64_t)(n_cols - B) * ldlc * 2 < ((int64_t)1 << 31),
-                "spmm_task_codes: lcodes layout (ldlc=%lld)", (long long)ldlc);
-  VQGNN_REQUIRE(ldw % 4 == 0 && col_offset % 4 == 0 && emb_bstride % 4 == 0 &&
-                    ((uintptr_t)emb & 15) == 0 && col_offset + D <= ldw,
-                "spmm_task_codes: codebook rows must be 16-byte aligned");
-  if (!X) X = out;                       // B = 0: no X row is ever read
-  TaskArgs a{};
-  bool near = false;
-  // the X rows alone form the near range (columns >= B never address it)
-  const int rc = task_setup(a, rowptr, n_rows, B, nnz, B, X, ldx, X, ldx, F, out, ldo, plan,
-                            records, K, n_jobs, n_empty, workspace, &near);
-  if (rc != VQGNN_OK) return rc;
-  VQGNN_REQUIRE(near, "spmm_task_codes: X / out outside the 32-bit near path");
-  a.B = B;
-  hipStream_t s = as_stream(stream);
-  if (nnz > 0) {
-    CodeTile ct{};
-    ct.lcodes = lcodes;
-    ct.ldlcb = (uint32_t)(ldlc * 2);
-    ct.lcspan = (uint32_t)((int64_t)(n_cols - B) * ldlc * 2);
-    ct.emb = emb;
-    ct.bstride = emb_bstride;
-    ct.ldw = ldw;
-    ct.off = col_offset;
-    ct.M = M;
-    ct.nb = nb;
-    int dev = 0, ncu = 256;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      ncu = 256;
-    const size_t lds = (size_t)kCodeBranches * M * 16;
-    const int tiles = (nb + kCodeBranches - 1) / kCodeBranches;
-    const int Ue = task_env("VQGNN_TASK_U", 8);
-    const dim3 grid((unsigned)ncu, (unsigned)tiles);
-#define VQ_CODES(UU)                                                                           \
-  do {                                                                                         \
-    (void)hipFuncSetAttribute((const void*)spmm_task_codes_kernel<UU>,                        \
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);          \
-    hipLaunchKernelGGL(spmm_task_codes_kernel<UU>, grid, dim3(kCodeThreads), lds, s, a, ct);  \
-  } while (0)
-    if (Ue >= 8) VQ_CODES(8);
-    else if (Ue >= 4) VQ_CODES(4);
-    else VQ_CODES(2);
-#undef VQ_CODES
-  }
-  task_fixup<false>(a, s);
-  return check_launch("spmm_task_codes");
 }

@@ -30,7 +30,15 @@ class CodebookSync:
     statistic uses world * capacity as its row bound, and the code exchange
     pads to capacity rows.  Without it every update first agrees on max(B)
     with one blocking all-reduce (correct for any batch sizes, but a host
-    round trip per call)."""
+    round trip per call).
+
+    Exactness: the EMA statistic is an exact int64 sum at every world size,
+    but its fixed-point resolution follows the row bound (world * capacity,
+    or world * max(B)), so the codebooks are bit-identical to one process on
+    the union batch only when that bound equals the one process's row count
+    (capacity == every rank's B); otherwise they differ by the rounding of
+    the normalised values to the coarser grid (include/vqgnn.h §3), within
+    the EMA tolerance the tests use."""
 
     def __init__(self, group=None, count_group=None, capacity=None):
         self.group = group
@@ -39,8 +47,10 @@ class CodebookSync:
         self.count_group = count_group
         self.world = dist.get_world_size(group)
         self.capacity = None if capacity is None else int(capacity)
+        self._overflow = None  # device sum of the over-capacity flags (allreduce_stats_)
         self._wire = {}       # persistent code-exchange buffers per shape
         self._inflight = {}   # buffer key -> the PendingWire still reading them
+        self._epoch = {}      # buffer key -> exchanges issued on its winner table
 
     def allreduce_(self, t: torch.Tensor, async_op: bool = False):
         """In-place sum over the ranks; async_op=True returns the work (its
@@ -58,11 +68,31 @@ class CodebookSync:
         return self.global_max(B)
 
     def allreduce_stats_(self, sums: torch.Tensor, B: int) -> int:
-        """All-reduce the fp64 BatchNorm sums in place ([4F + 1] with the row
-        count last: bn_finalize(count=0) reads the global count on the device)
-        -> the per-rank row bound (rows_per_rank)."""
+        """All-reduce the fp64 BatchNorm sums in place ([4F + 2]: the row count
+        at 4F, read on the device by bn_finalize(count=0), and at 4F + 1 the
+        number of ranks whose batch exceeds ``capacity``) -> the per-rank row
+        bound.  A rank over capacity does not raise here (the other ranks
+        would wait in this collective forever): the flag travels with the
+        sums, so every rank raises together at the next 'Bad Init!' check
+        (take_overflow), after the update's collectives all completed."""
+        if self.capacity is not None and B > self.capacity:
+            sums[-1:].fill_(1.0)
         self.allreduce_(sums)
-        return self.rows_per_rank(B)
+        if self.capacity is not None:
+            if self._overflow is None:
+                self._overflow = torch.zeros(1, dtype=sums.dtype, device=sums.device)
+            self._overflow.add_(sums[-1:])
+            return self.capacity
+        return self.global_max(B)
+
+    def take_overflow(self) -> bool:
+        """True (on every rank alike) when some rank's batch exceeded capacity
+        in an update since the last call; one device read."""
+        if self._overflow is None:
+            return False
+        over = float(self._overflow.item()) > 0
+        self._overflow.zero_()
+        return over
 
     def global_count(self, B: int) -> int:
         """Sum of B over the ranks (a blocking host collective; not on the
@@ -128,9 +158,14 @@ class CodebookSync:
         if prev is not None:
             prev.wait()
         send, recv, winner = self._wire_buffers(key)
+        epoch = self._epoch.get(key, 0) + 1
+        if epoch >= (1 << 31):              # stamps are epoch << 32 | record: restart
+            winner.zero_()
+            epoch = 1
+        self._epoch[key] = epoch
         kernels.pack_codes(batch_idx, local, M, max_B, send, codes=codes)
         work = dist.all_gather_into_tensor(recv, send, group=self.group, async_op=True)
-        pend = PendingWire(work, recv, self.world * max_B, nb, M, winner, codes)
+        pend = PendingWire(work, recv, self.world * max_B, nb, M, winner, codes, epoch)
         self._inflight[key] = pend
         return pend
 
@@ -141,7 +176,8 @@ class CodebookSync:
             rec = kernels.codes_wire_record(nb, M)
             send = torch.empty(max_B * rec, dtype=torch.uint8, device=device)
             recv = torch.empty(self.world * max_B * rec, dtype=torch.uint8, device=device)
-            winner = torch.full((N,), -1, dtype=torch.int32, device=device)
+            # stamp table of the scatter's "last record wins" (int64, never reset)
+            winner = torch.zeros(N, dtype=torch.int64, device=device)
             buf = self._wire[key] = (send, recv, winner)
         return buf
 
@@ -170,15 +206,16 @@ class PendingCodes:
 class PendingWire:
     """An in-flight all_gather of packed code records (start_codes_exchange)."""
 
-    def __init__(self, work, recv, n_records, nb, M, winner, codes):
+    def __init__(self, work, recv, n_records, nb, M, winner, codes, epoch):
         self.work, self.recv, self.n, self.nb, self.M = work, recv, n_records, nb, M
-        self.winner, self.codes = winner, codes
+        self.winner, self.codes, self.epoch = winner, codes, epoch
 
     def wait(self):
         if self.work is not None:
             self.work.wait()
             self.work = None
-            kernels.scatter_wire(self.recv, self.n, self.nb, self.M, self.winner, self.codes)
+            kernels.scatter_wire(self.recv, self.n, self.nb, self.M, self.winner, self.codes,
+                                 self.epoch)
 
 
 def _device_of(group):

@@ -37,19 +37,21 @@ def bn_arith_of(t: torch.Tensor, D: int) -> int:
 def bn_stats(X: torch.Tensor, G: torch.Tensor | None, F: int,
              with_count: bool = False) -> torch.Tensor:
     """fp64 column sums [4, F]: sum x, sum x^2, sum g, sum g^2 (vq.py:162/223).
-    with_count: a flat [4F + 1] buffer whose last element is the row count B
-    (summed with the statistics by the multi-GPU all-reduce; bn_finalize with
-    count=0 reads it on the device)."""
+    with_count: a flat [4F + 2] buffer: element 4F is the row count B (summed
+    with the statistics by the multi-GPU all-reduce; bn_finalize with count=0
+    reads it on the device), element 4F + 1 the over-capacity flag
+    (CodebookSync.allreduce_stats_), 0 here."""
     require_gpu(X, "bn_stats")
     B = X.shape[0]
     L = lib()
     ws = workspace(L.vqgnn_bn_stats_workspace(B, F), X.device)
-    flat = torch.empty(4 * F + int(with_count), dtype=torch.float64, device=X.device)
+    flat = torch.empty(4 * F + 2 * int(with_count), dtype=torch.float64, device=X.device)
     sums = flat[:4 * F].view(4, F)
     if G is None:
         sums[2:].zero_()
     if with_count:
-        flat[4 * F:].fill_(float(B))
+        flat[4 * F:].fill_(0.0)
+        flat[4 * F:4 * F + 1].fill_(float(B))
     check(L.vqgnn_bn_stats(ptr(X), _ld(X), ptr(G), _ld(G) if G is not None else 0, B, F,
                            int(G is not None), ptr(sums), ptr(ws), stream_ptr()), "bn_stats")
     return flat if with_count else sums
@@ -230,11 +232,15 @@ def pack_codes(batch_idx, local, M, max_B, send, codes=None):
                                  stream_ptr()), "pack_codes")
 
 
-def scatter_wire(recv, n_records, nb, M, winner, codes):
-    """All ranks' records into ``codes``; the last record of a node wins."""
+def scatter_wire(recv, n_records, nb, M, winner, codes, epoch):
+    """All ranks' records into ``codes``; the last record of a node wins.
+    winner: int64 [N] stamp table, zero-initialised once; epoch: 1, 2, ... per
+    call on the same table (include/vqgnn.h §5b)."""
+    if winner.dtype != torch.int64 or winner.numel() < codes.shape[0]:
+        raise ValueError("scatter_wire: winner must be an int64 [N] stamp table")
     check(lib().vqgnn_scatter_wire(ptr(recv), int(n_records), int(nb), int(M), ptr(winner),
-                                   codes.shape[0], ptr(codes), codes.stride(0), stream_ptr()),
-          "scatter_wire")
+                                   int(epoch), codes.shape[0], ptr(codes), codes.stride(0),
+                                   stream_ptr()), "scatter_wire")
 
 
 def scatter_codes(batch_idx: torch.Tensor, local: torch.Tensor, codes: torch.Tensor) -> None:
@@ -244,53 +250,31 @@ def scatter_codes(batch_idx: torch.Tensor, local: torch.Tensor, codes: torch.Ten
                                     codes.stride(0), stream_ptr()), "scatter_codes")
 
 
-def spmm_plan(rowptr, n_rows, nnz, F):
-    """Chunk plan of a CSR for vqgnn_spmm (include/vqgnn.h §6b)."""
-    L = lib()
-    m = L.vqgnn_spmm_plan_size(int(nnz), int(F))
-    plan = torch.empty(max(m, 1), dtype=torch.int32, device=rowptr.device)
-    check(L.vqgnn_spmm_plan(ptr(rowptr), int(n_rows), int(nnz), int(F), ptr(plan),
-                            stream_ptr()), "spmm_plan")
-    return plan
-
-
-class PairPlan:
-    """Segment plan of a CSR for vqgnn_spmm_pair (include/vqgnn.h §6d): built
-    for feature width F, batch split B and rows [0, n_rows); ``chunk`` is the
-    chunk plan (§6b) the call falls back to when X and X2 are far apart."""
-
-    def __init__(self, buf, F, B, n_rows, chunk=None):
-        self.buf, self.F, self.B, self.n_rows, self.chunk = buf, F, B, n_rows, chunk
-
-
-def spmm_pair_supported(F) -> bool:
-    return bool(lib().vqgnn_spmm_pair_supported(int(F)))
-
-
-def spmm_pair_plan(rowptr, n_rows, nnz, F, B, chunk=None):
-    """Build the segment-pair plan (device-side, once per batch adjacency)."""
-    L = lib()
-    dev = rowptr.device
-    m = L.vqgnn_spmm_pair_plan_size(int(n_rows), int(nnz), int(F))
-    buf = torch.empty(max(m, 1), dtype=torch.int32, device=dev)
-    ws = workspace(L.vqgnn_spmm_pair_plan_workspace(int(n_rows), int(nnz), int(F)), dev)
-    check(L.vqgnn_spmm_pair_plan(ptr(rowptr), int(n_rows), int(nnz), int(F), int(B), ptr(buf),
-                                 ptr(ws), stream_ptr()), "spmm_pair_plan")
-    return PairPlan(buf, int(F), int(B), int(n_rows), chunk)
-
-
 class TaskPlan:
-    """Task plan of a CSR for vqgnn_spmm_task (include/vqgnn.h §6e): per-edge
+    """Task plan of a CSR for vqgnn_spmm_task (include/vqgnn.h §6): per-edge
     records (column, row-end flag, weight), the tasks' first edges and rows,
     and the fix-up jobs (cut rows, empty rows); built once per batch
     adjacency, valid for any F and any leading row count.  Building it reads
     the two job counts back to the host (one sync per plan)."""
 
-    def __init__(self, plan, records, K, nnz, n_rows, val, n_jobs, n_empty):
+    def __init__(self, plan, records, K, nnz, n_rows, val, n_jobs, n_empty, rowptr=None):
         self.plan, self.records, self.K = plan, records, K
         self.nnz, self.n_rows = nnz, n_rows
         self.val_ptr = val.data_ptr() if val is not None else 0
         self.n_jobs, self.n_empty = n_jobs, n_empty
+        self.rowptr = rowptr
+
+    def with_values(self, col, val, records=None):
+        """The same plan over other edge values on the same structure (GAT's
+        coefficients): new records only (vqgnn_spmm_task_records, no host
+        read); ``records`` may be a reused int64 [nnz] buffer."""
+        if records is None:
+            records = torch.empty(max(self.nnz, 1), dtype=torch.int64, device=val.device)
+        check(lib().vqgnn_spmm_task_records(ptr(self.rowptr), ptr(col), ptr(val), self.n_rows,
+                                            self.nnz, ptr(records), stream_ptr()),
+              "spmm_task_records")
+        return TaskPlan(self.plan, records, self.K, self.nnz, self.n_rows, val, self.n_jobs,
+                        self.n_empty, self.rowptr)
 
 
 TASK_K = 64
@@ -372,7 +356,7 @@ def spmm_task_plan(rowptr, col, val, n_rows, nnz, K=None):
                                  ptr(plan), ptr(records), ptr(counts), stream_ptr()),
           "spmm_task_plan")
     n_jobs, n_empty = (int(v) for v in counts.tolist())
-    return TaskPlan(plan, records, K, int(nnz), int(n_rows), val, n_jobs, n_empty)
+    return TaskPlan(plan, records, K, int(nnz), int(n_rows), val, n_jobs, n_empty, rowptr)
 
 
 def spmm(rowptr, col, val, n_rows, nnz, X, F, X2=None, B=None, out=None, plan=None):
@@ -390,6 +374,8 @@ def spmm(rowptr, col, val, n_rows, nnz, X, F, X2=None, B=None, out=None, plan=No
     n_cols = Bv + X2.shape[0] if X2 is not None else X.shape[0]
     if X2 is not None and X.shape[0] < Bv:
         raise ValueError(f"spmm: X has {X.shape[0]} rows < B={Bv}")
+    if plan is None:            # a one-off product: plan it here (one host read)
+        plan = spmm_task_plan(rowptr, col, val, rowptr.numel() - 1, nnz)
     if isinstance(plan, TilePlan):
         if (val.data_ptr() if val is not None else 0) != plan.val_ptr:
             raise ValueError("spmm: the tile plan's records hold other values than val")
@@ -421,107 +407,7 @@ def spmm(rowptr, col, val, n_rows, nnz, X, F, X2=None, B=None, out=None, plan=No
                                 _ld(out), ptr(plan.plan), ptr(plan.records), plan.K,
                                 plan.n_jobs, plan.n_empty, ptr(ws), stream_ptr()), "spmm_task")
         return out
-    ws = workspace(L.vqgnn_spmm_workspace(n_rows, nnz, F), dev)
-    if isinstance(plan, PairPlan):
-        if plan.F != F or plan.n_rows != int(n_rows):
-            raise ValueError(f"spmm: pair plan built for F={plan.F}, n_rows={plan.n_rows}; "
-                             f"called with F={F}, n_rows={n_rows}")
-        check(L.vqgnn_spmm_pair(ptr(rowptr), ptr(col), ptr(val), int(n_rows), int(n_cols),
-                                int(nnz), Bv, ptr(X), _ld(X), ptr(X2),
-                                _ld(X2) if X2 is not None else 0, F, ptr(out), _ld(out),
-                                ptr(plan.buf), ptr(plan.chunk), ptr(ws), stream_ptr()),
-              "spmm_pair")
-        return out
-    check(L.vqgnn_spmm(ptr(rowptr), ptr(col), ptr(val), int(n_rows), int(n_cols), int(nnz), Bv,
-                       ptr(X), _ld(X),
-                       ptr(X2), _ld(X2) if X2 is not None else 0, F, ptr(out), _ld(out),
-                       ptr(plan), ptr(ws), stream_ptr()), "spmm")
-    return out
-
-
-def spmm_codes_supported(F, nb, M, D) -> bool:
-    """True when vqgnn_spmm_codes applies (include/vqgnn.h §6c)."""
-    return bool(lib().vqgnn_spmm_codes_supported(int(F), int(nb), int(M), int(D)))
-
-
-def spmm_codes(rowptr, col, val, n_rows, nnz, X, F, lcodes, emb_out, D, B, out=None, plan=None,
-               col_offset=0):
-    """vqgnn_spmm with the out-of-batch rows read as codewords:
-    xin[j] = X[j] (j < B), concat_b emb_out[b, lcodes[j-B, b], col_offset:col_offset+D]
-    (j >= B) — x_input = cat([x, x_first_order]) of models.py:168-174 without
-    materialising x_first_order.  lcodes: gather_codewords(..., want_x=False,
-    want_codes=True)."""
-    if isinstance(plan, TaskPlan):
-        return spmm_task_codes(plan, n_rows, X, F, lcodes, emb_out, D, B, out=out,
-                               col_offset=col_offset, rowptr=rowptr, nnz=nnz, val=val)
-    if isinstance(plan, PairPlan):   # the code-source kernel walks chunks
-        plan = plan.chunk
-    require_gpu(X, "spmm_codes")
-    dev = X.device
-    nb, M = emb_out.shape[0], emb_out.shape[1]
-    if out is None:
-        out = torch.empty(n_rows, F, dtype=torch.float32, device=dev)
-    if lcodes.dtype != torch.int16 or lcodes.dim() != 2 or lcodes.shape[1] != nb or \
-            lcodes.stride(1) != 1:
-        raise ValueError("spmm_codes: lcodes must be int16 [n-B, nb], row-major")
-    if emb_out.stride(2) != 1 or emb_out.stride(1) != emb_out.shape[2]:
-        raise ValueError("spmm_codes: emb_out must be [nb, M, W] with contiguous rows")
-    if X.shape[0] < int(B):
-        raise ValueError(f"spmm_codes: X has {X.shape[0]} rows < B={B}")
-    L = lib()
-    ws = workspace(L.vqgnn_spmm_workspace(n_rows, nnz, F), dev)
-    n_cols = int(B) + lcodes.shape[0]
-    check(L.vqgnn_spmm_codes(ptr(rowptr), ptr(col), ptr(val), int(n_rows), n_cols, int(nnz),
-                             int(B), ptr(X), _ld(X), ptr(lcodes), lcodes.stride(0), nb,
-                             ptr(emb_out), M, int(D), emb_out.shape[2], emb_out.stride(0),
-                             int(col_offset), int(F), ptr(out), _ld(out), ptr(plan), ptr(ws),
-                             stream_ptr()), "spmm_codes")
-    return out
-
-
-def spmm_task_codes_supported(F, nb, M, D) -> bool:
-    """True when vqgnn_spmm_task_codes applies (include/vqgnn.h §6g)."""
-    return bool(lib().vqgnn_spmm_task_codes_supported(int(F), int(nb), int(M), int(D)))
-
-
-def spmm_task_codes(plan, n_rows, X, F, lcodes, emb_out, D, B, out=None, col_offset=0,
-                    rowptr=None, nnz=None, val=None):
-    """The task-split SpMM (plan: TaskPlan) with the out-of-batch columns read
-    as codes: xin[j] = X[j] (j < B), concat_b emb_out[b, lcodes[j-B, b],
-    col_offset:col_offset+D] (j >= B); codebook column tiles of 8 branches
-    staged in LDS (any M <= 1280).  Same records, order and bits as
-    vqgnn_spmm_task on the gathered x_first_order."""
-    require_gpu(X, "spmm_task_codes")
-    dev = X.device
-    nb, M = emb_out.shape[0], emb_out.shape[1]
-    if not spmm_task_codes_supported(F, nb, M, D):
-        raise ValueError(f"spmm_task_codes: F={F} nb={nb} M={M} D={D} unsupported")
-    if lcodes.dtype != torch.int16 or lcodes.dim() != 2 or lcodes.shape[1] != nb or \
-            (lcodes.shape[0] > 0 and lcodes.stride(1) != 1):
-        raise ValueError("spmm_task_codes: lcodes must be int16 [n-B, nb], row-major")
-    if emb_out.stride(2) != 1 or emb_out.stride(1) != emb_out.shape[2]:
-        raise ValueError("spmm_task_codes: emb_out must be [nb, M, W] with contiguous rows")
-    if X.shape[0] < int(B):
-        raise ValueError(f"spmm_task_codes: X has {X.shape[0]} rows < B={B}")
-    if val is not None and val.data_ptr() != plan.val_ptr:
-        raise ValueError("spmm_task_codes: the task plan's records hold other values than val")
-    if nnz is not None and int(nnz) != plan.nnz or int(n_rows) > plan.n_rows:
-        raise ValueError(f"spmm_task_codes: task plan for nnz={plan.nnz}, rows={plan.n_rows}")
-    if rowptr is None:
-        raise ValueError("spmm_task_codes: rowptr is required")
-    if out is None:
-        out = torch.empty(n_rows, F, dtype=torch.float32, device=dev)
-    L = lib()
-    ws = workspace(L.vqgnn_spmm_task_workspace(plan.nnz, plan.K, F), dev)
-    n_cols = int(B) + lcodes.shape[0]
-    check(L.vqgnn_spmm_task_codes(ptr(rowptr), int(n_rows), n_cols, plan.nnz, int(B),
-                                  ptr(X) if int(B) > 0 else None, _ld(X), ptr(lcodes),
-                                  max(lcodes.stride(0), nb), nb, ptr(emb_out), M, int(D),
-                                  emb_out.shape[2], emb_out.stride(0), int(col_offset), int(F),
-                                  ptr(out), _ld(out), ptr(plan.plan), ptr(plan.records), plan.K,
-                                  plan.n_jobs, plan.n_empty, ptr(ws), stream_ptr()),
-          "spmm_task_codes")
-    return out
+    raise TypeError(f"spmm: plan must be a TaskPlan or TilePlan (CSR.plan), got {type(plan)}")
 
 
 def csr_transpose(rowptr, col, val, n_rows, n_cols, nnz, want_perm=False):

@@ -118,53 +118,32 @@ class CSR:
             self._t = t
         return self._t
 
-    def plan(self, F, B=None, n_rows=None, kind=None):
-        """SpMM plan for feature width F, cached like torch_sparse's storage
-        caches: by default the task plan (include/vqgnn.h §6e, any F);
-        the task records hold this CSR's values, so products with other
-        values (GAT coefficients) ask for ``kind="chunk"``;
-        ``VQGNN_SPMM=chunk`` selects the chunk plan (§6b), or with
-        ``VQGNN_SPMM_PAIR=1`` the segment-pair plan (§6d) where it applies
-        (F = 128; bit-identical output, measured within +-8% of the chunk
-        kernel across boxes, so not the default).  The pair plan covers rows
-        [0, n_rows) (default: all) and uses B (default n_rows) to split batch
-        from out-of-batch rows."""
+    def plan(self, F=None, B=None, n_rows=None, kind=None):
+        """SpMM plan, cached like torch_sparse's storage caches: the task plan
+        (include/vqgnn.h §6) -- per-edge records of this CSR's values, task
+        starts and fix-up jobs, valid for any F and any leading row count
+        (products with other values on the same structure, e.g. GAT's
+        coefficients: ``plan().with_values(col, values)``).
+        ``kind="tile"`` (or VQGNN_SPMM=tile) asks for the opt-in tiled plan
+        (§6f: dense blocks through LDS tiles plus the sparse remainder's task
+        plan), for the full row range only; F, B and n_rows are accepted for
+        call-site symmetry and do not change the plan."""
         import os
         from . import kernels
         mode = kind or os.environ.get("VQGNN_SPMM", "task")
-        if mode == "tile" and os.environ.get("VQGNN_SPMM_PAIR", "0") != "1":
-            # opt-in (DESIGN §4.2b): the dense blocks through LDS tiles, the
-            # sparse remainder through the task kernel; measured no faster
-            # than the task kernel alone on the reddit batch, whose sparse
-            # remainder (41 % of the edges) is bound by MALL row reads
+        if mode == "tile" and (n_rows is None or int(n_rows) == self._sizes[0]):
             p = self._plans.get("tile", False)
             if p is False:
                 p = kernels.spmm_tile_plan(self.rowptr, self.col, self.value, self._sizes[0],
                                            self._sizes[1], self._host_nnz, min_fraction=0.0)
                 self._plans["tile"] = p
-            if p is not None and (n_rows is None or int(n_rows) == self._sizes[0]):
+            if p is not None:
                 return p
-            mode = "task"
-        if mode == "task" and os.environ.get("VQGNN_SPMM_PAIR", "0") != "1":
-            p = self._plans.get("task")
-            if p is None:
-                p = kernels.spmm_task_plan(self.rowptr, self.col, self.value, self._sizes[0],
-                                           self._host_nnz)
-                self._plans["task"] = p
-            return p
-        chunk = self._plans.get(F)
-        if chunk is None:
-            chunk = kernels.spmm_plan(self.rowptr, self._sizes[0], self._host_nnz, F)
-            self._plans[F] = chunk
-        if os.environ.get("VQGNN_SPMM_PAIR", "0") != "1" or not kernels.spmm_pair_supported(F):
-            return chunk
-        nr = self._sizes[0] if n_rows is None else int(n_rows)
-        b = nr if B is None else int(B)
-        key = ("pair", F, b, nr)
-        p = self._plans.get(key)
+        p = self._plans.get("task")
         if p is None:
-            p = kernels.spmm_pair_plan(self.rowptr, nr, self._host_nnz, F, b, chunk=chunk)
-            self._plans[key] = p
+            p = kernels.spmm_task_plan(self.rowptr, self.col, self.value, self._sizes[0],
+                                       self._host_nnz)
+            self._plans["task"] = p
         return p
 
     def rows(self):

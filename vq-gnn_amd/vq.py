@@ -112,6 +112,9 @@ class VQBank(nn.Module):
 
     # ------------------------------------------------------------------ #
     def check_bad_init(self):
+        if self.comm is not None and self.comm.take_overflow():
+            raise ValueError(f"a rank's batch exceeded CodebookSync capacity "
+                             f"{self.comm.capacity}")
         if int(self.bad_flag.item()) != 0:
             self.bad_flag.zero_()
             raise ValueError('Bad Init!')
@@ -140,7 +143,12 @@ class VQBank(nn.Module):
 
     def _exchange_codes(self, batch_idx, local, codes, max_B):
         """Own codes now (scattered by the pack kernel), everyone's
-        asynchronously (landed by sync_codes)."""
+        asynchronously (landed by sync_codes).  Rows past max_B (a batch over
+        the CodebookSync capacity, raised at the next check on every rank)
+        are scattered locally only, so the collective keeps its shape."""
+        if local.shape[0] > max_B:
+            kernels.scatter_codes(batch_idx[max_B:], local[max_B:], codes)
+            batch_idx, local = batch_idx[:max_B], local[:max_B]
         self._pending_codes = self.comm.start_codes_exchange(batch_idx, local, codes,
                                                              max_B, self.M)
 
