@@ -1,0 +1,24 @@
+#!/bin/bash
+# Build a library variant with one source file replaced (A/B measurements):
+#   build_variant.sh <name> <replaced.hip> <replacement file>
+# -> vq-gnn_amd/lib/ab_<name>.so (travels to the GPU box; select it with
+#    VQGNN_LIB=vq-gnn_amd/lib/ab_<name>.so)
+set -e
+cd "$(dirname "$0")/../vq-gnn_amd/csrc"
+name=$1; src=$2; repl=$3
+make -s -j8 >/dev/null
+tmp=../lib/obj/ab_$name
+mkdir -p $tmp
+cp "$repl" $tmp/$src
+objs=""
+for f in $(sed -n 's/^SRCS := //p;s/^         //p' Makefile | tr ' ' '\n' | grep hip); do
+  if [ "$f" = "$src" ]; then
+    /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++20 -ffp-contract=off -Wall \
+      -Wno-unused-function -munsafe-fp-atomics -I$PWD -c $tmp/$src -o $tmp/${src%.hip}.o
+    objs="$objs $tmp/${src%.hip}.o"
+  else
+    objs="$objs ../lib/obj/${f%.hip}.o"
+  fi
+done
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../lib/ab_$name.so $objs
+echo "built vq-gnn_amd/lib/ab_$name.so"

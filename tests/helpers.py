@@ -86,3 +86,51 @@ class torch_threads:
 
     def __exit__(self, *a):
         torch.set_num_threads(self.old)
+
+
+def sequential_argmin(xn, emb, window=1e-3):
+    """argmin_m of the distance in the arithmetic the golden fixtures pin
+    (vq.py:166-171 as restated in oracle/vq_ref.py): |x|^2 and |e|^2 summed
+    sequentially in fp32, x.e as a k-ordered fp32 fma chain from fl(e0 x0),
+    d = fl(fl(|x|^2 + |e|^2) - 2 x.e), first index on ties -- evaluated
+    exactly (Fraction arithmetic) for every codeword within ``window`` of the
+    fp64 minimum.  The fixtures were generated on this container's CPU; the
+    GPU box's MKL picks other sgemm kernels for some shapes, whose last-ulp
+    rounding differs, so ulp-level near-ties are checked against this model.
+    xn [B, W] float32, emb [M, >= W] float32 -> int64 [B]."""
+    from fractions import Fraction
+
+    xn = np.asarray(xn, np.float32)
+    W = xn.shape[1]
+    e = np.asarray(emb, np.float32)[:, :W]
+    d64 = ((xn.astype(np.float64) ** 2).sum(1)[:, None] + (e.astype(np.float64) ** 2).sum(1)[None]
+           - 2 * xn.astype(np.float64) @ e.astype(np.float64).T)
+    lo = d64.min(1)
+
+    def f32(v):
+        return np.float32(float(v))
+
+    def seqsq(v):
+        s = f32(Fraction(float(v[0])) * Fraction(float(v[0])))
+        for k in range(1, len(v)):
+            s = f32(Fraction(float(s)) + Fraction(float(f32(Fraction(float(v[k])) ** 2))))
+        return s
+
+    se_cache = {}
+    out = np.empty(xn.shape[0], np.int64)
+    for i in range(xn.shape[0]):
+        x = xn[i]
+        sx = seqsq(x)
+        best, bm = None, -1
+        for m in np.nonzero(d64[i] <= lo[i] + window)[0]:
+            if m not in se_cache:
+                se_cache[m] = seqsq(e[m])
+            dot = f32(Fraction(float(e[m, 0])) * Fraction(float(x[0])))
+            for k in range(1, W):
+                dot = f32(Fraction(float(e[m, k])) * Fraction(float(x[k])) + Fraction(float(dot)))
+            S = f32(Fraction(float(sx)) + Fraction(float(se_cache[m])))
+            d = f32(Fraction(float(S)) - 2 * Fraction(float(dot)))
+            if best is None or d < best:
+                best, bm = d, m
+        out[i] = bm
+    return out

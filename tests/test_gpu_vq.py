@@ -6,7 +6,7 @@ import torch
 import numpy as np
 
 from helpers import (STATE_KEYS, as_layout, golden_cases, load_case, oracle_state_from,
-                     tie_aware_mismatch, torch_threads)
+                     sequential_argmin, tie_aware_mismatch, torch_threads)
 from oracle import vq_ref
 from vq_gnn_amd import kernels
 from vq_gnn_amd.vq import VQBank, VectorQuantizerEMA
@@ -61,6 +61,51 @@ def test_assign_bit_exact_given_coefficients(M, D, W, B, tie):
     absw = torch.zeros(M, W, dtype=torch.float64).index_add_(0, idx_ref, xn.double().abs())
     tol = cnt[:, None] * unit * 0.5 + 1e-6 * absw   # + fp32 rounding of xn itself
     assert ((st[:, 1:] - dw).abs() <= tol + 1e-7).all()
+
+
+@pytest.mark.parametrize("M,W", [(256, 8), (256, 4), (1024, 8), (4096, 8), (40, 8)])
+def test_assign_near_ties_resolved_exactly(M, W):
+    """The filtered sweep (t' = |e|^2 - 2 x.e from the MFMA) sends rows whose
+    minimum is within its error bound of another codeword to the exact
+    near-tie kernel.  Crafted ties: exact duplicate codewords, codewords one
+    or two ulps apart, and rows placed on the bisector of two codewords --
+    every index equals the pinned sequential arithmetic's (first index on
+    exact ties; helpers.sequential_argmin -- at the ulp level the box's MKL
+    is not that arithmetic for every shape), in every branch, with the EMA
+    counts and the scattered codes consistent."""
+    D, nb, B, N = 4, 5, 4000, 9000
+    g = torch.Generator().manual_seed(M + W)
+    emb = torch.randn(nb, M, 2 * D, generator=g) * 0.7
+    emb[0, 1::2] = emb[0, 0::2][: M // 2]                       # exact duplicates
+    emb[1, 1::2] = torch.nextafter(emb[1, 0::2][: M // 2], torch.tensor(10.0))  # 1 ulp apart
+    emb[2, 1::2] = torch.nextafter(torch.nextafter(emb[2, 0::2][: M // 2], torch.tensor(-9.0)),
+                                   torch.tensor(-9.0))
+    X = torch.randn(B, nb * D, generator=g)
+    G = torch.randn(B, nb * D, generator=g) * 1e-3
+    # branch 3: rows on the bisector of codewords (2c, 2c+1) in normalised
+    # space (identity coefficients below), up to fp32 rounding
+    c = torch.randint(0, M // 2, (B,), generator=g)
+    mid = 0.5 * (emb[3, 2 * c] + emb[3, 2 * c + 1])
+    X[:, 3 * D:4 * D] = mid[:, :D]
+    G[:, 3 * D:4 * D] = mid[:, D:]
+    coef = torch.zeros(6, nb * D)
+    coef[0] = coef[2] = 1.0                          # x -> x (grad half scaled below)
+    scale = 1.0
+    batch_idx = torch.randperm(N, generator=g)[:B]
+    codes = torch.full((N, nb), -1, dtype=torch.int16, device=DEV)
+    idx = torch.empty(nb, B, dtype=torch.long, device=DEV)
+    stats = kernels.vq_assign(X.to(DEV), G.to(DEV) if W == 2 * D else None, coef.to(DEV), scale,
+                              emb.to(DEV), D, W, idx_out=idx, codes=codes,
+                              batch_idx=batch_idx.to(DEV), want_stats=True)
+    st = kernels.vq_ema_reduce(stats)[0].cpu()
+    for b in range(nb):
+        xb, gb = X[:, b * D:(b + 1) * D], G[:, b * D:(b + 1) * D]
+        xn = torch.cat([xb, gb], 1)[:, :W]              # identity coefficients
+        r = torch.from_numpy(sequential_argmin(xn.numpy(), emb[b].numpy()))
+        n_mis = int((idx.cpu()[b] != r).sum())
+        assert n_mis == 0, f"M={M} W={W} branch {b}: {n_mis} index mismatches"
+        assert torch.equal(codes.cpu()[batch_idx, b].long(), r)
+        assert torch.equal(st[b, :, 0], torch.bincount(r, minlength=M))
 
 
 def test_assign_multibranch_strided_views_and_codes():

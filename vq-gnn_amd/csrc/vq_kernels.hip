@@ -586,6 +586,8 @@ struct AssignGeom {
   int kc;             // k-chunks of 4 (W padded to 4*kc)
   bool fused;         // EMA statistics accumulated in the assign kernel
   int wv;             // waves per workgroup (8 or 16)
+  bool filter;        // vq_filter_kernel (W <= 8) instead of vq_assign_kernel
+  size_t lds;         // dynamic LDS of the filter kernel's launch
 };
 
 template <int KC>
@@ -657,6 +659,63 @@ vq_assign_kernel(const float* __restrict__ X, int64_t ldx,
                  int* __restrict__ idx32, unsigned long long* __restrict__ partial,
                  int rows_per_part, int chunk, int shift_f, int shift_g, int m_sweep);
 
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
+constexpr int kFltSlack = 32;          // one tile pair of prefetch past a chunk
+constexpr int kFltBytesPerCode = 52;   // 3 f16 planes of 16 B + |e|^2 (f32)
+
+static size_t flt_lds_bytes(int chunk) {
+  return (size_t)kFltBytesPerCode * (chunk + kFltSlack);
+}
+
+// Per-wave row scratch of vq_filter_kernel (after the codebook planes and
+// the fused slab): [NG][16 rows][8] f32 normalised rows, then [16 rows][8]
+// dwords of f16 pairs (x_hi pairs k = 2q, 2q+1 at dword q, x_lo pairs at
+// dword 4 + q), shared by the row groups one after the other
+constexpr int kFltScratch = kAsgGroups * 512 + 512;
+
+// filtered assignment for W <= 8 (section 3b)
+template <bool FUSED, int WM, int WV>
+__global__ void __launch_bounds__(WV * 64)
+vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restrict__ Gr,
+                 int64_t ldg, int B, int nb, int D, int M, int W,
+                 const float* __restrict__ coef, float grad_scale,
+                 const float* __restrict__ emb, int ldw, int64_t emb_bstride,
+                 int64_t* __restrict__ idx_out, int16_t* __restrict__ codes, int64_t ldc,
+                 const int64_t* __restrict__ batch_idx, int* __restrict__ idx32,
+                 unsigned long long* __restrict__ partial, int* __restrict__ flags,
+                 int rows_per_part, int chunk, int shift_f, int shift_g, int m_sweep);
+
+// the filter's row-load mode: 2 -> W = 8 = 2D, D = 4; 1 -> W = D = 4 (float4
+// rows, aligned); 0 -> general
+static int flt_mode(int W, int D, int64_t ldx, int64_t ldg, const void* X, const void* G) {
+  const bool ax = (ldx & 3) == 0 && (reinterpret_cast<uintptr_t>(X) & 15) == 0;
+  const bool ag = G && (ldg & 3) == 0 && (reinterpret_cast<uintptr_t>(G) & 15) == 0;
+  if (D == 4 && W == 8 && ax && ag) return 2;
+  if (D == 4 && W == 4 && ax) return 1;
+  return 0;
+}
+
+template <int WV>
+static const void* flt_fn_wv(bool fused, int wm) {
+  if (fused) return wm == 1 ? (const void*)vq_filter_kernel<true, 1, WV>
+                  : wm == 2 ? (const void*)vq_filter_kernel<true, 2, WV>
+                            : (const void*)vq_filter_kernel<true, 0, WV>;
+  return wm == 1 ? (const void*)vq_filter_kernel<false, 1, WV>
+       : wm == 2 ? (const void*)vq_filter_kernel<false, 2, WV>
+                 : (const void*)vq_filter_kernel<false, 0, WV>;
+}
+static const void* flt_fn(bool fused, int wm, int wv) {
+  return wv == 16 ? flt_fn_wv<16>(fused, wm) : flt_fn_wv<8>(fused, wm);
+}
+
+// the filtered path serves W <= 8 (VQGNN_ASSIGN_EXACT=1: the exact f32 sweep
+// for every W, a measurement and cross-check knob)
+static bool use_filter(int W) {
+  static const int exact_env = env_int_vq("VQGNN_ASSIGN_EXACT", 0);
+  return W <= 8 && !exact_env;
+}
+
 // k-slot layout: 0 general (W < 4*KC, padded), 1 W == 4*KC == D (features),
 // 2 W == 4*KC == 2*D (features then grads)
 static int slot_mode(int kc, int W, int D) {
@@ -681,7 +740,7 @@ static const void* assign_fn(bool fused, int wm, int wv) {
 // Workgroups of the assign kernel the current device holds at once (register
 // and LDS limited), cached per configuration.  Without a device (host-only
 // queries) a static estimate is returned; the value only sizes the grid.
-static int assign_capacity(int kc, bool fused, int wm, size_t lds, int wv) {
+static int assign_capacity(int kc, bool fused, int wm, size_t lds, int wv, bool flt) {
   const int fallback = 512 * 8 / wv;
   int dev = 0, cus = 0, per_cu = 0;
   if (hipGetDevice(&dev) != hipSuccess) {
@@ -690,11 +749,12 @@ static int assign_capacity(int kc, bool fused, int wm, size_t lds, int wv) {
   }
   static std::mutex mu;
   static std::map<std::tuple<int, int, bool, size_t>, int> cache;
-  const auto key = std::make_tuple(dev, (kc * 4 + wm) * 32 + wv, fused, lds);
+  const auto key = std::make_tuple(dev, ((flt ? 8 : 0) + kc) * 128 + wm * 32 + wv, fused, lds);
   std::lock_guard<std::mutex> lk(mu);
   auto it = cache.find(key);
   if (it != cache.end()) return it->second;
-  const void* fn = kc == 1 ? assign_fn<1>(fused, wm, wv)
+  const void* fn = flt ? flt_fn(fused, wm, wv)
+                 : kc == 1 ? assign_fn<1>(fused, wm, wv)
                  : kc == 2 ? assign_fn<2>(fused, wm, wv) : assign_fn<4>(fused, wm, wv);
   if (lds > 64 * 1024)
     (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -711,13 +771,25 @@ static int assign_capacity(int kc, bool fused, int wm, size_t lds, int wv) {
 static AssignGeom assign_geom(int B, int nb, int M, int W) {
   AssignGeom g;
   g.kc = W <= 4 ? 1 : (W <= 8 ? 2 : 4);
+  g.filter = use_filter(W);
   g.mpad = (M + 15) / 16 * 16;
   const size_t acc = (size_t)M * (W + 1) * sizeof(unsigned long long);
-  // fused EMA when codebook + accumulators share the LDS
-  g.fused = cb_lds_bytes(g.kc, g.mpad) + acc <= kLdsBudget;
-  if (g.fused) {
+  if (g.filter) {
+    // staged in tile pairs: chunks of 32 codewords; room for 16 waves' row
+    // scratch
+    g.mpad = (M + 31) / 32 * 32;
+    const size_t scr = (size_t)16 * kFltScratch;
+    g.fused = flt_lds_bytes(g.mpad) + acc + scr <= kLdsBudget;
+    int c = g.mpad;
+    if (!g.fused)
+      while (c > 32 && flt_lds_bytes(c) + scr > kLdsBudget) c = (c / 2 + 31) / 32 * 32;
+    g.chunk = c;
+  } else if (cb_lds_bytes(g.kc, g.mpad) + acc <= kLdsBudget) {
+    // fused EMA when codebook + accumulators share the LDS
+    g.fused = true;
     g.chunk = g.mpad;
   } else {
+    g.fused = false;
     int c = g.mpad;
     while (c > 16 && cb_lds_bytes(g.kc, c) > kLdsBudget) c = (c / 2 + 15) / 16 * 16;
     // measurement knob: a smaller staged chunk (more resident workgroups,
@@ -726,15 +798,17 @@ static AssignGeom assign_geom(int B, int nb, int M, int W) {
     if (cenv >= 32 && cenv < c) c = cenv / 32 * 32;
     g.chunk = c;
   }
-  size_t lds = cb_lds_bytes(g.kc, g.chunk);
+  size_t lds = g.filter ? flt_lds_bytes(g.chunk) : cb_lds_bytes(g.kc, g.chunk);
   if (g.fused) lds += acc;
-  const int wm = W == 4 * g.kc ? 2 : 0;
+  const size_t scr8 = g.filter ? (size_t)8 * kFltScratch : 0;
+  const int wm = g.filter ? (W == 8 ? 2 : (W == 4 ? 1 : 0)) : (W == 4 * g.kc ? 2 : 0);
   // waves per workgroup: the choice with more resident waves per CU (ties: 8)
-  const int cap8 = assign_capacity(g.kc, g.fused, wm, lds, 8);
-  const int cap16 = assign_capacity(g.kc, g.fused, wm, lds, 16);
+  const int cap8 = assign_capacity(g.kc, g.fused, wm, lds + scr8, 8, g.filter);
+  const int cap16 = assign_capacity(g.kc, g.fused, wm, lds + 2 * scr8, 16, g.filter);
   g.wv = cap16 * 16 > cap8 * 8 ? 16 : 8;
   const int wenv = env_int_vq("VQGNN_ASG_WAVES", 0);
   if (wenv == 8 || wenv == 16) g.wv = wenv;
+  g.lds = lds + (g.wv == 16 ? 2 * scr8 : scr8);
   const int rows_per_iter = g.wv * 16 * kAsgGroups;
   const int row_blocks = (B + rows_per_iter - 1) / rows_per_iter;
   // one full round of resident workgroups: parts x nb <= what the device
@@ -1128,6 +1202,508 @@ vq_assign_kernel(const float* __restrict__ X, int64_t ldx,
             if (kval[kc]) atomicAdd(a + 1 + kc * 4 + q, to_fixed(xk[g][kc], isg[kc] ? shift_g : shift_f));
         }
       }
+    }
+  }
+
+  if constexpr (FUSED) {   // fold into the single zeroed slab: integer, exact, order-free
+    __syncthreads();
+    unsigned long long* out = partial + (int64_t)b * M * (W + 1);
+    for (int i = tid; i < M * (W + 1); i += NT)
+      if (acc[i]) atomicAdd(out + i, acc[i]);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// 3b. Filtered assignment, W <= 8 (the default path)
+//
+// The sweep scores every codeword on v_mfma_f32_16x16x32_f16 (16 cycles per
+// 16x16 tile against 2 x 32 for the exact f32 MFMA at W = 8) from an f16
+// split of both operands, and only the codewords that can win are computed
+// in the reference's f32 arithmetic.  K slots of one MFMA (quad q of the A/B
+// fragments holds k = 8q .. 8q+7):
+//   quad 0: (-2 e_hi) . x_hi      quad 1: (-2 e_lo) . x_hi
+//   quad 2: (-2 e_hi) . x_lo      quad 3: (|e|^2 split in three f16) . 1
+//                                         + 1 . (|x|^2 + 1 split in three f16)
+// with v_hi = f16(v), v_lo = f16(v - v_hi), so each score is
+//   s = |x|^2 + 1 + |e|^2 - 2 x.e  (+ the split and accumulation error),
+// the reference distance plus 1: positive, so scores compare as unsigned
+// integers (v_min3_u32 / v_med3_u32, no float canonicalisation).
+// Per lane and row group the sweep keeps the minimum over tile pairs (32
+// codewords: 8 scores per lane), the pair that first reached it and the
+// second-smallest pair minimum.  The resolve recomputes the winner lane's 8
+// codewords of the winning pair with vq.py's operations and order (bit-exact,
+// first index on ties); when any other codeword's score lies within the
+// error bound Delta of the minimum (a near-tie), the row is appended to the
+// workgroup's list and swept exactly after the row loop.  Delta
+// (DESIGN.md §4.1): per codeword |score - (ref. distance + 1)| <=
+// 2^-24 (89.5 |x|^2 + 88.5 |e|^2 + 36) for W <= 8, |e|^2 of any codeword within
+// 1 of the minimum <= 4.01 |x|^2 + 2 |t| + 2.1 (t = minimum - |x|^2 - 1),
+// twice that with a 10 % margin: Delta = 2^-24 (978 |x|^2 + 390 |t| + 489).
+// The accumulation term assumes every internal add of the MFMA rounds to
+// f32 or better (32 u of the summed magnitudes; scripts/probes/
+// f16_mfma_accum.hip measured at most 5.1 u) and f16 subnormal operands
+// kept (measured).  Rows with |x|^2 >= 2^16 go to the exact path.  Codewords
+// with |e|^2 >= 2^15 (dead codewords of a trained codebook reach 10^10) are
+// scored +inf; a row is decided by the filter only if the smallest such
+// |e|^2, E0, keeps all of them out: (sqrt(E0) - |x|)^2 > score + Delta.
+// ---------------------------------------------------------------------------
+
+__device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t r;   // operands are VALU results (never raw MFMA results: no hazard)
+  asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
+// stage codebook rows [mc0, mc0 + chunk + slack) of E: planes -2 e_hi,
+// -2 e_lo, (|e|^2 split, 1, 1, 1, 0, 0) and |e|^2 in f32 (vq.py's order);
+// past mcount: zero planes, |e|^2 = +inf.  Codewords with |e|^2 >= 2^15 (or
+// NaN) are staged like empty ones and their smallest |e|^2 (0 for NaN) is
+// folded into *bigmin (f32 bits; positive floats order as integers).
+template <int NT>
+__device__ __forceinline__ void stage_filter(const float* __restrict__ E, int ldw, int W, int mc0,
+                                             int mcount, int chunk, char* smem, int tid,
+                                             unsigned int* bigmin) {
+  const int cs = chunk + kFltSlack;
+  half8* p0 = reinterpret_cast<half8*>(smem);
+  half8* p1 = p0 + cs;
+  half8* p2 = p1 + cs;
+  float* sef = reinterpret_cast<float*>(p2 + cs);
+  for (int m = tid; m < cs; m += NT) {
+    float e[8];
+    const bool mv = m < mcount;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) e[k] = (mv && k < W) ? E[(int64_t)(mc0 + m) * ldw + k] : 0.f;
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (k < W) s = (k == 0) ? __fmul_rn(e[k], e[k]) : __fadd_rn(s, __fmul_rn(e[k], e[k]));
+    const bool big = mv && !(s < 32768.f);
+    if (big) atomicMin(bigmin, s == s ? __float_as_uint(s) : 0u);
+    half8 hi, lo, sp;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float ek = big ? 0.f : e[k];
+      const _Float16 h = (_Float16)ek;
+      const float hf = (float)h;
+      const _Float16 l = (_Float16)__fsub_rn(ek, hf);
+      hi[k] = (_Float16)(-2.f * hf);                 // exact: a doubled f16
+      lo[k] = (_Float16)(-2.f * (float)l);
+    }
+    if (mv && !big) {
+      const _Float16 s0 = (_Float16)s;
+      const float r1 = __fsub_rn(s, (float)s0);      // exact
+      const _Float16 s1 = (_Float16)r1;
+      const _Float16 s2 = (_Float16)__fsub_rn(r1, (float)s1);
+      sp = half8{s0, s1, s2, (_Float16)1.f, (_Float16)1.f, (_Float16)1.f, (_Float16)0.f,
+                 (_Float16)0.f};
+    } else {
+      sp = half8{(_Float16)INFINITY, (_Float16)0.f, (_Float16)0.f, (_Float16)1.f, (_Float16)1.f,
+                 (_Float16)1.f, (_Float16)0.f, (_Float16)0.f};
+    }
+    p0[m] = hi;
+    p1[m] = lo;
+    p2[m] = sp;
+    sef[m] = mv ? s : INFINITY;
+  }
+}
+
+
+// minimum over the 4 q-lanes of a row (lanes j, j+16, j+32, j+48): the
+// gfx950 permlane swaps hand each lane {v[l], v[l ^ 32]} and then
+// {v[l], v[l ^ 16]} as VALU operations (no LDS traffic)
+__device__ __forceinline__ uint32_t qmin_u(uint32_t v) {
+  const auto a = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  v = min((uint32_t)a[0], (uint32_t)a[1]);
+  const auto c = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+  return min((uint32_t)c[0], (uint32_t)c[1]);
+}
+__device__ __forceinline__ int qmin_i(int v) {
+  const auto a = __builtin_amdgcn_permlane32_swap((uint32_t)v, (uint32_t)v, false, false);
+  v = min((int)a[0], (int)a[1]);
+  const auto c = __builtin_amdgcn_permlane16_swap((uint32_t)v, (uint32_t)v, false, false);
+  return min((int)c[0], (int)c[1]);
+}
+// lexicographic (distance, index) minimum over the 4 q-lanes
+__device__ __forceinline__ void qmin_lex(float& d, int& i) {
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const uint32_t du = __float_as_uint(d);
+    const auto a = s == 0 ? __builtin_amdgcn_permlane32_swap(du, du, false, false)
+                          : __builtin_amdgcn_permlane16_swap(du, du, false, false);
+    const auto b = s == 0 ? __builtin_amdgcn_permlane32_swap((uint32_t)i, (uint32_t)i, false, false)
+                          : __builtin_amdgcn_permlane16_swap((uint32_t)i, (uint32_t)i, false, false);
+    const float d0 = __uint_as_float(a[0]), d1 = __uint_as_float(a[1]);
+    const int i0 = (int)b[0], i1 = (int)b[1];
+    const bool one = d1 < d0 || (d1 == d0 && i1 < i0);
+    d = one ? d1 : d0;
+    i = one ? i1 : i0;
+  }
+}
+
+// WM: 2 -> W = 8 = 2D with D = 4 (features then gradients); 1 -> W = D = 4;
+//     0 -> any W <= 8
+template <bool FUSED, int WM, int WV>
+__global__ void __launch_bounds__(WV * 64)
+vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restrict__ Gr,
+                 int64_t ldg, int B, int nb, int D_, int M, int W_,
+                 const float* __restrict__ coef, float grad_scale,
+                 const float* __restrict__ emb, int ldw, int64_t emb_bstride,
+                 int64_t* __restrict__ idx_out, int16_t* __restrict__ codes, int64_t ldc,
+                 const int64_t* __restrict__ batch_idx, int* __restrict__ idx32,
+                 unsigned long long* __restrict__ partial, int* __restrict__ flags,
+                 int rows_per_part, int chunk, int shift_f, int shift_g, int m_sweep) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  constexpr int NG = kAsgGroups, NT = WV * 64;
+  const int W = WM == 2 ? 8 : (WM == 1 ? 4 : W_);          // compile-time in the row modes
+  const int D = WM != 0 ? 4 : D_;
+  const int F = nb * D;
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int b = wg % nb;
+  const int part = wg / nb;
+  const int cs = chunk + kFltSlack;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int q = lane >> 4, j = lane & 15;
+  char* lds = reinterpret_cast<char*>(smem);
+  const float* sef = reinterpret_cast<const float*>(lds + (size_t)48 * cs);
+  unsigned long long* acc = reinterpret_cast<unsigned long long*>(lds + (size_t)52 * cs);
+  char* scr = lds + (size_t)52 * cs + (FUSED ? (size_t)M * (W + 1) * 8 : 0) +
+              (size_t)wave * kFltScratch;
+  float* xs = reinterpret_cast<float*>(scr);                          // [NG][16][8]
+  uint32_t* hl = reinterpret_cast<uint32_t*>(scr + NG * 512);         // [16][8]
+  const float* E = emb + (int64_t)b * emb_bstride;
+  const int nchunks = (M + chunk - 1) / chunk;
+  const bool vec_rows = (ldw & 3) == 0 && (emb_bstride & 3) == 0 &&
+                        (reinterpret_cast<uintptr_t>(emb) & 15) == 0;
+  __shared__ int s_nflag;
+  __shared__ unsigned int s_bigmin;
+  if (tid == 0) {
+    s_nflag = 0;
+    s_bigmin = 0x7f800000u;                           // +inf: no out-of-range codeword
+  }
+  if constexpr (FUSED) {
+    for (int i = tid; i < M * (W + 1); i += NT) acc[i] = 0ull;
+  }
+  int* const flist = flags + (int64_t)wg * rows_per_part;
+  // k-slot table in LDS: per k (alpha, beta, shift, grad scale), read back by
+  // the lanes of k-slots 2q, 2q+1 in the row phase (not held in registers
+  // across the sweep); grad scale is 1 for features (v * 1 is exact)
+  __shared__ __attribute__((aligned(16))) float s_kt[8][4];
+  if (tid < 8) {
+    const int k = tid;
+    const bool kvv = k < W;
+    const bool gk = W != D && k >= D;
+    const int c = b * D + (gk ? k - D : k);
+    s_kt[k][0] = kvv ? coef[(gk ? 2 * F : 0) + c] : 0.f;
+    s_kt[k][1] = kvv ? coef[(gk ? 3 * F : F) + c] : 0.f;
+    s_kt[k][2] = kvv ? coef[(gk ? 5 * F : 4 * F) + c] : 0.f;
+    s_kt[k][3] = gk ? grad_scale : 1.f;
+  }
+  // k-slot 2q + u of this lane: valid, a gradient column
+  auto kvalid = [&](int u) { return 2 * q + u < W; };
+  auto kgrad = [&](int u) { return W != D && 2 * q + u >= D; };
+  auto kcol = [&](int u) { return b * D + (kgrad(u) ? 2 * q + u - D : 2 * q + u); };
+  __syncthreads();
+  if (nchunks == 1) stage_filter<NT>(E, ldw, W, 0, M, chunk, lds, tid, &s_bigmin);
+
+  const int part_begin = part * rows_per_part;
+  const int part_end = min(B, part_begin + rows_per_part);
+  constexpr int RPW = 16 * NG, RPI = WV * RPW;
+  const int n_iters = part_end > part_begin ? (part_end - part_begin + RPI - 1) / RPI : 0;
+  // A-fragment byte offset of this lane: plane (q: 0 -> hi, 1 -> lo, 2 -> hi,
+  // 3 -> |e|^2 parts), codeword j of tile 0
+  const uint32_t a_lane = (uint32_t)(((q == 1) ? 1 : (q == 3 ? 2 : 0)) * cs + j) * 16u;
+  if (nchunks == 1) __syncthreads();
+
+  for (int it = 0; it < n_iters; ++it) {
+    const int row0 = part_begin + it * RPI + wave * RPW;
+    float sx[NG];
+    half8 bop[NG];
+    bool rowbad[NG];
+    // ---- rows: lane (q, j) loads and normalises k-slots 2q, 2q+1 of row j
+    // (vq.py's bn_apply), splits them into f16 hi/lo pairs, and every lane
+    // reads its whole row back from the wave's LDS scratch
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      const int64_t rowi = min(row0 + g * 16 + j, part_end - 1);
+      float v[2];
+      if constexpr (WM != 0) {
+        // k = 2q, 2q+1 sit side by side in one of X / G (D = 4): one float2
+        float2 r2 = make_float2(0.f, 0.f);
+        if (kvalid(0))
+          r2 = kgrad(0) ? *reinterpret_cast<const float2*>(Gr + rowi * ldg + kcol(0))
+                        : *reinterpret_cast<const float2*>(X + rowi * ldx + kcol(0));
+        v[0] = r2.x;
+        v[1] = r2.y;
+      } else {
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+          v[u] = kvalid(u) ? (kgrad(u) ? Gr[rowi * ldg + kcol(u)] : X[rowi * ldx + kcol(u)]) : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const float4 t = *reinterpret_cast<const float4*>(&s_kt[2 * q + u][0]);
+        v[u] = __fmul_rn(fmaf(__fsub_rn(v[u], t.z), t.x, t.y), t.w);      // vq.py:224
+      }
+      *reinterpret_cast<float2*>(xs + (g * 16 + j) * 8 + 2 * q) = make_float2(v[0], v[1]);
+      const half2_t h = half2_t{(_Float16)v[0], (_Float16)v[1]};
+      const half2_t l = half2_t{(_Float16)__fsub_rn(v[0], (float)h[0]),
+                                (_Float16)__fsub_rn(v[1], (float)h[1])};
+      hl[j * 8 + q] = __builtin_bit_cast(uint32_t, h);
+      hl[j * 8 + 4 + q] = __builtin_bit_cast(uint32_t, l);
+      __builtin_amdgcn_wave_barrier();
+      const float4 x0 = *reinterpret_cast<const float4*>(xs + (g * 16 + j) * 8);
+      const float4 x1 = *reinterpret_cast<const float4*>(xs + (g * 16 + j) * 8 + 4);
+      const uint4 fr = *reinterpret_cast<const uint4*>(hl + j * 8 + (q == 2 ? 4 : 0));
+      __builtin_amdgcn_wave_barrier();
+      const float xr[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+      float s = 0.f;                                  // |x|^2 in k order
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (k < W) s = (k == 0) ? __fmul_rn(xr[k], xr[k]) : __fadd_rn(s, __fmul_rn(xr[k], xr[k]));
+      sx[g] = s;
+      rowbad[g] = !(s < 65536.f);
+      // quad 3: (1, 1, 1, |x|^2 + 1 split in three f16, 0, 0)
+      const float c1 = __fadd_rn(s, 1.f);
+      const _Float16 c0 = (_Float16)c1;
+      const float r1 = __fsub_rn(c1, (float)c0);
+      const _Float16 cl = (_Float16)r1;
+      const _Float16 cll = (_Float16)__fsub_rn(r1, (float)cl);
+      const uint4 f3 = {0x3c003c00u, __builtin_bit_cast(uint32_t, half2_t{(_Float16)1.f, c0}),
+                        __builtin_bit_cast(uint32_t, half2_t{cl, cll}), 0u};
+      bop[g] = __builtin_bit_cast(half8, q == 3 ? f3 : fr);
+    }
+
+    float best[NG];
+    int bidx[NG];
+    bool ntie[NG];
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      best[g] = INFINITY;
+      bidx[g] = 0;
+      ntie[g] = rowbad[g];
+    }
+
+    for (int ch = 0; ch < nchunks; ++ch) {
+      const int mc0 = ch * chunk;
+      const int mcount = min(chunk, M - mc0);
+      if (nchunks > 1) {
+        __syncthreads();
+        stage_filter<NT>(E, ldw, W, mc0, mcount, chunk, lds, tid, &s_bigmin);
+        __syncthreads();
+      }
+      uint32_t cbest[NG], s2[NG];
+      int cpair[NG];
+#pragma unroll
+      for (int g = 0; g < NG; ++g) {
+        cbest[g] = 0xffffffffu;
+        s2[g] = 0xffffffffu;
+        cpair[g] = 0;
+      }
+      const char* ap = lds + a_lane;
+      half8 an0 = *reinterpret_cast<const half8*>(ap);
+      half8 an1 = *reinterpret_cast<const half8*>(ap + 256);
+      const int mlim = min(mcount, m_sweep);
+      const floatx4 zero = {0.f, 0.f, 0.f, 0.f};
+      for (int p = 0; p * 32 < mlim; ++p) {
+        const half8 a0 = an0, a1 = an1;
+        ap += 512;
+        an0 = *reinterpret_cast<const half8*>(ap);      // next pair (past the chunk: slack)
+        an1 = *reinterpret_cast<const half8*>(ap + 256);
+        floatx4 d0[NG], d1[NG];
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+          d0[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, bop[g], zero, 0, 0, 0);
+          d1[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, bop[g], zero, 0, 0, 0);
+        }
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+          uint32_t u[8];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            // by value: clang's __builtin_bit_cast of a vector-element
+            // subscript reads element 0 (seen with ROCm 7.2's clang)
+            u[r] = __float_as_uint(d0[g][r]);
+            u[4 + r] = __float_as_uint(d1[g][r]);
+          }
+          const uint32_t mt = min(min(min(u[0], u[1]), min(u[2], u[3])),
+                                  min(min(u[4], u[5]), min(u[6], u[7])));
+          s2[g] = umed3(mt, cbest[g], s2[g]);          // min(s2, max(mt, cbest)): cbest <= s2
+          cpair[g] = mt < cbest[g] ? p : cpair[g];     // strict: the earliest pair wins ties
+          cbest[g] = min(mt, cbest[g]);
+        }
+      }
+      // ---- resolve, spread over the 4 q-lanes of a row
+      const unsigned int bigm = s_bigmin;
+#pragma unroll
+      for (int g = 0; g < NG; ++g) {
+        const uint32_t rmin = qmin_u(cbest[g]);
+        const int mykey = cpair[g] * 4 + q;
+        const int key = qmin_i(cbest[g] == rmin ? mykey : 0x7fffffff);
+        // smallest score outside the 8 recomputed codewords
+        const uint32_t sec = qmin_u(key == mykey ? s2[g] : cbest[g]);
+        const float fmin = __uint_as_float(rmin);
+        const float fsec = __uint_as_float(sec);
+        const float tmin = fmin - (sx[g] + 1.f);
+        const float delta = (978.f * sx[g] + 390.f * fabsf(tmin) + 489.f) * 5.9604645e-8f;
+        bool exact_ok = (fsec - fmin > delta) && (delta < 0.25f);
+        if (bigm != 0x7f800000u) {                    // out-of-range codewords staged
+          // v_sqrt_f32 (1 ulp): the 1e-4 margin below covers it
+          const float r = __builtin_amdgcn_sqrtf(__uint_as_float(bigm)) -
+                          __builtin_amdgcn_sqrtf(sx[g]);
+          exact_ok = exact_ok && r > 0.f && r * r * 0.9999f > fmin + delta;
+        }
+        // lane q recomputes candidates (t = q >> 1, r = 2 (q & 1) + {0, 1}) of
+        // the winner lane's quad in the winning pair, in index order over q
+        const int pw = key >> 2, qw = key & 3;
+        const int c0i = pw * 32 + (q >> 1) * 16 + 4 * qw + 2 * (q & 1);
+        const float4 x0 = *reinterpret_cast<const float4*>(xs + (g * 16 + j) * 8);
+        const float4 x1 = *reinterpret_cast<const float4*>(xs + (g * 16 + j) * 8 + 4);
+        const float xr[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+        float dd[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int ci = c0i + u;
+          const bool cv = ci < mcount;
+          const float* er = E + (int64_t)(mc0 + (cv ? ci : 0)) * ldw;
+          float e[8];
+          if (vec_rows && W > 4) {
+            const float4 t0 = *reinterpret_cast<const float4*>(er);
+            const float4 t1 = *reinterpret_cast<const float4*>(er + 4);
+            e[0] = t0.x; e[1] = t0.y; e[2] = t0.z; e[3] = t0.w;
+            e[4] = t1.x; e[5] = t1.y; e[6] = t1.z; e[7] = t1.w;
+          } else if (vec_rows && W == 4) {
+            const float4 t0 = *reinterpret_cast<const float4*>(er);
+            e[0] = t0.x; e[1] = t0.y; e[2] = t0.z; e[3] = t0.w;
+            e[4] = e[5] = e[6] = e[7] = 0.f;
+          } else {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) e[k] = k < W ? er[k] : 0.f;
+          }
+          float dot = 0.f;
+#pragma unroll
+          for (int k = 0; k < 8; ++k)
+            if (k < W) dot = (k == 0) ? __fmul_rn(e[k], xr[k]) : fmaf(e[k], xr[k], dot);
+          const float se_c = sef[cv ? ci : 0];
+          dd[u] = cv ? fmaf(-2.f, dot, __fadd_rn(sx[g], se_c)) : INFINITY;
+        }
+        float dm = dd[0];
+        int im = c0i;
+        if (dd[1] < dm) {
+          dm = dd[1];
+          im = c0i + 1;
+        }
+        qmin_lex(dm, im);
+        if (dm < best[g]) {                           // earlier chunk wins ties
+          best[g] = dm;
+          bidx[g] = mc0 + im;
+        }
+        ntie[g] = ntie[g] || (!exact_ok && m_sweep >= mcount);
+      }
+    }
+
+    // ---- outputs: lane (q, j) writes group q's row j; a near-tie row is
+    // appended to the workgroup's list instead (resolved after the row loop)
+    {
+      bool nq = ntie[0];
+#pragma unroll
+      for (int g = 1; g < NG; ++g) nq = q == g ? ntie[g] : nq;
+      const int lrow = row0 + q * 16 + j;
+      const bool live = q < NG && lrow < part_end;
+      const bool near_tie = live && nq;
+      if (live && !near_tie) {
+        const int m = pickn<NG>(bidx, q);
+        if (idx_out) idx_out[(int64_t)b * B + lrow] = (int64_t)m;
+        if (idx32) idx32[(int64_t)b * B + lrow] = m;
+        if (codes) codes[batch_idx[lrow] * ldc + b] = (int16_t)m;
+      }
+      const uint64_t am = __ballot(near_tie);
+      if (am) {                                       // wave-uniform
+        int base = 0;
+        if (lane == 0) base = atomicAdd(&s_nflag, __popcll(am));
+        base = __shfl(base, 0);
+        if (near_tie) flist[base + __popcll(am & ((1ull << lane) - 1))] = lrow;
+      }
+    }
+
+    if constexpr (FUSED) {   // lane q adds k-slots 2q, 2q+1 of its row
+#pragma unroll
+      for (int g = 0; g < NG; ++g) {
+        if (row0 + g * 16 + j < part_end && !ntie[g]) {
+          const float2 v2 = *reinterpret_cast<const float2*>(xs + (g * 16 + j) * 8 + 2 * q);
+          unsigned long long* a = acc + bidx[g] * (W + 1);
+          if (q == 0) atomicAdd(a, 1ull);
+          if (kvalid(0)) atomicAdd(a + 1 + 2 * q, to_fixed(v2.x, kgrad(0) ? shift_g : shift_f));
+          if (kvalid(1)) atomicAdd(a + 2 + 2 * q, to_fixed(v2.y, kgrad(1) ? shift_g : shift_f));
+        }
+      }
+    }
+  }
+
+  // ---- near-tie rows of this workgroup: one wave per row sweeps every
+  // codeword in vq.py's arithmetic (BatchNorm apply, |x|^2 and |e|^2 summed
+  // in k order, the k-ordered dot, fma(-2, dot, |x|^2 + |e|^2)) and takes the
+  // lexicographic (distance, index) minimum -- torch.argmin's first index
+  __syncthreads();
+  const int n_near = s_nflag;
+  for (int i = wave; i < n_near; i += WV) {
+    const int row = flist[i];
+    float xv[8];
+    float sxr = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float v = 0.f;
+      if (k < W) {
+        const bool gk = W != D && k >= D;
+        const int c = b * D + (gk ? k - D : k);
+        const float raw = gk ? Gr[(int64_t)row * ldg + c] : X[(int64_t)row * ldx + c];
+        v = __fmul_rn(fmaf(__fsub_rn(raw, coef[(gk ? 5 * F : 4 * F) + c]),
+                           coef[(gk ? 2 * F : 0) + c], coef[(gk ? 3 * F : F) + c]),
+                      gk ? grad_scale : 1.f);
+        sxr = (k == 0) ? __fmul_rn(v, v) : __fadd_rn(sxr, __fmul_rn(v, v));
+      }
+      xv[k] = v;
+    }
+    float bd = INFINITY;
+    int bm = 0x7fffffff;
+    for (int m = lane; m < M; m += 64) {
+      const float* er = E + (int64_t)m * ldw;
+      float dot = 0.f, se_m = 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        if (k < W) {
+          const float ek = er[k];
+          dot = (k == 0) ? __fmul_rn(ek, xv[k]) : fmaf(ek, xv[k], dot);
+          se_m = (k == 0) ? __fmul_rn(ek, ek) : __fadd_rn(se_m, __fmul_rn(ek, ek));
+        }
+      }
+      const float dd = fmaf(-2.f, dot, __fadd_rn(sxr, se_m));
+      if (dd < bd) {                                  // increasing m: the first index stays
+        bd = dd;
+        bm = m;
+      }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {               // lexicographic (d, m) minimum
+      const float od = __shfl_xor(bd, o);
+      const int om = __shfl_xor(bm, o);
+      if (od < bd || (od == bd && om < bm)) {
+        bd = od;
+        bm = om;
+      }
+    }
+    if (lane == 0) {
+      if (idx_out) idx_out[(int64_t)b * B + row] = (int64_t)bm;
+      if (idx32) idx32[(int64_t)b * B + row] = bm;
+      if (codes) codes[batch_idx[row] * ldc + b] = (int16_t)bm;
+    }
+    if constexpr (FUSED) {
+      unsigned long long* a = acc + bm * (W + 1);
+      if (lane == 0) atomicAdd(a, 1ull);
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (k < W && lane == k)
+          atomicAdd(a + 1 + k, to_fixed(xv[k], (W != D && k >= D) ? shift_g : shift_f));
     }
   }
 
@@ -1668,11 +2244,21 @@ extern "C" int32_t vqgnn_vq_ema_parts(int32_t B, int32_t nb, int32_t M, int32_t 
   return (B <= 0 || nb <= 0 || M <= 0 || W <= 0) ? 0 : 1;
 }
 
+// Workspace of vq_assign: [the non-fused EMA path's row indices][the
+// filtered path's per-workgroup near-tie row lists: rows_per_part ints per
+// workgroup]
+static size_t idx32_bytes(const AssignGeom& g, int B, int nb) {
+  return g.fused ? 256 : align_up((size_t)nb * B * sizeof(int), 256);
+}
+static size_t flag_bytes(const AssignGeom& g, int nb) {
+  if (!g.filter) return 0;
+  return align_up((size_t)g.parts * nb * g.rows_per_part * sizeof(int), 256);
+}
+
 extern "C" size_t vqgnn_vq_assign_workspace(int32_t B, int32_t nb, int32_t M, int32_t W) {
   if (B <= 0 || nb <= 0 || M <= 0 || W <= 0) return 0;
   const AssignGeom g = assign_geom(B, nb, M, W);
-  // the non-fused EMA path's row indices
-  return g.fused ? 256 : align_up((size_t)nb * B * sizeof(int), 256);
+  return idx32_bytes(g, B, nb) + flag_bytes(g, nb);
 }
 
 // Measurement facility for bench.py: while enabled, every vq_assign_kernel
@@ -1694,6 +2280,11 @@ static void timing_events(hipEvent_t* a, hipEvent_t* b) {
   }
   g_timing_ev.emplace_back(*a, *b);
 }
+
+static int launch_ema_tail(const float* X, int64_t ldx, const float* G, int64_t ldg, int B,
+                           int nb, int D, int M, int W, const float* coef, float grad_scale,
+                           const int* idx32, unsigned long long* parts, const AssignGeom& g,
+                           const StatShift& sh, hipStream_t s);
 
 template <int KC>
 static int launch_assign(const float* X, int64_t ldx, const float* G, int64_t ldg, int B,
@@ -1750,6 +2341,17 @@ static int launch_assign(const float* X, int64_t ldx, const float* G, int64_t ld
 #undef VQ_LAUNCH
   int rc = check_launch("vq_assign");
   if (rc || !want_ema || fused) return rc;
+  return launch_ema_tail(X, ldx, G, ldg, B, nb, D, M, W, coef, grad_scale, idx32, parts, g, sh, s);
+}
+
+// EMA statistics after an assign that could not fuse them (row indices in
+// idx32): one workgroup per (branch, part) with an LDS slab, or the split
+// kernel when the slab exceeds the LDS
+static int launch_ema_tail(const float* X, int64_t ldx, const float* G, int64_t ldg, int B,
+                           int nb, int D, int M, int W, const float* coef, float grad_scale,
+                           const int* idx32, unsigned long long* parts, const AssignGeom& g,
+                           const StatShift& sh, hipStream_t s) {
+  const int wgs = g.parts * nb;
   const size_t acc_bytes = (size_t)M * (W + 1) * sizeof(unsigned long long);
   if (acc_bytes <= kLdsBudget) {
     if (acc_bytes > 64 * 1024)
@@ -1786,6 +2388,67 @@ static int launch_assign(const float* X, int64_t ldx, const float* G, int64_t ld
   return check_launch("vq_ema_partial");
 }
 
+
+// Filtered path (W <= 8): vq_filter_kernel (near-tie rows included).
+static int launch_filter(const float* X, int64_t ldx, const float* G, int64_t ldg, int B, int nb,
+                         int D, int M, int W, const float* coef, float grad_scale,
+                         const float* emb, int ldw, int64_t emb_bstride, int64_t* idx_out,
+                         int16_t* codes, int64_t ldc, const int64_t* batch_idx,
+                         unsigned long long* parts, int ema_zeroed, int64_t stat_count,
+                         void* workspace, hipStream_t s) {
+  const AssignGeom g = assign_geom(B, nb, M, W);
+  const StatShift sh = stat_shift(stat_count, grad_scale);
+  const bool want_ema = parts != nullptr;
+  const bool fused = want_ema && g.fused;
+  int* idx32 = (want_ema && !g.fused) ? reinterpret_cast<int*>(workspace) : nullptr;
+  int* flags = reinterpret_cast<int*>(reinterpret_cast<char*>(workspace) + idx32_bytes(g, B, nb));
+  // the geometry sized the slab in when the EMA statistics fuse; without
+  // them the kernel does not touch it (the same LDS is reserved)
+  size_t lds = g.lds;
+  if (g.fused && !fused) lds -= (size_t)M * (W + 1) * sizeof(unsigned long long);
+  if (lds > kLdsBudget) {
+    set_error("vq_assign: LDS %zu B exceeds 160 KiB (M=%d W=%d)", lds, M, W);
+    return VQGNN_ERR_UNSUPPORTED;
+  }
+  const int wgs = g.parts * nb;
+  const int wm = flt_mode(W, D, ldx, ldg, X, G);
+  if (want_ema && !ema_zeroed)
+    (void)hipMemsetAsync(parts, 0, (size_t)nb * M * (W + 1) * sizeof(unsigned long long), s);
+  static const int msw_env = env_int_vq("VQGNN_ASSIGN_MSWEEP", -1);
+  const int m_sweep = msw_env >= 0 ? msw_env : (1 << 30);
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  timing_events(&ev0, &ev1);
+#define FLT_LAUNCH(FU, WMV, WVV)                                                              \
+  do {                                                                                        \
+    const void* fn = (const void*)vq_filter_kernel<FU, WMV, WVV>;                             \
+    if (lds > 64 * 1024)                                                                      \
+      (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);    \
+    hipExtLaunchKernelGGL((vq_filter_kernel<FU, WMV, WVV>), dim3(wgs), dim3(WVV * 64),          \
+                          (uint32_t)lds, s, ev0, ev1, 0, X, ldx, G, ldg, B, nb, D, M, W,       \
+                          coef, grad_scale, emb, ldw, emb_bstride, idx_out, codes, ldc,        \
+                          batch_idx, idx32, parts, flags, g.rows_per_part, g.chunk, sh.f,      \
+                          sh.g, m_sweep);                                                      \
+  } while (0)
+#define FLT_LAUNCH_WV(FU, WMV)                                                                \
+  do {                                                                                        \
+    if (g.wv == 16) FLT_LAUNCH(FU, WMV, 16);                                                  \
+    else FLT_LAUNCH(FU, WMV, 8);                                                              \
+  } while (0)
+#define FLT_LAUNCH_WM(FU)                                                                     \
+  do {                                                                                        \
+    if (wm == 1) FLT_LAUNCH_WV(FU, 1);                                                        \
+    else if (wm == 2) FLT_LAUNCH_WV(FU, 2);                                                   \
+    else FLT_LAUNCH_WV(FU, 0);                                                                \
+  } while (0)
+  if (fused) FLT_LAUNCH_WM(true); else FLT_LAUNCH_WM(false);
+#undef FLT_LAUNCH_WM
+#undef FLT_LAUNCH_WV
+#undef FLT_LAUNCH
+  const int rc = check_launch("vq_filter");
+  if (rc || !want_ema || fused) return rc;
+  return launch_ema_tail(X, ldx, G, ldg, B, nb, D, M, W, coef, grad_scale, idx32, parts, g, sh, s);
+}
+
 extern "C" int vqgnn_vq_assign(const float* X, int64_t ldx, const float* G, int64_t ldg,
                                int32_t B, int32_t nb, int32_t D, int32_t M, int32_t W,
                                const float* coef, float grad_scale, const float* embedding,
@@ -1802,7 +2465,8 @@ extern "C" int vqgnn_vq_assign(const float* X, int64_t ldx, const float* G, int6
   VQGNN_REQUIRE(W == D || (G && ldg >= (int64_t)nb * D), "vq_assign: grads required for W=2D");
   VQGNN_REQUIRE(ldw >= W && emb_bstride >= (int64_t)M * ldw, "vq_assign: bad codebook layout");
   VQGNN_REQUIRE(!codes || (batch_idx && ldc >= nb), "vq_assign: codes needs batch_idx, ldc>=nb");
-  VQGNN_REQUIRE(!ema_parts || workspace, "vq_assign: workspace required for EMA statistics");
+  VQGNN_REQUIRE(workspace || (!ema_parts && !use_filter(W)),
+                "vq_assign: workspace required (vqgnn_vq_assign_workspace)");
   VQGNN_REQUIRE(M <= 32767 || !codes, "vq_assign: int16 codes need M <= 32767");
   VQGNN_REQUIRE(!ema_parts || stat_count >= B, "vq_assign: stat_count < B");
   VQGNN_REQUIRE((int64_t)B * ldx * 4 < ((int64_t)1 << 32) &&
@@ -1810,6 +2474,10 @@ extern "C" int vqgnn_vq_assign(const float* X, int64_t ldx, const float* G, int6
                 "vq_assign: B*ldx (and B*ldg) must span < 4 GiB");
   hipStream_t s = as_stream(stream);
   unsigned long long* parts = reinterpret_cast<unsigned long long*>(ema_parts);
+  if (use_filter(W))
+    return launch_filter(X, ldx, G, ldg, B, nb, D, M, W, coef, grad_scale, embedding, ldw,
+                         emb_bstride, idx_out, codes, ldc, batch_idx, parts, ema_zeroed,
+                         stat_count, workspace, s);
   const int kc = W <= 4 ? 1 : (W <= 8 ? 2 : 4);
   if (kc == 1)
     return launch_assign<1>(X, ldx, G, ldg, B, nb, D, M, W, coef, grad_scale, embedding, ldw,
