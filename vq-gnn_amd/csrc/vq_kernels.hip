@@ -668,11 +668,9 @@ static size_t flt_lds_bytes(int chunk) {
   return (size_t)kFltBytesPerCode * (chunk + kFltSlack);
 }
 
-// Per-wave row scratch of vq_filter_kernel (after the codebook planes and
-// the fused slab): [NG][16 rows][8] f32 normalised rows, then [16 rows][8]
-// dwords of f16 pairs (x_hi pairs k = 2q, 2q+1 at dword q, x_lo pairs at
-// dword 4 + q), shared by the row groups one after the other
-constexpr int kFltScratch = kAsgGroups * 512 + 512;
+// Per-wave fragment buffer of vq_filter_kernel (after the codebook planes
+// and the fused slab): [16 rows][12 dwords], one row group at a time
+constexpr int kFltScratch = 16 * 48;
 
 // filtered assignment for W <= 8 (section 3b)
 template <bool FUSED, int WM, int WV>
@@ -809,7 +807,8 @@ static AssignGeom assign_geom(int B, int nb, int M, int W) {
   const int wenv = env_int_vq("VQGNN_ASG_WAVES", 0);
   if (wenv == 8 || wenv == 16) g.wv = wenv;
   g.lds = lds + (g.wv == 16 ? 2 * scr8 : scr8);
-  const int rows_per_iter = g.wv * 16 * kAsgGroups;
+  // rows per workgroup iteration: the filter's lanes own one row each
+  const int rows_per_iter = g.filter ? g.wv * 64 : g.wv * 16 * kAsgGroups;
   const int row_blocks = (B + rows_per_iter - 1) / rows_per_iter;
   // one full round of resident workgroups: parts x nb <= what the device
   // holds at once (every part has the same row count, so no tail round)
@@ -1308,40 +1307,34 @@ __device__ __forceinline__ void stage_filter(const float* __restrict__ E, int ld
 }
 
 
-// minimum over the 4 q-lanes of a row (lanes j, j+16, j+32, j+48): the
-// gfx950 permlane swaps hand each lane {v[l], v[l ^ 32]} and then
-// {v[l], v[l ^ 16]} as VALU operations (no LDS traffic)
-__device__ __forceinline__ uint32_t qmin_u(uint32_t v) {
-  const auto a = __builtin_amdgcn_permlane32_swap(v, v, false, false);
-  v = min((uint32_t)a[0], (uint32_t)a[1]);
-  const auto c = __builtin_amdgcn_permlane16_swap(v, v, false, false);
-  return min((uint32_t)c[0], (uint32_t)c[1]);
-}
-__device__ __forceinline__ int qmin_i(int v) {
-  const auto a = __builtin_amdgcn_permlane32_swap((uint32_t)v, (uint32_t)v, false, false);
-  v = min((int)a[0], (int)a[1]);
-  const auto c = __builtin_amdgcn_permlane16_swap((uint32_t)v, (uint32_t)v, false, false);
-  return min((int)c[0], (int)c[1]);
-}
-// lexicographic (distance, index) minimum over the 4 q-lanes
-__device__ __forceinline__ void qmin_lex(float& d, int& i) {
-#pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    const uint32_t du = __float_as_uint(d);
-    const auto a = s == 0 ? __builtin_amdgcn_permlane32_swap(du, du, false, false)
-                          : __builtin_amdgcn_permlane16_swap(du, du, false, false);
-    const auto b = s == 0 ? __builtin_amdgcn_permlane32_swap((uint32_t)i, (uint32_t)i, false, false)
-                          : __builtin_amdgcn_permlane16_swap((uint32_t)i, (uint32_t)i, false, false);
-    const float d0 = __uint_as_float(a[0]), d1 = __uint_as_float(a[1]);
-    const int i0 = (int)b[0], i1 = (int)b[1];
-    const bool one = d1 < d0 || (d1 == d0 && i1 < i0);
-    d = one ? d1 : d0;
-    i = one ? i1 : i0;
-  }
+// 4 x 4 transpose over (quad, group) of per-lane values r[g]: afterwards
+// lane (q = g, j) holds r[t] = the value of quad t, group g, column j (two
+// permlane32 and two permlane16 swaps, VALU; scripts/probes/permlane_swap.hip)
+__device__ __forceinline__ void transpose_quads(uint32_t (&r)[4]) {
+  const auto s02 = __builtin_amdgcn_permlane32_swap(r[0], r[2], false, false);
+  r[0] = s02[0];
+  r[2] = s02[1];
+  const auto s13 = __builtin_amdgcn_permlane32_swap(r[1], r[3], false, false);
+  r[1] = s13[0];
+  r[3] = s13[1];
+  const auto s01 = __builtin_amdgcn_permlane16_swap(r[0], r[1], false, false);
+  r[0] = s01[0];
+  r[1] = s01[1];
+  const auto s23 = __builtin_amdgcn_permlane16_swap(r[2], r[3], false, false);
+  r[2] = s23[0];
+  r[3] = s23[1];
 }
 
 // WM: 2 -> W = 8 = 2D with D = 4 (features then gradients); 1 -> W = D = 4;
 //     0 -> any W <= 8
+//
+// Work layout: a wave takes 64 rows per iteration, lane l owning row row0 + l
+// (group g = l >> 4, the B columns of the g-th MFMA); the owner lane loads
+// and normalises its whole row, builds its f16 split and, after the sweep,
+// resolves it alone.  The sweep itself runs in the MFMA layout: lane (q, j)
+// keeps, for each group g, the running minimum over its quad's codewords
+// 4q .. 4q+3 of every tile; a 4 x 4 transpose over the quads (permlane
+// swaps, VALU) hands the owner lane the four quads' minima of its row.
 template <bool FUSED, int WM, int WV>
 __global__ void __launch_bounds__(WV * 64)
 vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restrict__ Gr,
@@ -1353,7 +1346,7 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
                  unsigned long long* __restrict__ partial, int* __restrict__ flags,
                  int rows_per_part, int chunk, int shift_f, int shift_g, int m_sweep) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  constexpr int NG = kAsgGroups, NT = WV * 64;
+  constexpr int NT = WV * 64;
   const int W = WM == 2 ? 8 : (WM == 1 ? 4 : W_);          // compile-time in the row modes
   const int D = WM != 0 ? 4 : D_;
   const int F = nb * D;
@@ -1367,122 +1360,136 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
   char* lds = reinterpret_cast<char*>(smem);
   const float* sef = reinterpret_cast<const float*>(lds + (size_t)48 * cs);
   unsigned long long* acc = reinterpret_cast<unsigned long long*>(lds + (size_t)52 * cs);
-  char* scr = lds + (size_t)52 * cs + (FUSED ? (size_t)M * (W + 1) * 8 : 0) +
-              (size_t)wave * kFltScratch;
-  float* xs = reinterpret_cast<float*>(scr);                          // [NG][16][8]
-  uint32_t* hl = reinterpret_cast<uint32_t*>(scr + NG * 512);         // [16][8]
+  // the wave's fragment buffer: [16 rows][12 dwords] = x_hi pairs, x_lo
+  // pairs, quad-3 parts of the 16 rows of one group
+  uint32_t* buf = reinterpret_cast<uint32_t*>(
+      lds + (size_t)52 * cs + (FUSED ? (size_t)M * (W + 1) * 8 : 0) + (size_t)wave * kFltScratch);
   const float* E = emb + (int64_t)b * emb_bstride;
   const int nchunks = (M + chunk - 1) / chunk;
   const bool vec_rows = (ldw & 3) == 0 && (emb_bstride & 3) == 0 &&
                         (reinterpret_cast<uintptr_t>(emb) & 15) == 0;
   __shared__ int s_nflag;
   __shared__ unsigned int s_bigmin;
+  // k-slot table: alpha, beta, shift, grad scale per k (field-major, so the
+  // packed-f32 normalisation reads k-pairs as register pairs); grad scale is
+  // 1 for features (v * 1 is exact)
+  __shared__ __attribute__((aligned(16))) float s_kt[4][8];
   if (tid == 0) {
     s_nflag = 0;
     s_bigmin = 0x7f800000u;                           // +inf: no out-of-range codeword
   }
-  if constexpr (FUSED) {
-    for (int i = tid; i < M * (W + 1); i += NT) acc[i] = 0ull;
-  }
-  int* const flist = flags + (int64_t)wg * rows_per_part;
-  // k-slot table in LDS: per k (alpha, beta, shift, grad scale), read back by
-  // the lanes of k-slots 2q, 2q+1 in the row phase (not held in registers
-  // across the sweep); grad scale is 1 for features (v * 1 is exact)
-  __shared__ __attribute__((aligned(16))) float s_kt[8][4];
   if (tid < 8) {
     const int k = tid;
     const bool kvv = k < W;
     const bool gk = W != D && k >= D;
     const int c = b * D + (gk ? k - D : k);
-    s_kt[k][0] = kvv ? coef[(gk ? 2 * F : 0) + c] : 0.f;
-    s_kt[k][1] = kvv ? coef[(gk ? 3 * F : F) + c] : 0.f;
-    s_kt[k][2] = kvv ? coef[(gk ? 5 * F : 4 * F) + c] : 0.f;
-    s_kt[k][3] = gk ? grad_scale : 1.f;
+    s_kt[0][k] = kvv ? coef[(gk ? 2 * F : 0) + c] : 0.f;
+    s_kt[1][k] = kvv ? coef[(gk ? 3 * F : F) + c] : 0.f;
+    s_kt[2][k] = kvv ? coef[(gk ? 5 * F : 4 * F) + c] : 0.f;
+    s_kt[3][k] = gk ? grad_scale : 1.f;
   }
-  // k-slot 2q + u of this lane: valid, a gradient column
-  auto kvalid = [&](int u) { return 2 * q + u < W; };
-  auto kgrad = [&](int u) { return W != D && 2 * q + u >= D; };
-  auto kcol = [&](int u) { return b * D + (kgrad(u) ? 2 * q + u - D : 2 * q + u); };
+  if constexpr (FUSED) {
+    for (int i = tid; i < M * (W + 1); i += NT) acc[i] = 0ull;
+  }
+  int* const flist = flags + (int64_t)wg * rows_per_part;
   __syncthreads();
   if (nchunks == 1) stage_filter<NT>(E, ldw, W, 0, M, chunk, lds, tid, &s_bigmin);
 
   const int part_begin = part * rows_per_part;
   const int part_end = min(B, part_begin + rows_per_part);
-  constexpr int RPW = 16 * NG, RPI = WV * RPW;
+  constexpr int RPI = WV * 64;
   const int n_iters = part_end > part_begin ? (part_end - part_begin + RPI - 1) / RPI : 0;
   // A-fragment byte offset of this lane: plane (q: 0 -> hi, 1 -> lo, 2 -> hi,
   // 3 -> |e|^2 parts), codeword j of tile 0
   const uint32_t a_lane = (uint32_t)(((q == 1) ? 1 : (q == 3 ? 2 : 0)) * cs + j) * 16u;
+  // B-fragment part read by this lane: x_hi (quads 0, 1), x_lo (2), quad-3 parts
+  const int bpart = q < 2 ? 0 : q - 1;
   if (nchunks == 1) __syncthreads();
 
-  for (int it = 0; it < n_iters; ++it) {
-    const int row0 = part_begin + it * RPI + wave * RPW;
-    float sx[NG];
-    half8 bop[NG];
-    bool rowbad[NG];
-    // ---- rows: lane (q, j) loads and normalises k-slots 2q, 2q+1 of row j
-    // (vq.py's bn_apply), splits them into f16 hi/lo pairs, and every lane
-    // reads its whole row back from the wave's LDS scratch
-#pragma unroll
-    for (int g = 0; g < NG; ++g) {
-      const int64_t rowi = min(row0 + g * 16 + j, part_end - 1);
-      float v[2];
-      if constexpr (WM != 0) {
-        // k = 2q, 2q+1 sit side by side in one of X / G (D = 4): one float2
-        float2 r2 = make_float2(0.f, 0.f);
-        if (kvalid(0))
-          r2 = kgrad(0) ? *reinterpret_cast<const float2*>(Gr + rowi * ldg + kcol(0))
-                        : *reinterpret_cast<const float2*>(X + rowi * ldx + kcol(0));
-        v[0] = r2.x;
-        v[1] = r2.y;
+  // the owner lane's raw row (k-slot order: features, then gradients)
+  auto load_raw = [&](int rowi, float (&raw)[8]) {
+    if constexpr (WM != 0) {
+      const float4 a = *reinterpret_cast<const float4*>(X + (int64_t)rowi * ldx + b * 4);
+      raw[0] = a.x; raw[1] = a.y; raw[2] = a.z; raw[3] = a.w;
+      if constexpr (WM == 2) {
+        const float4 c = *reinterpret_cast<const float4*>(Gr + (int64_t)rowi * ldg + b * 4);
+        raw[4] = c.x; raw[5] = c.y; raw[6] = c.z; raw[7] = c.w;
       } else {
-#pragma unroll
-        for (int u = 0; u < 2; ++u)
-          v[u] = kvalid(u) ? (kgrad(u) ? Gr[rowi * ldg + kcol(u)] : X[rowi * ldx + kcol(u)]) : 0.f;
+        raw[4] = raw[5] = raw[6] = raw[7] = 0.f;
       }
+    } else {
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const float4 t = *reinterpret_cast<const float4*>(&s_kt[2 * q + u][0]);
-        v[u] = __fmul_rn(fmaf(__fsub_rn(v[u], t.z), t.x, t.y), t.w);      // vq.py:224
+      for (int k = 0; k < 8; ++k) {
+        const bool gk = W != D && k >= D;
+        const int c = b * D + (gk ? k - D : k);
+        raw[k] = k < W ? (gk ? Gr[(int64_t)rowi * ldg + c] : X[(int64_t)rowi * ldx + c]) : 0.f;
       }
-      *reinterpret_cast<float2*>(xs + (g * 16 + j) * 8 + 2 * q) = make_float2(v[0], v[1]);
-      const half2_t h = half2_t{(_Float16)v[0], (_Float16)v[1]};
-      const half2_t l = half2_t{(_Float16)__fsub_rn(v[0], (float)h[0]),
-                                (_Float16)__fsub_rn(v[1], (float)h[1])};
-      hl[j * 8 + q] = __builtin_bit_cast(uint32_t, h);
-      hl[j * 8 + 4 + q] = __builtin_bit_cast(uint32_t, l);
-      __builtin_amdgcn_wave_barrier();
-      const float4 x0 = *reinterpret_cast<const float4*>(xs + (g * 16 + j) * 8);
-      const float4 x1 = *reinterpret_cast<const float4*>(xs + (g * 16 + j) * 8 + 4);
-      const uint4 fr = *reinterpret_cast<const uint4*>(hl + j * 8 + (q == 2 ? 4 : 0));
-      __builtin_amdgcn_wave_barrier();
-      const float xr[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-      float s = 0.f;                                  // |x|^2 in k order
+    }
+  };
+  // normalised as vq.py's bn_apply (+ vq.py:224's grad scale); returns |x|^2
+  // summed in k order
+  auto row_vals = [&](const float (&raw)[8], float (&xv)[8]) {
+    float s = 0.f;
 #pragma unroll
-      for (int k = 0; k < 8; ++k)
-        if (k < W) s = (k == 0) ? __fmul_rn(xr[k], xr[k]) : __fadd_rn(s, __fmul_rn(xr[k], xr[k]));
-      sx[g] = s;
-      rowbad[g] = !(s < 65536.f);
+    for (int k = 0; k < 8; ++k) {
+      float v = 0.f;
+      if (k < W) {
+        v = __fmul_rn(fmaf(__fsub_rn(raw[k], s_kt[2][k]), s_kt[0][k], s_kt[1][k]), s_kt[3][k]);
+        s = (k == 0) ? __fmul_rn(v, v) : __fadd_rn(s, __fmul_rn(v, v));
+      }
+      xv[k] = v;
+    }
+    return s;
+  };
+
+  float raw[8];                                       // the next row, loaded ahead
+  if (n_iters > 0) load_raw(min(part_begin + wave * 64 + lane, part_end - 1), raw);
+  for (int it = 0; it < n_iters; ++it) {
+    const int row0 = part_begin + it * RPI + wave * 64;
+    const bool live = row0 + lane < part_end;
+    float sx;
+    half8 bop[4];
+    float xr[8];                                      // the row: scores, resolve, EMA
+    {
+      float (&xv)[8] = xr;
+      sx = row_vals(raw, xv);
+      if (it + 1 < n_iters)                           // in flight under the sweep
+        load_raw(min(row0 + RPI + lane, part_end - 1), raw);
+      uint32_t hw[4], lw[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const half2_t h = half2_t{(_Float16)xv[2 * i], (_Float16)xv[2 * i + 1]};
+        const half2_t l = half2_t{(_Float16)__fsub_rn(xv[2 * i], (float)h[0]),
+                                  (_Float16)__fsub_rn(xv[2 * i + 1], (float)h[1])};
+        hw[i] = __builtin_bit_cast(uint32_t, h);
+        lw[i] = __builtin_bit_cast(uint32_t, l);
+      }
       // quad 3: (1, 1, 1, |x|^2 + 1 split in three f16, 0, 0)
-      const float c1 = __fadd_rn(s, 1.f);
+      const float c1 = __fadd_rn(sx, 1.f);
       const _Float16 c0 = (_Float16)c1;
       const float r1 = __fsub_rn(c1, (float)c0);
       const _Float16 cl = (_Float16)r1;
       const _Float16 cll = (_Float16)__fsub_rn(r1, (float)cl);
       const uint4 f3 = {0x3c003c00u, __builtin_bit_cast(uint32_t, half2_t{(_Float16)1.f, c0}),
                         __builtin_bit_cast(uint32_t, half2_t{cl, cll}), 0u};
-      bop[g] = __builtin_bit_cast(half8, q == 3 ? f3 : fr);
-    }
-
-    float best[NG];
-    int bidx[NG];
-    bool ntie[NG];
+      // group g's owners (lanes 16g + j) publish their row's parts, every
+      // lane (q, j) reads part q of row (g, j): its B fragment for group g
 #pragma unroll
-    for (int g = 0; g < NG; ++g) {
-      best[g] = INFINITY;
-      bidx[g] = 0;
-      ntie[g] = rowbad[g];
+      for (int g = 0; g < 4; ++g) {
+        if (q == g) {
+          uint4* w = reinterpret_cast<uint4*>(buf + j * 12);
+          w[0] = uint4{hw[0], hw[1], hw[2], hw[3]};
+          w[1] = uint4{lw[0], lw[1], lw[2], lw[3]};
+          w[2] = f3;
+        }
+        __builtin_amdgcn_wave_barrier();
+        bop[g] = __builtin_bit_cast(half8, *reinterpret_cast<const uint4*>(buf + j * 12 + 4 * bpart));
+        __builtin_amdgcn_wave_barrier();
+      }
     }
+    float best = INFINITY;
+    int bidx = 0;
+    bool ntie = !(sx < 65536.f);
 
     for (int ch = 0; ch < nchunks; ++ch) {
       const int mc0 = ch * chunk;
@@ -1492,150 +1499,140 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
         stage_filter<NT>(E, ldw, W, mc0, mcount, chunk, lds, tid, &s_bigmin);
         __syncthreads();
       }
-      uint32_t cbest[NG], s2[NG];
-      int cpair[NG];
+      uint32_t cb[4], s2[4];
+      int cp[4];
 #pragma unroll
-      for (int g = 0; g < NG; ++g) {
-        cbest[g] = 0xffffffffu;
+      for (int g = 0; g < 4; ++g) {
+        cb[g] = 0xffffffffu;
         s2[g] = 0xffffffffu;
-        cpair[g] = 0;
+        cp[g] = 0;
       }
       const char* ap = lds + a_lane;
-      half8 an0 = *reinterpret_cast<const half8*>(ap);
-      half8 an1 = *reinterpret_cast<const half8*>(ap + 256);
       const int mlim = min(mcount, m_sweep);
       const floatx4 zero = {0.f, 0.f, 0.f, 0.f};
-      for (int p = 0; p * 32 < mlim; ++p) {
-        const half8 a0 = an0, a1 = an1;
-        ap += 512;
-        an0 = *reinterpret_cast<const half8*>(ap);      // next pair (past the chunk: slack)
-        an1 = *reinterpret_cast<const half8*>(ap + 256);
-        floatx4 d0[NG], d1[NG];
+      for (int p = 0; p * 32 < mlim; ++p, ap += 512) {
+        const half8 a0 = *reinterpret_cast<const half8*>(ap);
+        const half8 a1 = *reinterpret_cast<const half8*>(ap + 256);
+        uint32_t m4[4];
+        {
+          floatx4 d[4];
 #pragma unroll
-        for (int g = 0; g < NG; ++g) {
-          d0[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, bop[g], zero, 0, 0, 0);
-          d1[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, bop[g], zero, 0, 0, 0);
+          for (int g = 0; g < 4; ++g) d[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, bop[g], zero, 0, 0, 0);
+#pragma unroll
+          for (int g = 0; g < 4; ++g)   // by value: clang's __builtin_bit_cast of a vector-element
+                                        // subscript reads element 0 (ROCm 7.2's clang)
+            m4[g] = min(min(__float_as_uint(d[g][0]), __float_as_uint(d[g][1])),
+                        min(__float_as_uint(d[g][2]), __float_as_uint(d[g][3])));
         }
+        // one tile's four accumulators in flight at a time (register budget)
+        __builtin_amdgcn_sched_barrier(0);
+        {
+          floatx4 d[4];
 #pragma unroll
-        for (int g = 0; g < NG; ++g) {
-          uint32_t u[8];
+          for (int g = 0; g < 4; ++g) d[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, bop[g], zero, 0, 0, 0);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            // by value: clang's __builtin_bit_cast of a vector-element
-            // subscript reads element 0 (seen with ROCm 7.2's clang)
-            u[r] = __float_as_uint(d0[g][r]);
-            u[4 + r] = __float_as_uint(d1[g][r]);
+          for (int g = 0; g < 4; ++g) {
+            const uint32_t mt = min(min(m4[g], min(__float_as_uint(d[g][0]), __float_as_uint(d[g][1]))),
+                                    min(__float_as_uint(d[g][2]), __float_as_uint(d[g][3])));
+            s2[g] = umed3(mt, cb[g], s2[g]);            // min(s2, max(mt, cb)): cb <= s2
+            cp[g] = mt < cb[g] ? p : cp[g];             // strict: the earliest pair wins ties
+            cb[g] = min(mt, cb[g]);
           }
-          const uint32_t mt = min(min(min(u[0], u[1]), min(u[2], u[3])),
-                                  min(min(u[4], u[5]), min(u[6], u[7])));
-          s2[g] = umed3(mt, cbest[g], s2[g]);          // min(s2, max(mt, cbest)): cbest <= s2
-          cpair[g] = mt < cbest[g] ? p : cpair[g];     // strict: the earliest pair wins ties
-          cbest[g] = min(mt, cbest[g]);
         }
       }
-      // ---- resolve, spread over the 4 q-lanes of a row
+      // ---- hand the owner lane the four quads' statistics of its row: a
+      // 4 x 4 transpose over (quad, group); keys carry their quad (index order
+      // = pair, then quad)
+      uint32_t kk[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) kk[g] = (uint32_t)(cp[g] * 4 + q);
+      transpose_quads(cb);
+      transpose_quads(s2);
+      transpose_quads(kk);
+      // ---- resolve (owner lane)
+      const uint32_t rmin = min(min(cb[0], cb[1]), min(cb[2], cb[3]));
+      uint32_t key = 0xffffffffu;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) key = min(key, cb[t] == rmin ? kk[t] : 0xffffffffu);
+      uint32_t sec = 0xffffffffu;                     // smallest score outside the 8 candidates
+#pragma unroll
+      for (int t = 0; t < 4; ++t) sec = min(sec, kk[t] == key ? s2[t] : cb[t]);
+      const float fmin = __uint_as_float(rmin);
+      const float fsec = __uint_as_float(sec);
+      const float tmin = fmin - (sx + 1.f);
+      const float delta = (978.f * sx + 390.f * fabsf(tmin) + 489.f) * 5.9604645e-8f;
+      bool exact_ok = (fsec - fmin > delta) && (delta < 0.25f);
       const unsigned int bigm = s_bigmin;
-#pragma unroll
-      for (int g = 0; g < NG; ++g) {
-        const uint32_t rmin = qmin_u(cbest[g]);
-        const int mykey = cpair[g] * 4 + q;
-        const int key = qmin_i(cbest[g] == rmin ? mykey : 0x7fffffff);
-        // smallest score outside the 8 recomputed codewords
-        const uint32_t sec = qmin_u(key == mykey ? s2[g] : cbest[g]);
-        const float fmin = __uint_as_float(rmin);
-        const float fsec = __uint_as_float(sec);
-        const float tmin = fmin - (sx[g] + 1.f);
-        const float delta = (978.f * sx[g] + 390.f * fabsf(tmin) + 489.f) * 5.9604645e-8f;
-        bool exact_ok = (fsec - fmin > delta) && (delta < 0.25f);
-        if (bigm != 0x7f800000u) {                    // out-of-range codewords staged
-          // v_sqrt_f32 (1 ulp): the 1e-4 margin below covers it
-          const float r = __builtin_amdgcn_sqrtf(__uint_as_float(bigm)) -
-                          __builtin_amdgcn_sqrtf(sx[g]);
-          exact_ok = exact_ok && r > 0.f && r * r * 0.9999f > fmin + delta;
-        }
-        // lane q recomputes candidates (t = q >> 1, r = 2 (q & 1) + {0, 1}) of
-        // the winner lane's quad in the winning pair, in index order over q
-        const int pw = key >> 2, qw = key & 3;
-        const int c0i = pw * 32 + (q >> 1) * 16 + 4 * qw + 2 * (q & 1);
-        const float4 x0 = *reinterpret_cast<const float4*>(xs + (g * 16 + j) * 8);
-        const float4 x1 = *reinterpret_cast<const float4*>(xs + (g * 16 + j) * 8 + 4);
-        const float xr[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-        float dd[2];
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const int ci = c0i + u;
-          const bool cv = ci < mcount;
-          const float* er = E + (int64_t)(mc0 + (cv ? ci : 0)) * ldw;
-          float e[8];
-          if (vec_rows && W > 4) {
-            const float4 t0 = *reinterpret_cast<const float4*>(er);
-            const float4 t1 = *reinterpret_cast<const float4*>(er + 4);
-            e[0] = t0.x; e[1] = t0.y; e[2] = t0.z; e[3] = t0.w;
-            e[4] = t1.x; e[5] = t1.y; e[6] = t1.z; e[7] = t1.w;
-          } else if (vec_rows && W == 4) {
-            const float4 t0 = *reinterpret_cast<const float4*>(er);
-            e[0] = t0.x; e[1] = t0.y; e[2] = t0.z; e[3] = t0.w;
-            e[4] = e[5] = e[6] = e[7] = 0.f;
-          } else {
-#pragma unroll
-            for (int k = 0; k < 8; ++k) e[k] = k < W ? er[k] : 0.f;
-          }
-          float dot = 0.f;
-#pragma unroll
-          for (int k = 0; k < 8; ++k)
-            if (k < W) dot = (k == 0) ? __fmul_rn(e[k], xr[k]) : fmaf(e[k], xr[k], dot);
-          const float se_c = sef[cv ? ci : 0];
-          dd[u] = cv ? fmaf(-2.f, dot, __fadd_rn(sx[g], se_c)) : INFINITY;
-        }
-        float dm = dd[0];
-        int im = c0i;
-        if (dd[1] < dm) {
-          dm = dd[1];
-          im = c0i + 1;
-        }
-        qmin_lex(dm, im);
-        if (dm < best[g]) {                           // earlier chunk wins ties
-          best[g] = dm;
-          bidx[g] = mc0 + im;
-        }
-        ntie[g] = ntie[g] || (!exact_ok && m_sweep >= mcount);
+      if (bigm != 0x7f800000u) {                      // out-of-range codewords staged
+        // v_sqrt_f32 (1 ulp): the 1e-4 margin below covers it
+        const float r = __builtin_amdgcn_sqrtf(__uint_as_float(bigm)) - __builtin_amdgcn_sqrtf(sx);
+        exact_ok = exact_ok && r > 0.f && r * r * 0.9999f > fmin + delta;
       }
+      // the 8 candidates (winning pair pw, quad qw: codewords pw*32 + 16t +
+      // 4qw + r) in the reference arithmetic, in index order: strict < keeps
+      // the first index of a tie
+      const int pw = (int)(key >> 2), qw = (int)(key & 3);
+      float dm = INFINITY;
+      int im = 0;
+#pragma unroll 2
+      for (int c = 0; c < 8; ++c) {
+        const int ci = pw * 32 + (c >> 2) * 16 + 4 * qw + (c & 3);
+        const bool cv = ci < mcount;
+        const float* er = E + (int64_t)(mc0 + (cv ? ci : 0)) * ldw;
+        float e[8];
+        if (vec_rows && W > 4) {
+          const float4 t0 = *reinterpret_cast<const float4*>(er);
+          const float4 t1 = *reinterpret_cast<const float4*>(er + 4);
+          e[0] = t0.x; e[1] = t0.y; e[2] = t0.z; e[3] = t0.w;
+          e[4] = t1.x; e[5] = t1.y; e[6] = t1.z; e[7] = t1.w;
+        } else if (vec_rows && W == 4) {
+          const float4 t0 = *reinterpret_cast<const float4*>(er);
+          e[0] = t0.x; e[1] = t0.y; e[2] = t0.z; e[3] = t0.w;
+          e[4] = e[5] = e[6] = e[7] = 0.f;
+        } else {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) e[k] = k < W ? er[k] : 0.f;
+        }
+        float dot = 0.f;
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          if (k < W) dot = (k == 0) ? __fmul_rn(e[k], xr[k]) : fmaf(e[k], xr[k], dot);
+        const float se_c = sef[cv ? ci : 0];
+        const float dd = cv ? fmaf(-2.f, dot, __fadd_rn(sx, se_c)) : INFINITY;
+        if (dd < dm) {
+          dm = dd;
+          im = ci;
+        }
+      }
+      if (dm < best) {                                // earlier chunk wins ties
+        best = dm;
+        bidx = mc0 + im;
+      }
+      ntie = ntie || (!exact_ok && m_sweep >= mcount);
     }
 
-    // ---- outputs: lane (q, j) writes group q's row j; a near-tie row is
-    // appended to the workgroup's list instead (resolved after the row loop)
-    {
-      bool nq = ntie[0];
-#pragma unroll
-      for (int g = 1; g < NG; ++g) nq = q == g ? ntie[g] : nq;
-      const int lrow = row0 + q * 16 + j;
-      const bool live = q < NG && lrow < part_end;
-      const bool near_tie = live && nq;
-      if (live && !near_tie) {
-        const int m = pickn<NG>(bidx, q);
-        if (idx_out) idx_out[(int64_t)b * B + lrow] = (int64_t)m;
-        if (idx32) idx32[(int64_t)b * B + lrow] = m;
-        if (codes) codes[batch_idx[lrow] * ldc + b] = (int16_t)m;
-      }
-      const uint64_t am = __ballot(near_tie);
-      if (am) {                                       // wave-uniform
-        int base = 0;
-        if (lane == 0) base = atomicAdd(&s_nflag, __popcll(am));
-        base = __shfl(base, 0);
-        if (near_tie) flist[base + __popcll(am & ((1ull << lane) - 1))] = lrow;
-      }
+    // ---- outputs (owner lane); a near-tie row is appended to the
+    // workgroup's list instead (resolved after the row loop)
+    const bool near_tie = live && ntie;
+    if (live && !ntie) {
+      if (idx_out) idx_out[(int64_t)b * B + row0 + lane] = (int64_t)bidx;
+      if (idx32) idx32[(int64_t)b * B + row0 + lane] = bidx;
+      if (codes) codes[batch_idx[row0 + lane] * ldc + b] = (int16_t)bidx;
     }
-
-    if constexpr (FUSED) {   // lane q adds k-slots 2q, 2q+1 of its row
+    const uint64_t am = __ballot(near_tie);
+    if (am) {                                         // wave-uniform
+      int base = 0;
+      if (lane == 0) base = atomicAdd(&s_nflag, __popcll(am));
+      base = __shfl(base, 0);
+      if (near_tie) flist[base + __popcll(am & ((1ull << lane) - 1))] = row0 + lane;
+    }
+    if constexpr (FUSED) {
+      if (live && !ntie) {
+        unsigned long long* a = acc + bidx * (W + 1);
+        atomicAdd(a, 1ull);
 #pragma unroll
-      for (int g = 0; g < NG; ++g) {
-        if (row0 + g * 16 + j < part_end && !ntie[g]) {
-          const float2 v2 = *reinterpret_cast<const float2*>(xs + (g * 16 + j) * 8 + 2 * q);
-          unsigned long long* a = acc + bidx[g] * (W + 1);
-          if (q == 0) atomicAdd(a, 1ull);
-          if (kvalid(0)) atomicAdd(a + 1 + 2 * q, to_fixed(v2.x, kgrad(0) ? shift_g : shift_f));
-          if (kvalid(1)) atomicAdd(a + 2 + 2 * q, to_fixed(v2.y, kgrad(1) ? shift_g : shift_f));
-        }
+        for (int k = 0; k < 8; ++k)
+          if (k < W) atomicAdd(a + 1 + k, to_fixed(xr[k], (W != D && k >= D) ? shift_g : shift_f));
       }
     }
   }
