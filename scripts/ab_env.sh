@@ -1,13 +1,24 @@
 #!/bin/bash
-# Interleaved A/B of environment settings on one box: ab_env.sh "name=VAR=val,VAR2=val ..." [bench args]
-set -o pipefail
+# Interleaved A/B of environment settings for one library: bench lines per
+# setting and config, repeated; prints ms/step and the assign kernel's own
+# duration.   ab_env.sh "NAME=VAL;NAME2=VAL ..." [configs "cfg:semantics ..."]
+# (settings separated by spaces; "-" = no extra variable)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-VARS="$1"; shift
+O=gpurun_out/${TAG:-abenv}
+mkdir -p $O
+CFGS="${2:-arxiv_gcn:update}"
 for rep in 1 2; do
-  for v in $VARS; do
-    n=${v%%=*}; e=${v#*=}
-    envs=(); [ "$e" != "none" ] && IFS=, read -ra envs <<< "$e"
-    env "${envs[@]}" timeout -k 10 200 python bench.py --no-cpu-baseline "$@" > gpurun_out/abe_$n.json 2>/dev/null || exit 1
-    python -c "import json; d=json.loads(open('gpurun_out/abe_$n.json').read().strip().splitlines()[-1]); print('$n', round(d['ms_per_step'],4), round(d['kernels']['spmm_ms'],4))"
+  for cs in $CFGS; do
+    cfg=${cs%%:*}; sem=${cs#*:}
+    i=0
+    for setting in $1; do
+      i=$((i+1))
+      envs=""
+      [ "$setting" != "-" ] && envs=$(echo "$setting" | tr ';' ' ')
+      f=$O/ab${i}_${cfg}_${sem}_$rep
+      env $envs timeout -k 10 200 python bench.py --no-cpu-baseline --steps 30 --warmup 5 --config $cfg \
+        --semantics $sem > $f.json 2> $f.err || exit 1
+      python3 -c "import json; d=json.loads(open('$f.json').read().strip().splitlines()[-1]); k=d['kernels']['vq_assign']; print('$rep $cfg $sem [$setting]', 'ms/step %.4f'%d['ms_per_step'], 'assign us %.1f'%(k['ms_per_launch']*1e3))"
+    done
   done
 done

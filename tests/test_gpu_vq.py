@@ -65,9 +65,9 @@ def test_assign_bit_exact_given_coefficients(M, D, W, B, tie):
 
 @pytest.mark.parametrize("M,W", [(256, 8), (256, 4), (1024, 8), (4096, 8), (40, 8)])
 def test_assign_near_ties_resolved_exactly(M, W):
-    """The filtered sweep (t' = |e|^2 - 2 x.e from the MFMA) sends rows whose
-    minimum is within its error bound of another codeword to the exact
-    near-tie kernel.  Crafted ties: exact duplicate codewords, codewords one
+    """The filtered sweep (f16-split scores on the MFMA) sends rows whose
+    minimum is within its error bound of another codeword's score to the
+    exact near-tie sweep.  Crafted ties: exact duplicate codewords, codewords one
     or two ulps apart, and rows placed on the bisector of two codewords --
     every index equals the pinned sequential arithmetic's (first index on
     exact ties; helpers.sequential_argmin -- at the ulp level the box's MKL
@@ -106,6 +106,54 @@ def test_assign_near_ties_resolved_exactly(M, W):
         assert n_mis == 0, f"M={M} W={W} branch {b}: {n_mis} index mismatches"
         assert torch.equal(codes.cpu()[batch_idx, b].long(), r)
         assert torch.equal(st[b, :, 0], torch.bincount(r, minlength=M))
+
+
+@pytest.mark.parametrize("W", [8, 4])
+def test_assign_out_of_range_codewords_and_rows(W):
+    """The filter's range limits: codewords with |e|^2 >=
+    2^15 are scored +inf and admitted only through the per-workgroup norm
+    test, rows with |x|^2 >= 2^16 take the exact sweep.  Branch 0: dead
+    codewords with huge norms (|e|^2 up to 10^10, as a trained codebook's
+    unused entries reach); branch 1: codewords just past the range with half
+    of the rows placed next to them (they must win); branch 2: every 7th row
+    scaled past |x|^2 = 2^16, and codewords of the same scale.  Indices equal
+    the pinned sequential arithmetic's, EMA counts agree."""
+    D, nb, B, N, M = 4, 3, 3000, 6000, 256
+    g = torch.Generator().manual_seed(77 + W)
+    emb = torch.randn(nb, M, 2 * D, generator=g) * 0.7
+    emb[0, 5] *= 1e5
+    emb[0, 77] *= 3e4
+    emb[0, 200] = 1e4
+    big = torch.randn(16, 2 * D, generator=g)
+    big = big / big[:, :W].norm(dim=1, keepdim=True) * 190.0        # |e|^2 ~ 36100 > 2^15
+    emb[1, 100:116] = big
+    emb[2, 40:60] *= 300.0
+    X = torch.randn(B, nb * D, generator=g)
+    G = torch.randn(B, nb * D, generator=g) * 1e-3
+    c = torch.randint(0, 16, (B // 2,), generator=g)
+    near = big[c] + 0.01 * torch.randn(B // 2, 2 * D, generator=g)
+    X[: B // 2, D:2 * D] = near[:, :D]
+    G[: B // 2, D:2 * D] = near[:, D:]
+    X[::7, 2 * D:3 * D] *= 300.0
+    G[::7, 2 * D:3 * D] = X[::7, 2 * D:3 * D] * 0.5
+    coef = torch.zeros(6, nb * D)
+    coef[0] = coef[2] = 1.0
+    batch_idx = torch.randperm(N, generator=g)[:B]
+    codes = torch.full((N, nb), -1, dtype=torch.int16, device=DEV)
+    idx = torch.empty(nb, B, dtype=torch.long, device=DEV)
+    stats = kernels.vq_assign(X.to(DEV), G.to(DEV) if W == 2 * D else None, coef.to(DEV), 1.0,
+                              emb.to(DEV), D, W, idx_out=idx, codes=codes,
+                              batch_idx=batch_idx.to(DEV), want_stats=True)
+    st = kernels.vq_ema_reduce(stats)[0].cpu()
+    for b in range(nb):
+        xn = torch.cat([X[:, b * D:(b + 1) * D], G[:, b * D:(b + 1) * D]], 1)[:, :W]
+        r = torch.from_numpy(sequential_argmin(xn.numpy(), emb[b].numpy()))
+        n_mis = int((idx.cpu()[b] != r).sum())
+        assert n_mis == 0, f"W={W} branch {b}: {n_mis} index mismatches"
+        assert torch.equal(codes.cpu()[batch_idx, b].long(), r)
+        assert torch.equal(st[b, :, 0], torch.bincount(r, minlength=M))
+        if b == 1:                          # the out-of-range codewords do win their rows
+            assert (r[: B // 2] >= 100).float().mean() > 0.9
 
 
 def test_assign_multibranch_strided_views_and_codes():

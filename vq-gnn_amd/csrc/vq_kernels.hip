@@ -588,6 +588,7 @@ struct AssignGeom {
   int wv;             // waves per workgroup (8 or 16)
   bool filter;        // vq_filter_kernel (W <= 8) instead of vq_assign_kernel
   size_t lds;         // dynamic LDS of the filter kernel's launch
+  int elds;           // filter: f32 codebook copy in LDS for the resolve
 };
 
 template <int KC>
@@ -682,7 +683,7 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
                  int64_t* __restrict__ idx_out, int16_t* __restrict__ codes, int64_t ldc,
                  const int64_t* __restrict__ batch_idx, int* __restrict__ idx32,
                  unsigned long long* __restrict__ partial, int* __restrict__ flags,
-                 int rows_per_part, int chunk, int shift_f, int shift_g, int m_sweep);
+                 int rows_per_part, int chunk, int shift_f, int shift_g, int m_sweep, int elds);
 
 // the filter's row-load mode: 2 -> W = 8 = 2D, D = 4; 1 -> W = D = 4 (float4
 // rows, aligned); 0 -> general
@@ -807,6 +808,20 @@ static AssignGeom assign_geom(int B, int nb, int M, int W) {
   const int wenv = env_int_vq("VQGNN_ASG_WAVES", 0);
   if (wenv == 8 || wenv == 16) g.wv = wenv;
   g.lds = lds + (g.wv == 16 ? 2 * scr8 : scr8);
+  // the filter's f32 codebook copy, when it fits without costing resident
+  // workgroups (VQGNN_FLT_ELDS=0/1 forces it off/on where it fits)
+  g.elds = 0;
+  if (g.filter) {
+    const size_t ef = (size_t)(g.chunk + kFltSlack) * 32;
+    const int wmv = wm;
+    const int cap = g.wv == 16 ? cap16 : cap8;
+    const int env = env_int_vq("VQGNN_FLT_ELDS", -1);
+    if (g.lds + ef <= kLdsBudget && env != 0 &&
+        (env == 1 || assign_capacity(g.kc, g.fused, wmv, g.lds + ef, g.wv, true) >= cap)) {
+      g.elds = 1;
+      g.lds += ef;
+    }
+  }
   // rows per workgroup iteration: the filter's lanes own one row each
   const int rows_per_iter = g.filter ? g.wv * 64 : g.wv * 16 * kAsgGroups;
   const int row_blocks = (B + rows_per_iter - 1) / rows_per_iter;
@@ -1261,7 +1276,7 @@ __device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
 template <int NT>
 __device__ __forceinline__ void stage_filter(const float* __restrict__ E, int ldw, int W, int mc0,
                                              int mcount, int chunk, char* smem, int tid,
-                                             unsigned int* bigmin) {
+                                             unsigned int* bigmin, float* ef = nullptr) {
   const int cs = chunk + kFltSlack;
   half8* p0 = reinterpret_cast<half8*>(smem);
   half8* p1 = p0 + cs;
@@ -1303,6 +1318,10 @@ __device__ __forceinline__ void stage_filter(const float* __restrict__ E, int ld
     p1[m] = lo;
     p2[m] = sp;
     sef[m] = mv ? s : INFINITY;
+    if (ef) {
+      reinterpret_cast<float4*>(ef)[2 * m] = make_float4(e[0], e[1], e[2], e[3]);
+      reinterpret_cast<float4*>(ef)[2 * m + 1] = make_float4(e[4], e[5], e[6], e[7]);
+    }
   }
 }
 
@@ -1344,7 +1363,7 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
                  int64_t* __restrict__ idx_out, int16_t* __restrict__ codes, int64_t ldc,
                  const int64_t* __restrict__ batch_idx, int* __restrict__ idx32,
                  unsigned long long* __restrict__ partial, int* __restrict__ flags,
-                 int rows_per_part, int chunk, int shift_f, int shift_g, int m_sweep) {
+                 int rows_per_part, int chunk, int shift_f, int shift_g, int m_sweep, int elds) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int NT = WV * 64;
   const int W = WM == 2 ? 8 : (WM == 1 ? 4 : W_);          // compile-time in the row modes
@@ -1364,6 +1383,12 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
   // pairs, quad-3 parts of the 16 rows of one group
   uint32_t* buf = reinterpret_cast<uint32_t*>(
       lds + (size_t)52 * cs + (FUSED ? (size_t)M * (W + 1) * 8 : 0) + (size_t)wave * kFltScratch);
+  // the chunk's codewords in f32 [cs][8] for the resolve's exact candidates
+  // (elds: when the LDS has room; else they are read from global memory)
+  float* ef = elds ? reinterpret_cast<float*>(lds + (size_t)52 * cs +
+                                              (FUSED ? (size_t)M * (W + 1) * 8 : 0) +
+                                              (size_t)WV * kFltScratch)
+                   : nullptr;
   const float* E = emb + (int64_t)b * emb_bstride;
   const int nchunks = (M + chunk - 1) / chunk;
   const bool vec_rows = (ldw & 3) == 0 && (emb_bstride & 3) == 0 &&
@@ -1393,7 +1418,7 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
   }
   int* const flist = flags + (int64_t)wg * rows_per_part;
   __syncthreads();
-  if (nchunks == 1) stage_filter<NT>(E, ldw, W, 0, M, chunk, lds, tid, &s_bigmin);
+  if (nchunks == 1) stage_filter<NT>(E, ldw, W, 0, M, chunk, lds, tid, &s_bigmin, ef);
 
   const int part_begin = part * rows_per_part;
   const int part_end = min(B, part_begin + rows_per_part);
@@ -1496,7 +1521,7 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
       const int mcount = min(chunk, M - mc0);
       if (nchunks > 1) {
         __syncthreads();
-        stage_filter<NT>(E, ldw, W, mc0, mcount, chunk, lds, tid, &s_bigmin);
+        stage_filter<NT>(E, ldw, W, mc0, mcount, chunk, lds, tid, &s_bigmin, ef);
         __syncthreads();
       }
       uint32_t cb[4], s2[4];
@@ -1580,7 +1605,12 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
         const bool cv = ci < mcount;
         const float* er = E + (int64_t)(mc0 + (cv ? ci : 0)) * ldw;
         float e[8];
-        if (vec_rows && W > 4) {
+        if (ef) {                                     // staged f32 copy (k >= W staged as 0)
+          const float4 t0 = reinterpret_cast<const float4*>(ef)[2 * ci];
+          const float4 t1 = reinterpret_cast<const float4*>(ef)[2 * ci + 1];
+          e[0] = t0.x; e[1] = t0.y; e[2] = t0.z; e[3] = t0.w;
+          e[4] = t1.x; e[5] = t1.y; e[6] = t1.z; e[7] = t1.w;
+        } else if (vec_rows && W > 4) {
           const float4 t0 = *reinterpret_cast<const float4*>(er);
           const float4 t1 = *reinterpret_cast<const float4*>(er + 4);
           e[0] = t0.x; e[1] = t0.y; e[2] = t0.z; e[3] = t0.w;
@@ -2424,7 +2454,7 @@ static int launch_filter(const float* X, int64_t ldx, const float* G, int64_t ld
                           (uint32_t)lds, s, ev0, ev1, 0, X, ldx, G, ldg, B, nb, D, M, W,       \
                           coef, grad_scale, emb, ldw, emb_bstride, idx_out, codes, ldc,        \
                           batch_idx, idx32, parts, flags, g.rows_per_part, g.chunk, sh.f,      \
-                          sh.g, m_sweep);                                                      \
+                          sh.g, m_sweep, g.elds);                                              \
   } while (0)
 #define FLT_LAUNCH_WV(FU, WMV)                                                                \
   do {                                                                                        \
