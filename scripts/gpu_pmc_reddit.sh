@@ -19,6 +19,7 @@ for cfg in ${CONFIGS:-reddit_gcn reddit_gcn_l1}; do
       [ -z "$line" ] && continue
       i=$((i+1))
       d=$O/${cfg}_${what}/p$i
+      mkdir -p $O/${cfg}_${what}
       echo "== $(date +%T) $cfg $what pass $i: $line"
       CONFIG=$cfg REPS=3 timeout -s KILL 240 rocprofv3 --pmc $line --kernel-trace -d $d -o run \
         --output-format csv -- python scripts/pmc_target.py $what > $d.log 2>&1
