@@ -289,7 +289,9 @@ def main():
     assign_ms = float(np.mean(assign_ms_list))
 
     # Algorithmic work per launch:
-    #  vq_assign_kernel: 2*B*M*W flops per branch (the distance contraction);
+    #  the assign: 2*B*M*W flops per branch (the distance contraction in f32,
+    #  the exact path's work; for W <= 8 vq_filter_kernel scores on f16 MFMA
+    #  and recomputes only the candidates);
     #  SpMM (spmm_task_kernel + spmm_task_fixup_kernel): rowptr + (col, val) + every
     #  input row once (x and x_first_order) + the output rows.
     spmm_bytes = 4 * (n + 1) + 8 * nnz + 4 * n * F + 4 * n * F
@@ -309,10 +311,21 @@ def main():
         # the kernel's own floor: the same plan shape with every column folded
         # onto 1,024 hot rows (all gathers hit L2), DESIGN.md §4.2
         rl_spmm["floor_ms"], rl_spmm["floor_note"] = spmm_floor(kernels, adj, Xd, B, n, nnz, F)
-    rl_vq = dict(kernel="vq_assign_kernel", bound="mfma",
+    if args.config in FABRIC_CEILING:
+        # counter-backed ceiling of the per-edge row gathers:
+        # L2-miss bytes measured per launch at the fabric rate they saturate
+        gb, hit, rate = FABRIC_CEILING[args.config]
+        rl_spmm["ceiling_ms"] = gb / rate
+        rl_spmm["ceiling_note"] = (f"{gb:.1f} GB of L2-miss (MALL/HBM) traffic per launch at "
+                                   f"L2 hit {hit:.2f}, at the {rate:.2f} TB/s the gathers saturate "
+                                   "(profiles/r03_reddit_spmm_pmc.txt)")
+    asg_name = ("vq_filter_kernel" if W <= 8 and os.environ.get("VQGNN_ASSIGN_EXACT", "0") in ("", "0")
+                else "vq_assign_kernel")
+    rl_vq = dict(kernel=asg_name, bound="mfma",
                  achieved=vq_flops / (assign_ms * 1e-3) / 1e12, peak=157.3, unit="TFLOP/s",
                  flops_per_launch=vq_flops, ms_per_launch=assign_ms,
-                 traffic=pmc.get("vq_assign_kernel"))
+                 flops_note="2*B*M*W*nb f32 distance flops over the f32 matrix peak",
+                 traffic=pmc.get(asg_name))
     rl_vq["frac"] = rl_vq["achieved"] / rl_vq["peak"]
     dominant = rl_spmm if spmm_ms >= assign_ms else rl_vq
     roofline = dict(bound=dominant["bound"], achieved=dominant["achieved"], peak=dominant["peak"],
@@ -377,6 +390,13 @@ def lib_digest():
         for blk in iter(lambda: f.read(1 << 20), b""):
             h.update(blk)
     return h.hexdigest()
+
+
+# reddit SpMM: fabric (L2-miss) read + write GB per launch, L2 hit rate, and the
+# fabric rate in TB/s the per-edge gathers reach (the same 7.2-7.4 TB/s at F =
+# 128 and 604 and for the tiled plan's remainder pass), from the PMC passes
+# of scripts/gpu_pmc_reddit.sh (profiles/r03_reddit_spmm_pmc.txt)
+FABRIC_CEILING = {"reddit_gcn": (27.2, 0.56, 7.39), "reddit_gcn_l1": (164.8, 0.54, 7.39)}
 
 
 def load_pmc(args):

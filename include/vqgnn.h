@@ -264,59 +264,6 @@ int vqgnn_spmm_task(const int32_t* rowptr, int32_t n_rows, int32_t n_cols, int64
                     const int64_t* records, int32_t K, int32_t n_jobs, int32_t n_empty,
                     void* workspace, vqgnn_stream_t stream);
 
-/*     vqgnn_spmm_task_acc: the same product added into out (out[row] =
- *     out[row] + the row's chain; rows without edges keep their value) — the
- *     sparse remainder behind vqgnn_spmm_tile (6f).                          */
-int vqgnn_spmm_task_acc(const int32_t* rowptr, int32_t n_rows, int32_t n_cols, int64_t nnz,
-                        int32_t B, const float* X, int64_t ldx, const float* X2, int64_t ldx2,
-                        int32_t F, float* out, int64_t ldo, const int32_t* plan,
-                        const int64_t* records, int32_t K, int32_t n_jobs, int32_t n_empty,
-                        void* workspace, vqgnn_stream_t stream);
-
-/* 6f. Tiled SpMM for adjacencies with dense blocks (reddit-shaped batches:
- *     ~80 % of a row's edges inside its cluster's few thousand consecutive
- *     columns).  Same product as 6 / 6e, split into
- *       - dense blocks: windows of R = 256 rows x tiles of C = 128 columns holding
- *         >= min_edges edges.  vqgnn_spmm_tile: one workgroup per (window,
- *         64-float column slice) stages each dense block's 256 source rows in
- *         LDS once (with its row pointers and, per 64 rows, its records) and
- *         accumulates its rows in registers; it writes EVERY row
- *         (rows without dense edges as zeros);
- *       - the sparse remainder: a CSR of the other edges, added by
- *         vqgnn_spmm_task_acc with its own task plan.
- *     Per row: the dense blocks' chains in column-tile order, then the sparse
- *     chain added once — deterministic, within 1e-5 relative of the fp64 sum.
- *     Plan (once per batch adjacency, any F):
- *       vqgnn_spmm_tile_dims -> W windows, T tiles (nblk = W * T < 2^28), R, C;
- *       vqgnn_spmm_tile_plan_count fills grid [2 * nblk + 1] int32 (edges per
- *         block, then the dense block ids' exclusive scan) and counts[2]
- *         (device: dense blocks, their edges), which the caller reads;
- *       vqgnn_spmm_tile_plan_fill fills blocks [n_dense + W + 1] (dense block
- *         keys w*T+t, then each window's first block), rowptr_b
- *         [n_dense][257], boff [n_dense + 1], records drec [rec_cap] int64
- *         (local column, weight; padding = (C, 0))
- *         (per (row, block) padded to 4 edges: rec_cap >= dense edges + 3 *
- *         (dense row segments)), and the sparse CSR s_rowptr [n_rows + 1],
- *         s_col / s_val [nnz - dense edges]; segcnt is scratch [n_dense][256].
- *     Workspace of both plan calls: vqgnn_spmm_tile_plan_workspace bytes.
- *     drec 16-byte aligned.  Replaces convs.py:95 like 6.                    */
-int vqgnn_spmm_tile_dims(int32_t n_rows, int32_t n_cols, int32_t* windows, int32_t* tiles,
-                         int32_t* rows_per_window, int32_t* cols_per_tile);
-size_t vqgnn_spmm_tile_plan_workspace(int32_t n_rows, int32_t n_cols, int64_t nnz);
-int vqgnn_spmm_tile_plan_count(const int32_t* rowptr, const int32_t* col, int32_t n_rows,
-                               int32_t n_cols, int64_t nnz, int32_t min_edges, int32_t* grid,
-                               int32_t* counts, void* workspace, vqgnn_stream_t stream);
-int vqgnn_spmm_tile_plan_fill(const int32_t* rowptr, const int32_t* col, const float* val,
-                              int32_t n_rows, int32_t n_cols, int64_t nnz, const int32_t* grid,
-                              int32_t n_dense, int32_t* blocks, int32_t* rowptr_b, int32_t* boff,
-                              int32_t* segcnt, int64_t* drec, int64_t rec_cap, int32_t* s_rowptr,
-                              int32_t* s_col, float* s_val, void* workspace,
-                              vqgnn_stream_t stream);
-int vqgnn_spmm_tile(int32_t n_rows, int32_t n_cols, int32_t B, const float* X, int64_t ldx,
-                    const float* X2, int64_t ldx2, int32_t F, float* out, int64_t ldo,
-                    const int32_t* blocks, int32_t n_dense, const int32_t* rowptr_b,
-                    const int32_t* boff, const int64_t* drec, vqgnn_stream_t stream);
-
 /* 7. CSR transpose (structure + values) for the backward product
  *    dX = A^T dOut (torch_sparse matmul autograd, convs.py:95).  Output CSR of
  *    A^T with rows sorted by column of A; within a row, entries ordered by
@@ -374,7 +321,7 @@ int vqgnn_gat_edge_grad(const int32_t* rows, const int32_t* col, const float* co
  *     params[2] of vqgnn_gat_alpha), the ones column as a per-row
  *     coefficient sum, and rows < norm_B divided by that sum + 1e-16 before
  *     the store (models.py:188; norm_B = 0: no normalisation).  Replaces
- *     vqgnn_gat_coef + vqgnn_spmm + vqgnn_gat_normalize; the coefficients are
+ *     vqgnn_gat_coef + vqgnn_spmm_task + vqgnn_gat_normalize; the coefficients are
  *     never materialised unless coef (optional, [nnz], CSR order) is given for
  *     the backward; den (optional, [n_rows]) receives the sums.  erow: the
  *     COO row of every edge (vqgnn_csr_expand_rows).  Plan and workspace as

@@ -1,6 +1,6 @@
 """Run one hot-path kernel a few times on a bench config's batch (PMC target).
 CONFIG=<bench config> (reddit configs build graph and batch on the device);
-argv[1]: step | vq | spmm | spmm_tile (the opt-in tiled SpMM's plan)."""
+argv[1]: step | vq | spmm."""
 import os
 import sys
 
@@ -41,12 +41,12 @@ for i in range(nb):
 bank = bank.to(dev)
 bank.feature_update(X, 0, nb, True, codes=codes, batch_idx=bidx)
 xt, _ = kernels.gather_codewords(subset, b.B, codes, bank.emb_out, D)
-plan = adj.plan(F, B=b.B, kind="tile" if what == "spmm_tile" else None)
+plan = adj.plan(F, B=b.B)
 torch.cuda.synchronize()
 for _ in range(reps):
     if what in ("vq", "step"):
         bank.update(X, G, 0, nb, True, codes=codes, batch_idx=bidx)
-    if what in ("spmm", "step", "spmm_tile"):
+    if what in ("spmm", "step"):
         xt, _ = kernels.gather_codewords(subset, b.B, codes, bank.emb_out, D)
         kernels.spmm(adj.rowptr, adj.col, adj.value, b.n, b.nnz, X, F, X2=xt, B=b.B, plan=plan)
 torch.cuda.synchronize()

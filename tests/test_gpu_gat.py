@@ -166,7 +166,7 @@ def _hub_csr(n, B, rng):
 
 
 @pytest.mark.parametrize("F", [32, 128, 256])
-def test_gat_fused_kernel_matches_coefficient_path(F, monkeypatch):
+def test_gat_fused_kernel_matches_coefficient_path(F):
     """vqgnn_gat_spmm_task (coefficients in the aggregation kernel) against the
     coefficient pass + task SpMM on coefficient records + normalise, on hub
     rows cut across tasks,
@@ -211,8 +211,7 @@ def test_gat_fused_kernel_matches_coefficient_path(F, monkeypatch):
     again, _, _ = kernels.gat_spmm(adj.rowptr, adj.col, adj.value, n, nnz, x, F, al, ar, params,
                                    plan, adj.rows(), X2=xf, B=B, norm_B=B)
     assert torch.equal(out, again)
-    # the layer path runs the same fused kernel (also with the tiled plan asked for)
-    monkeypatch.setenv("VQGNN_SPMM", "tile")
+    # the layer path runs the same fused kernel
     assert torch.equal(conv.fused_forward(x, adj, xf, B), out)
 
 

@@ -62,21 +62,6 @@ SIGNATURES = {
     "vqgnn_spmm_task": (ctypes.c_int, [_c_void_p, _i32, _i32, _i64, _i32, _c_void_p, _i64,
                                        _c_void_p, _i64, _i32, _c_void_p, _i64, _c_void_p,
                                        _c_void_p, _i32, _i32, _i32, _c_void_p, _c_void_p]),
-    "vqgnn_spmm_task_acc": (ctypes.c_int, [_c_void_p, _i32, _i32, _i64, _i32, _c_void_p, _i64,
-                                           _c_void_p, _i64, _i32, _c_void_p, _i64, _c_void_p,
-                                           _c_void_p, _i32, _i32, _i32, _c_void_p, _c_void_p]),
-    "vqgnn_spmm_tile_dims": (ctypes.c_int, [_i32, _i32, _c_void_p, _c_void_p, _c_void_p,
-                                            _c_void_p]),
-    "vqgnn_spmm_tile_plan_workspace": (_size, [_i32, _i32, _i64]),
-    "vqgnn_spmm_tile_plan_count": (ctypes.c_int, [_c_void_p, _c_void_p, _i32, _i32, _i64, _i32,
-                                                  _c_void_p, _c_void_p, _c_void_p, _c_void_p]),
-    "vqgnn_spmm_tile_plan_fill": (ctypes.c_int, [_c_void_p, _c_void_p, _c_void_p, _i32, _i32,
-                                                 _i64, _c_void_p, _i32, _c_void_p, _c_void_p,
-                                                 _c_void_p, _c_void_p, _c_void_p, _i64, _c_void_p,
-                                                 _c_void_p, _c_void_p, _c_void_p, _c_void_p]),
-    "vqgnn_spmm_tile": (ctypes.c_int, [_i32, _i32, _i32, _c_void_p, _i64, _c_void_p, _i64, _i32,
-                                       _c_void_p, _i64, _c_void_p, _i32, _c_void_p, _c_void_p,
-                                       _c_void_p, _c_void_p]),
     "vqgnn_gat_att_grad_workspace": (_size, [_i32, _i32, _i32]),
     "vqgnn_gat_att_grad": (ctypes.c_int, [_c_void_p, _i64, _c_void_p, _i64, _i32, _i32, _i32,
                                           _i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p,

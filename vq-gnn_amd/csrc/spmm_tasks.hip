@@ -65,8 +65,6 @@ struct TaskArgs {
   uint32_t span, offx, ldxb, offx2, ldx2b;
   uint32_t ldob;            // near path: ldo in bytes (rows addressed with a 24-bit multiply)
   int dbg;                  // experiments: 1 = no row stores (results invalid)
-  int accum;                // 1: out[row] += the row's sum (vqgnn_spmm_task_acc: the
-                            // sparse remainder behind the tile kernel); empty rows kept
   // GAT mode (OurGATConv + the layer's ones-column normalisation): edge
   // weight = exp(leaky(al[j]/s + ar[i]/s)) * w, rows < norm_B divided by
   // their coefficient sum + 1e-16
@@ -336,19 +334,10 @@ __device__ __forceinline__ void task_walk(const TaskArgs& a, int wv, int nwaves)
           }
           den = 0.f;
         }
-        const bool addto = !GAT && a.accum && !head;
 #pragma unroll
         for (int i = 0; i < NC; ++i) {
-          if (pv[i] && !(a.dbg & 1)) {
-            float4* d4 = reinterpret_cast<float4*>(dst + 4 * (c4base + G * i));
-            float4 v = acc[i];
-            if (addto) {                   // dense partial first, then this chain
-              const float4 o = *d4;
-              v = make_float4(__fadd_rn(o.x, v.x), __fadd_rn(o.y, v.y), __fadd_rn(o.z, v.z),
-                              __fadd_rn(o.w, v.w));
-            }
-            *d4 = v;
-          }
+          if (pv[i] && !(a.dbg & 1))
+            *reinterpret_cast<float4*>(dst + 4 * (c4base + G * i)) = acc[i];
           acc[i] = make_float4(0.f, 0.f, 0.f, 0.f);
         }
         const uint32_t skip = (x >> kSkipShift) & kSkipEsc;
@@ -438,7 +427,6 @@ spmm_task_fixup_kernel(TaskArgs a) {
       }
       for (; u < t; ++u) sum = add4(sum, c4[((int64_t)u * 2 + 1) * C4 + c]);
       sum = add4(sum, c4[(int64_t)t * 2 * C4 + c]);
-      if (!GAT && a.accum) sum = add4(reinterpret_cast<const float4*>(a.out + (int64_t)r * a.ldo)[c], sum);
       if (norm) {
         sum.x = __fdiv_rn(sum.x, q);
         sum.y = __fdiv_rn(sum.y, q);
@@ -453,7 +441,7 @@ spmm_task_fixup_kernel(TaskArgs a) {
       if (a.den && lane == 0 && r0 >= 0 && r0 < a.n_rows) a.den[r0] = 0.f;
     }
     const int r = a.jobs[3 * a.ntasks + (w - a.n_jobs)];    // the empty-row list
-    if (r < 0 || r >= a.n_rows || a.accum) return;
+    if (r < 0 || r >= a.n_rows) return;
     float4* o = reinterpret_cast<float4*>(a.out + (int64_t)r * a.ldo);
     for (int c = lane; c < F4; c += L) o[c] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
@@ -685,23 +673,6 @@ extern "C" int vqgnn_spmm_task(const int32_t* rowptr, int32_t n_rows, int32_t n_
   if (rc != VQGNN_OK) return rc;
   task_launch<false>(a, near, as_stream(stream));
   return check_launch("spmm_task");
-}
-
-extern "C" int vqgnn_spmm_task_acc(const int32_t* rowptr, int32_t n_rows, int32_t n_cols,
-                                   int64_t nnz, int32_t B, const float* X, int64_t ldx,
-                                   const float* X2, int64_t ldx2, int32_t F, float* out,
-                                   int64_t ldo, const int32_t* plan, const int64_t* records,
-                                   int32_t K, int32_t n_jobs, int32_t n_empty, void* workspace,
-                                   vqgnn_stream_t stream) {
-  clear_error();
-  TaskArgs a{};
-  bool near = false;
-  const int rc = task_setup(a, rowptr, n_rows, n_cols, nnz, B, X, ldx, X2, ldx2, F, out, ldo,
-                            plan, records, K, n_jobs, n_empty, workspace, &near);
-  if (rc != VQGNN_OK) return rc;
-  a.accum = 1;
-  task_launch<false>(a, near, as_stream(stream));
-  return check_launch("spmm_task_acc");
 }
 
 extern "C" int vqgnn_gat_spmm_task(const int32_t* rowptr, int32_t n_rows, int32_t n_cols,

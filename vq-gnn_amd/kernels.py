@@ -280,70 +280,6 @@ class TaskPlan:
 TASK_K = 64
 
 
-class TilePlan:
-    """Tiled SpMM plan (include/vqgnn.h §6f): the dense (256-row window x
-    128-column tile) blocks as padded LDS-tile records, plus the sparse
-    remainder as its own CSR with a TaskPlan; built once per batch adjacency,
-    valid for any F.  spmm() runs vqgnn_spmm_tile then vqgnn_spmm_task_acc."""
-
-    def __init__(self, **kw):
-        self.__dict__.update(kw)
-
-
-TILE_MIN_EDGES = 256          # a block is dense with >= 2 edges per staged row
-TILE_MIN_FRACTION = 0.5       # use the tiled path when >= half the edges are dense
-
-
-def spmm_tile_plan(rowptr, col, val, n_rows, n_cols, nnz, min_edges=None, min_fraction=None):
-    """-> TilePlan, or None when fewer than min_fraction of the edges sit in
-    dense blocks (then the task plan is the better choice)."""
-    import os
-    L = lib()
-    dev = rowptr.device
-    min_edges = int(min_edges or os.environ.get("VQGNN_TILE_MIN", TILE_MIN_EDGES))
-    min_fraction = float(min_fraction if min_fraction is not None else
-                         os.environ.get("VQGNN_TILE_FRACTION", TILE_MIN_FRACTION))
-    n_rows, n_cols, nnz = int(n_rows), int(n_cols), int(nnz)
-    Wc, Tc, Rc, Cc = (ctypes.c_int32() for _ in range(4))
-    L.vqgnn_spmm_tile_dims(n_rows, n_cols, ctypes.byref(Wc), ctypes.byref(Tc), ctypes.byref(Rc),
-                           ctypes.byref(Cc))
-    W, T, R, C = Wc.value, Tc.value, Rc.value, Cc.value
-    nblk = W * T
-    if nnz == 0 or nblk >= 1 << 28:
-        return None
-    ws = workspace(L.vqgnn_spmm_tile_plan_workspace(n_rows, n_cols, nnz), dev)
-    grid = torch.empty(2 * nblk + 1, dtype=torch.int32, device=dev)
-    counts = torch.empty(2, dtype=torch.int32, device=dev)
-    check(L.vqgnn_spmm_tile_plan_count(ptr(rowptr), ptr(col), n_rows, n_cols, nnz, min_edges,
-                                       ptr(grid), ptr(counts), ptr(ws), stream_ptr()),
-          "spmm_tile_plan_count")
-    n_dense, dense_edges = (int(v) for v in counts.tolist())
-    if dense_edges < min_fraction * nnz:
-        return None
-    i32 = dict(dtype=torch.int32, device=dev)
-    blocks = torch.empty(n_dense + W + 1, **i32)
-    rowptr_b = torch.empty(max(n_dense, 1) * (R + 1), **i32)
-    boff = torch.empty(n_dense + 1, **i32)
-    segcnt = torch.empty(max(n_dense, 1) * R, **i32)
-    rec_cap = dense_edges + 3 * min(n_dense * R, dense_edges)
-    drec = torch.empty(max(rec_cap, 2), dtype=torch.int64, device=dev)
-    s_nnz = nnz - dense_edges
-    s_rowptr = torch.empty(n_rows + 1, **i32)
-    s_col = torch.empty(max(s_nnz, 1), **i32)
-    s_val = torch.empty(max(s_nnz, 1), dtype=torch.float32, device=dev)
-    check(L.vqgnn_spmm_tile_plan_fill(ptr(rowptr), ptr(col), ptr(val), n_rows, n_cols, nnz,
-                                      ptr(grid), n_dense, ptr(blocks), ptr(rowptr_b), ptr(boff),
-                                      ptr(segcnt), ptr(drec), rec_cap, ptr(s_rowptr), ptr(s_col),
-                                      ptr(s_val), ptr(ws), stream_ptr()), "spmm_tile_plan_fill")
-    sparse = spmm_task_plan(s_rowptr, s_col, s_val, n_rows, s_nnz) if s_nnz > 0 else None
-    del segcnt, grid
-    return TilePlan(blocks=blocks, rowptr_b=rowptr_b, boff=boff, drec=drec, n_dense=n_dense,
-                    dense_edges=dense_edges, W=W, T=T, R=R, C=C, nnz=nnz, n_rows=n_rows,
-                    n_cols=n_cols, val_ptr=val.data_ptr() if val is not None else 0,
-                    s_rowptr=s_rowptr, s_col=s_col, s_val=s_val, s_nnz=s_nnz, sparse=sparse,
-                    min_edges=min_edges)
-
-
 def spmm_task_plan(rowptr, col, val, n_rows, nnz, K=None):
     L = lib()
     K = int(K or TASK_K)
@@ -376,25 +312,6 @@ def spmm(rowptr, col, val, n_rows, nnz, X, F, X2=None, B=None, out=None, plan=No
         raise ValueError(f"spmm: X has {X.shape[0]} rows < B={Bv}")
     if plan is None:            # a one-off product: plan it here (one host read)
         plan = spmm_task_plan(rowptr, col, val, rowptr.numel() - 1, nnz)
-    if isinstance(plan, TilePlan):
-        if (val.data_ptr() if val is not None else 0) != plan.val_ptr:
-            raise ValueError("spmm: the tile plan's records hold other values than val")
-        if plan.nnz != int(nnz) or int(n_rows) != plan.n_rows or n_cols > plan.n_cols:
-            raise ValueError(f"spmm: tile plan for nnz={plan.nnz}, rows={plan.n_rows}; called "
-                             f"with nnz={nnz}, n_rows={n_rows}")
-        check(L.vqgnn_spmm_tile(int(n_rows), int(n_cols), Bv, ptr(X), _ld(X), ptr(X2),
-                                _ld(X2) if X2 is not None else 0, F, ptr(out), _ld(out),
-                                ptr(plan.blocks), plan.n_dense, ptr(plan.rowptr_b),
-                                ptr(plan.boff), ptr(plan.drec), stream_ptr()), "spmm_tile")
-        sp = plan.sparse
-        if sp is not None:
-            ws = workspace(L.vqgnn_spmm_task_workspace(sp.nnz, sp.K, F), dev)
-            check(L.vqgnn_spmm_task_acc(ptr(plan.s_rowptr), int(n_rows), int(n_cols), sp.nnz, Bv,
-                                        ptr(X), _ld(X), ptr(X2), _ld(X2) if X2 is not None else 0,
-                                        F, ptr(out), _ld(out), ptr(sp.plan), ptr(sp.records),
-                                        sp.K, sp.n_jobs, sp.n_empty, ptr(ws), stream_ptr()),
-                  "spmm_task_acc")
-        return out
     if isinstance(plan, TaskPlan):
         if (val.data_ptr() if val is not None else 0) != plan.val_ptr:
             raise ValueError("spmm: the task plan's records hold other values than val")
@@ -407,7 +324,7 @@ def spmm(rowptr, col, val, n_rows, nnz, X, F, X2=None, B=None, out=None, plan=No
                                 _ld(out), ptr(plan.plan), ptr(plan.records), plan.K,
                                 plan.n_jobs, plan.n_empty, ptr(ws), stream_ptr()), "spmm_task")
         return out
-    raise TypeError(f"spmm: plan must be a TaskPlan or TilePlan (CSR.plan), got {type(plan)}")
+    raise TypeError(f"spmm: plan must be a TaskPlan (CSR.plan), got {type(plan)}")
 
 
 def csr_transpose(rowptr, col, val, n_rows, n_cols, nnz, want_perm=False):

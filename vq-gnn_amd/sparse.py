@@ -123,22 +123,13 @@ class CSR:
         (include/vqgnn.h §6) -- per-edge records of this CSR's values, task
         starts and fix-up jobs, valid for any F and any leading row count
         (products with other values on the same structure, e.g. GAT's
-        coefficients: ``plan().with_values(col, values)``).
-        ``kind="tile"`` (or VQGNN_SPMM=tile) asks for the opt-in tiled plan
-        (§6f: dense blocks through LDS tiles plus the sparse remainder's task
-        plan), for the full row range only; F, B and n_rows are accepted for
-        call-site symmetry and do not change the plan."""
-        import os
+        coefficients: ``plan().with_values(col, values)``).  F, B, n_rows and
+        kind are accepted for call-site symmetry and do not change the plan
+        (kind must be None or "task")."""
         from . import kernels
-        mode = kind or os.environ.get("VQGNN_SPMM", "task")
-        if mode == "tile" and (n_rows is None or int(n_rows) == self._sizes[0]):
-            p = self._plans.get("tile", False)
-            if p is False:
-                p = kernels.spmm_tile_plan(self.rowptr, self.col, self.value, self._sizes[0],
-                                           self._sizes[1], self._host_nnz, min_fraction=0.0)
-                self._plans["tile"] = p
-            if p is not None:
-                return p
+        if kind not in (None, "task"):
+            raise ValueError(f"CSR.plan: unknown kind {kind!r} (the tiled path was removed, "
+                             "DESIGN.md §4.2b)")
         p = self._plans.get("task")
         if p is None:
             p = kernels.spmm_task_plan(self.rowptr, self.col, self.value, self._sizes[0],
