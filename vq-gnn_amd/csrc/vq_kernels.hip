@@ -1379,10 +1379,6 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
   char* lds = reinterpret_cast<char*>(smem);
   const float* sef = reinterpret_cast<const float*>(lds + (size_t)48 * cs);
   unsigned long long* acc = reinterpret_cast<unsigned long long*>(lds + (size_t)52 * cs);
-  // the wave's fragment buffer: [16 rows][12 dwords] = x_hi pairs, x_lo
-  // pairs, quad-3 parts of the 16 rows of one group
-  uint32_t* buf = reinterpret_cast<uint32_t*>(
-      lds + (size_t)52 * cs + (FUSED ? (size_t)M * (W + 1) * 8 : 0) + (size_t)wave * kFltScratch);
   // the chunk's codewords in f32 [cs][8] for the resolve's exact candidates
   // (elds: when the LDS has room; else they are read from global memory)
   float* ef = elds ? reinterpret_cast<float*>(lds + (size_t)52 * cs +
@@ -1427,8 +1423,6 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
   // A-fragment byte offset of this lane: plane (q: 0 -> hi, 1 -> lo, 2 -> hi,
   // 3 -> |e|^2 parts), codeword j of tile 0
   const uint32_t a_lane = (uint32_t)(((q == 1) ? 1 : (q == 3 ? 2 : 0)) * cs + j) * 16u;
-  // B-fragment part read by this lane: x_hi (quads 0, 1), x_lo (2), quad-3 parts
-  const int bpart = q < 2 ? 0 : q - 1;
   if (nchunks == 1) __syncthreads();
 
   // the owner lane's raw row (k-slot order: features, then gradients)
@@ -1451,6 +1445,19 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
       }
     }
   };
+  // the k-slot coefficients, wave-uniform: read once into scalar registers in
+  // the row modes (an LDS table re-read per iteration costs 8 LDS reads)
+  float kt[4][8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+#pragma unroll
+    for (int f = 0; f < 4; ++f)
+      kt[f][k] = WM != 0 ? __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(s_kt[f][k]))) : 0.f;
+  }
+  auto kc = [&](int f, int k) {
+    if constexpr (WM != 0) return kt[f][k];
+    else return s_kt[f][k];
+  };
   // normalised as vq.py's bn_apply (+ vq.py:224's grad scale); returns |x|^2
   // summed in k order
   auto row_vals = [&](const float (&raw)[8], float (&xv)[8]) {
@@ -1459,7 +1466,9 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
     for (int k = 0; k < 8; ++k) {
       float v = 0.f;
       if (k < W) {
-        v = __fmul_rn(fmaf(__fsub_rn(raw[k], s_kt[2][k]), s_kt[0][k], s_kt[1][k]), s_kt[3][k]);
+        v = fmaf(__fsub_rn(raw[k], kc(2, k)), kc(0, k), kc(1, k));
+        // grad scale on the gradient slots only (v * 1 is v: features skip it)
+        if (WM == 0 || (WM == 2 && k >= 4)) v = __fmul_rn(v, kc(3, k));
         s = (k == 0) ? __fmul_rn(v, v) : __fadd_rn(s, __fmul_rn(v, v));
       }
       xv[k] = v;
@@ -1497,20 +1506,22 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
       const _Float16 cll = (_Float16)__fsub_rn(r1, (float)cl);
       const uint4 f3 = {0x3c003c00u, __builtin_bit_cast(uint32_t, half2_t{(_Float16)1.f, c0}),
                         __builtin_bit_cast(uint32_t, half2_t{cl, cll}), 0u};
-      // group g's owners (lanes 16g + j) publish their row's parts, every
-      // lane (q, j) reads part q of row (g, j): its B fragment for group g
+      // lane (q, j)'s B fragment for group g is part q of row (g, j) (x_hi for
+      // quads 0 and 1, x_lo for 2, the quad-3 parts for 3): per dword, a
+      // 4 x 4 transpose over (quad, group) of (x_hi, x_hi, x_lo, quad 3) --
+      // permlane swaps, no LDS round trip
+      const uint32_t f3w[4] = {f3.x, f3.y, f3.z, f3.w};
+      uint32_t bw[4][4];
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        if (q == g) {
-          uint4* w = reinterpret_cast<uint4*>(buf + j * 12);
-          w[0] = uint4{hw[0], hw[1], hw[2], hw[3]};
-          w[1] = uint4{lw[0], lw[1], lw[2], lw[3]};
-          w[2] = f3;
-        }
-        __builtin_amdgcn_wave_barrier();
-        bop[g] = __builtin_bit_cast(half8, *reinterpret_cast<const uint4*>(buf + j * 12 + 4 * bpart));
-        __builtin_amdgcn_wave_barrier();
+      for (int d = 0; d < 4; ++d) {
+        uint32_t r[4] = {hw[d], hw[d], lw[d], f3w[d]};
+        transpose_quads(r);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) bw[g][d] = r[g];
       }
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        bop[g] = __builtin_bit_cast(half8, uint4{bw[g][0], bw[g][1], bw[g][2], bw[g][3]});
     }
     float best = INFINITY;
     int bidx = 0;
