@@ -194,7 +194,7 @@ __device__ __forceinline__ float gat_edge_coef(const TaskArgs& a, int e, uint32_
 // PART (near path): the last column tile is partial (F/4 not a multiple of
 // G*NC): its lanes past F load nothing (an offset past the buffer range
 // returns 0 without a memory access) instead of reading the next row
-template <int G, int NC, int U, bool FAR, bool GAT, bool PART, bool PIPE>
+template <int G, int NC, int U, bool FAR, bool GAT, bool PART>
 __device__ __forceinline__ void task_walk(const TaskArgs& a, int wv, int nwaves) {
   constexpr int TPW = 64 / G;
   const int lane = threadIdx.x & 63;
@@ -346,25 +346,7 @@ __device__ __forceinline__ void task_walk(const TaskArgs& a, int wv, int nwaves)
 
   // wave-uniform (every lane holds the max): an SGPR loop, not an exec-masked one
   const int nblk = __builtin_amdgcn_readfirstlane((len + U - 1) / U);
-  if constexpr (PIPE) {
-    // two blocks in flight: block b+1's gathers are issued before block b is
-    // consumed (records two blocks ahead)
-    int cx0[U], cw0[U], cx1[U], cw1[U];
-    float4 v0[U][NC], v1[U][NC];
-    int2 ra = load_rec(e0);
-    int2 rb = load_rec(e0 + U);
-    issue(ra, e0, cx0, cw0, v0);
-    for (int bi = 0; bi < nblk; bi += 2) {
-      const int e = e0 + bi * U;
-      ra = load_rec(e + 2 * U);
-      if (bi + 1 < nblk) issue(rb, e + U, cx1, cw1, v1);
-      consume(e, cx0, cw0, v0);
-      if (bi + 1 >= nblk) break;
-      rb = load_rec(e + 3 * U);
-      if (bi + 2 < nblk) issue(ra, e + 2 * U, cx0, cw0, v0);
-      consume(e + U, cx1, cw1, v1);
-    }
-  } else {
+  {
     int2 rraw = load_rec(e0);
     for (int bi = 0; bi < nblk; ++bi) {
       const int e = e0 + bi * U;
@@ -392,7 +374,7 @@ __device__ __forceinline__ void task_walk(const TaskArgs& a, int wv, int nwaves)
   }
 }
 
-template <int G, int NC, int U, bool FAR, bool GAT = false, bool PART = false, bool PIPE = false>
+template <int G, int NC, int U, bool FAR, bool GAT = false, bool PART = false>
 __global__ void __launch_bounds__(kTaskThreads)
 spmm_task_kernel(TaskArgs a) {
   const int nwaves = (int)gridDim.x * (kTaskThreads / 64);
@@ -400,7 +382,7 @@ spmm_task_kernel(TaskArgs a) {
   // scalar (a VGPR-derived resource costs a readfirstlane loop per block)
   const int wv = __builtin_amdgcn_readfirstlane(
       xcd_remap(blockIdx.x, gridDim.x) * (kTaskThreads / 64) + (threadIdx.x >> 6));
-  task_walk<G, NC, U, FAR, GAT, PART, PIPE>(a, wv, nwaves);
+  task_walk<G, NC, U, FAR, GAT, PART>(a, wv, nwaves);
 }
 
 // One wave per fix-up job.  A cut row: out[row] = tail[ts] + ... + tail[t-1]
@@ -484,11 +466,11 @@ static int task_env(const char* name, int dflt) {
   return v ? atoi(v) : dflt;
 }
 
-template <int G, int NC, int U, bool FAR, bool GAT, bool PART = false, bool PIPE = false>
+template <int G, int NC, int U, bool FAR, bool GAT, bool PART = false>
 static void launch_task(const TaskArgs& a, int tiles, hipStream_t s) {
   const int waves = (a.ntasks + 64 / G - 1) / (64 / G);
   const int blocks = (waves + 3) / 4;
-  hipLaunchKernelGGL((spmm_task_kernel<G, NC, U, FAR, GAT, PART, PIPE>), dim3(blocks, tiles),
+  hipLaunchKernelGGL((spmm_task_kernel<G, NC, U, FAR, GAT, PART>), dim3(blocks, tiles),
                      dim3(kTaskThreads), 0, s, a);
 }
 
@@ -498,10 +480,6 @@ static void launch_task_u(const TaskArgs& a, int tiles, int U, bool near, hipStr
   if (U > G) U = G;
   if (near) {
     if constexpr (G >= 16) {
-      if constexpr (!GAT && NC == 1) {     // experiment: two 8-edge blocks in flight
-        if (task_env("VQGNN_TASK_PIPE", 0) && (a.F >> 2) % (G * NC) == 0)
-          return launch_task<G, NC, 8, false, GAT, false, true>(a, tiles, s);
-      }
       if (U == 16) {
         if constexpr (!GAT && NC == 1) {   // the default shape: a partial last tile
           if ((a.F >> 2) % (G * NC) != 0) return launch_task<G, NC, 16, false, GAT, true>(a, tiles, s);

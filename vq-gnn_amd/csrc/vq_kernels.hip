@@ -671,7 +671,6 @@ static size_t flt_lds_bytes(int chunk) {
 
 // Per-wave fragment buffer of vq_filter_kernel (after the codebook planes
 // and the fused slab): [16 rows][12 dwords], one row group at a time
-constexpr int kFltScratch = 16 * 48;
 
 // filtered assignment for W <= 8 (section 3b)
 template <bool FUSED, int WM, int WV>
@@ -774,14 +773,12 @@ static AssignGeom assign_geom(int B, int nb, int M, int W) {
   g.mpad = (M + 15) / 16 * 16;
   const size_t acc = (size_t)M * (W + 1) * sizeof(unsigned long long);
   if (g.filter) {
-    // staged in tile pairs: chunks of 32 codewords; room for 16 waves' row
-    // scratch
+    // staged in tile pairs: chunks of 32 codewords
     g.mpad = (M + 31) / 32 * 32;
-    const size_t scr = (size_t)16 * kFltScratch;
-    g.fused = flt_lds_bytes(g.mpad) + acc + scr <= kLdsBudget;
+    g.fused = flt_lds_bytes(g.mpad) + acc <= kLdsBudget;
     int c = g.mpad;
     if (!g.fused)
-      while (c > 32 && flt_lds_bytes(c) + scr > kLdsBudget) c = (c / 2 + 31) / 32 * 32;
+      while (c > 32 && flt_lds_bytes(c) > kLdsBudget) c = (c / 2 + 31) / 32 * 32;
     g.chunk = c;
   } else if (cb_lds_bytes(g.kc, g.mpad) + acc <= kLdsBudget) {
     // fused EMA when codebook + accumulators share the LDS
@@ -799,7 +796,7 @@ static AssignGeom assign_geom(int B, int nb, int M, int W) {
   }
   size_t lds = g.filter ? flt_lds_bytes(g.chunk) : cb_lds_bytes(g.kc, g.chunk);
   if (g.fused) lds += acc;
-  const size_t scr8 = g.filter ? (size_t)8 * kFltScratch : 0;
+  const size_t scr8 = 0;   // (the filter hands fragments over by permlane swaps: no scratch)
   const int wm = g.filter ? (W == 8 ? 2 : (W == 4 ? 1 : 0)) : (W == 4 * g.kc ? 2 : 0);
   // waves per workgroup: the choice with more resident waves per CU (ties: 8)
   const int cap8 = assign_capacity(g.kc, g.fused, wm, lds + scr8, 8, g.filter);
@@ -809,7 +806,11 @@ static AssignGeom assign_geom(int B, int nb, int M, int W) {
   if (wenv == 8 || wenv == 16) g.wv = wenv;
   g.lds = lds + (g.wv == 16 ? 2 * scr8 : scr8);
   // the filter's f32 codebook copy, when it fits without costing resident
-  // workgroups (VQGNN_FLT_ELDS=0/1 forces it off/on where it fits)
+  // workgroups and the sweep leaves the LDS room: at chunks above 512
+  // codewords the sweep's fragment reads dominate the LDS and the resolve
+  // reads its candidates faster through L1 (arxiv_gat M = 1024: 274 us with
+  // the copy, 253 us without; arxiv M = 256: 98 us with, 121 without).
+  // VQGNN_FLT_ELDS=0/1 forces it off/on where it fits.
   g.elds = 0;
   if (g.filter) {
     const size_t ef = (size_t)(g.chunk + kFltSlack) * 32;
@@ -817,7 +818,8 @@ static AssignGeom assign_geom(int B, int nb, int M, int W) {
     const int cap = g.wv == 16 ? cap16 : cap8;
     const int env = env_int_vq("VQGNN_FLT_ELDS", -1);
     if (g.lds + ef <= kLdsBudget && env != 0 &&
-        (env == 1 || assign_capacity(g.kc, g.fused, wmv, g.lds + ef, g.wv, true) >= cap)) {
+        (env == 1 || (g.chunk <= 512 &&
+                      assign_capacity(g.kc, g.fused, wmv, g.lds + ef, g.wv, true) >= cap))) {
       g.elds = 1;
       g.lds += ef;
     }
@@ -1318,9 +1320,9 @@ __device__ __forceinline__ void stage_filter(const float* __restrict__ E, int ld
     p1[m] = lo;
     p2[m] = sp;
     sef[m] = mv ? s : INFINITY;
-    if (ef) {
-      reinterpret_cast<float4*>(ef)[2 * m] = make_float4(e[0], e[1], e[2], e[3]);
-      reinterpret_cast<float4*>(ef)[2 * m + 1] = make_float4(e[4], e[5], e[6], e[7]);
+    if (ef) {                     // k-planes [8][cs]: a run of 4 codewords is one float4
+#pragma unroll
+      for (int k = 0; k < 8; ++k) ef[k * cs + m] = e[k];
     }
   }
 }
@@ -1382,8 +1384,7 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
   // the chunk's codewords in f32 [cs][8] for the resolve's exact candidates
   // (elds: when the LDS has room; else they are read from global memory)
   float* ef = elds ? reinterpret_cast<float*>(lds + (size_t)52 * cs +
-                                              (FUSED ? (size_t)M * (W + 1) * 8 : 0) +
-                                              (size_t)WV * kFltScratch)
+                                              (FUSED ? (size_t)M * (W + 1) * 8 : 0))
                    : nullptr;
   const float* E = emb + (int64_t)b * emb_bstride;
   const int nchunks = (M + chunk - 1) / chunk;
@@ -1610,18 +1611,43 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
       const int pw = (int)(key >> 2), qw = (int)(key & 3);
       float dm = INFINITY;
       int im = 0;
+      if (ef) {
+        // staged f32 k-planes: each run of 4 candidates is one float4 per
+        // plane, the four dot chains advance together (k order per chain)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const int m0 = pw * 32 + t * 16 + 4 * qw;
+          float d4[4];
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            if (k < W) {
+              const float4 ek = *reinterpret_cast<const float4*>(ef + k * cs + m0);
+              const float ev[4] = {ek.x, ek.y, ek.z, ek.w};
+#pragma unroll
+              for (int c = 0; c < 4; ++c)
+                d4[c] = (k == 0) ? __fmul_rn(ev[c], xr[k]) : fmaf(ev[c], xr[k], d4[c]);
+            }
+          }
+          const float4 s4 = *reinterpret_cast<const float4*>(sef + m0);
+          const float sv[4] = {s4.x, s4.y, s4.z, s4.w};
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const int ci = m0 + c;
+            const float dd = ci < mcount ? fmaf(-2.f, d4[c], __fadd_rn(sx, sv[c])) : INFINITY;
+            if (dd < dm) {
+              dm = dd;
+              im = ci;
+            }
+          }
+        }
+      } else {
 #pragma unroll 2
       for (int c = 0; c < 8; ++c) {
         const int ci = pw * 32 + (c >> 2) * 16 + 4 * qw + (c & 3);
         const bool cv = ci < mcount;
         const float* er = E + (int64_t)(mc0 + (cv ? ci : 0)) * ldw;
         float e[8];
-        if (ef) {                                     // staged f32 copy (k >= W staged as 0)
-          const float4 t0 = reinterpret_cast<const float4*>(ef)[2 * ci];
-          const float4 t1 = reinterpret_cast<const float4*>(ef)[2 * ci + 1];
-          e[0] = t0.x; e[1] = t0.y; e[2] = t0.z; e[3] = t0.w;
-          e[4] = t1.x; e[5] = t1.y; e[6] = t1.z; e[7] = t1.w;
-        } else if (vec_rows && W > 4) {
+        if (vec_rows && W > 4) {
           const float4 t0 = *reinterpret_cast<const float4*>(er);
           const float4 t1 = *reinterpret_cast<const float4*>(er + 4);
           e[0] = t0.x; e[1] = t0.y; e[2] = t0.z; e[3] = t0.w;
@@ -1644,6 +1670,7 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
           dm = dd;
           im = ci;
         }
+      }
       }
       if (dm < best) {                                // earlier chunk wins ties
         best = dm;
