@@ -271,34 +271,50 @@ __device__ __forceinline__ void task_walk(const TaskArgs& a, int wv, int nwaves)
 #pragma unroll
   for (int o = G; o < 64; o <<= 1) len = max(len, __shfl_xor(len, o));
 
-  // one block: broadcast its records to the group (cx, cw) and issue its
-  // gathers (v); consume: the fma chain and the row ends, in edge order
-  auto issue = [&](int2 rraw, int e, int (&cx)[U], int (&cw)[U], float4 (&v)[U][NC]) {
+  // one block: broadcast its records to the group and issue its gathers (v);
+  // consume: the fma chain and the row ends, in edge order.
+  // Near path: the record lane computes its edge's source-row byte offset
+  // (column -> X or X2 row, one 24-bit multiply-add) once for the block and
+  // the group receives offsets (co) beside the record words (cx: row ends,
+  // skip counts) and weights (cw).  Far path: 64-bit addresses per step.
+  struct Blk {
+    int cx[U];      // record words: column, skip count, row end
+    int cw[U];      // weights (GAT: coefficients)
+    int co[U];      // near: source-row byte offsets
+  };
+  auto issue = [&](int2 rraw, int e, Blk& bk, float4 (&v)[U][NC]) {
     const int2 rcur = mask_rec(rraw, e);
-    group_bcast<kAnd>(rcur.x, cx, std::make_integer_sequence<int, U>{});
-    group_bcast<kAnd>(rcur.y, cw, std::make_integer_sequence<int, U>{});
+    group_bcast<kAnd>(rcur.x, bk.cx, std::make_integer_sequence<int, U>{});
+    if constexpr (!FAR) {
+      const uint32_t x = (uint32_t)rcur.x;
+      const bool s1 = (int)(x & kColMask) < a.B;
+      const uint32_t roff = __umul24(x, s1 ? a.ldxb : a.ldx2b) +
+                            (s1 ? a.offx : a.offx2 - (uint32_t)a.B * a.ldx2b);
+      group_bcast<kAnd>((int)roff, bk.co, std::make_integer_sequence<int, U>{});
+    }
+    group_bcast<kAnd>(rcur.y, bk.cw, std::make_integer_sequence<int, U>{});
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      uint32_t off = 0;
-      const char* p = nullptr;
-      row_src<FAR>(a, (uint32_t)cx[u], b1, b2, lane_off, &off, &p);
 #pragma unroll
       for (int i = 0; i < NC; ++i) {
         if constexpr (FAR) {
+          const char* p = nullptr;
+          uint32_t off = 0;
+          row_src<FAR>(a, (uint32_t)bk.cx[u], b1, b2, lane_off, &off, &p);
           v[u][i] = pv[i] ? *reinterpret_cast<const float4*>(p + 16 * G * i)
                           : make_float4(0.f, 0.f, 0.f, 0.f);
         } else {   // pieces past F read the next row (or 0 past the range): never stored
-          const uint32_t o = PART ? ((off + 16u * G * i) | kill[i]) : off + 16u * G * i;
+          const uint32_t off = (uint32_t)bk.co[u] + lane_off + 16u * G * i;
+          const uint32_t o = PART ? (off | kill[i]) : off;
           v[u][i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsx, o, 0, 0));
         }
       }
     }
   };
-  auto consume = [&](int e, const int (&cx)[U], const int (&cw)[U], const float4 (&v)[U][NC]) {
+  auto consume = [&](int e, const Blk& bk, const float4 (&v)[U][NC]) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const float w = __int_as_float(cw[u]);
-      const uint32_t x = (uint32_t)cx[u];
+      const float w = __int_as_float(bk.cw[u]);
 #pragma unroll
       for (int i = 0; i < NC; ++i) {
         acc[i].x = fmaf(w, v[u][i].x, acc[i].x);
@@ -307,6 +323,7 @@ __device__ __forceinline__ void task_walk(const TaskArgs& a, int wv, int nwaves)
         acc[i].w = fmaf(w, v[u][i].w, acc[i].w);
       }
       if constexpr (GAT) den = __fadd_rn(den, w);
+      const uint32_t x = (uint32_t)bk.cx[u];
       if (x & kEndBit) {                   // the row ends at this edge
         float* dst = head ? a.carry + (int64_t)t * 2 * a.cf
                    : FAR  ? a.out + (int64_t)r * a.ldo
@@ -352,10 +369,10 @@ __device__ __forceinline__ void task_walk(const TaskArgs& a, int wv, int nwaves)
       const int e = e0 + bi * U;
       // next block's records (past the buffer: zeros; outside the task: masked)
       const int2 rnxt = load_rec(e + U);
-      int cx[U], cw[U];
+      Blk bk;
       float4 v[U][NC];
-      issue(rraw, e, cx, cw, v);
-      consume(e, cx, cw, v);
+      issue(rraw, e, bk, v);
+      consume(e, bk, v);
       rraw = rnxt;
     }
   }
