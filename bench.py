@@ -115,7 +115,9 @@ def main():
             dist.init_process_group("gloo")
         from vq_gnn_amd.dist import CodebookSync
         cgroup = dist.new_group(backend="gloo")
-        comm = CodebookSync(count_group=cgroup)
+        # --graph: the process-group path (a side stream's collective left in
+        # flight across a captured step cannot be captured)
+        comm = CodebookSync(count_group=cgroup, direct=False if args.graph else None)
 
     cfg = CONFIGS[args.config]
     if cfg.get("device_build"):      # reddit-sized: graph and batch built on the device
@@ -184,6 +186,8 @@ def main():
             e[1].record()
         aggregate(record, e)
         bank.finish_update()  # EMA finalize (multi-GPU: after the overlapped all-reduce)
+        if args.graph:
+            bank.sync_codes()     # a captured step joins its code exchange
         # multi-GPU: the other ranks' codes land in the next update, after its
         # assign (VQBank.update): the exchange overlaps gather + SpMM + BN + assign
         if record:

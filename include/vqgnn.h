@@ -62,6 +62,14 @@ size_t vqgnn_bn_stats_workspace(int32_t B, int32_t F);
 int vqgnn_bn_stats(const float* X, int64_t ldx, const float* G, int64_t ldg,
                    int32_t B, int32_t F, int32_t with_grad,
                    double* sums, void* workspace, vqgnn_stream_t stream);
+/* Multi-GPU form: sums is a flat [4F + 2] buffer; after the four sums it
+ * holds sums[4F] = B (the row count every rank's all-reduce adds up, read by
+ * vqgnn_bn_finalize with count = 0) and sums[4F + 1] = 0 (the over-capacity
+ * flag a caller may set before the all-reduce) -- written on the device, so
+ * the caller issues no fill of its own.  Without grads the g sums are 0. */
+int vqgnn_bn_stats_count(const float* X, int64_t ldx, const float* G, int64_t ldg,
+                         int32_t B, int32_t F, int32_t with_grad,
+                         double* sums, void* workspace, vqgnn_stream_t stream);
 
 /* 2. BatchNorm finalize: batch statistics -> per-column normalisation
  *    coefficients and the running-stat EMA update.

@@ -4,6 +4,7 @@ import os
 import socket
 
 import numpy as np
+import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
@@ -123,3 +124,40 @@ def test_codebook_sync_gloo_world2(tmp_path):
         np.testing.assert_array_equal(r[k]["all_idx16"], idx)
     # every rank sees the same gathered codes (replicas stay identical)
     np.testing.assert_array_equal(r[0]["all_loc"], r[1]["all_loc"])
+
+
+def test_rccl_binding_unique_id_and_dtypes():
+    """vq-gnn_amd/rccl.py binds torch's own librccl: a unique id is the full
+    128 bytes (no NUL truncation), and only the exchange's dtypes map."""
+    from vq_gnn_amd import rccl
+    try:
+        u = rccl.unique_id()
+    except OSError as e:          # no RCCL in this torch build
+        pytest.skip(f"librccl not loadable: {e}")
+    assert isinstance(u, bytes) and len(u) == rccl.NCCL_UNIQUE_ID_BYTES
+    assert rccl.unique_id() != u
+    for dt in (torch.uint8, torch.int32, torch.int64, torch.float32, torch.float64):
+        assert rccl.Communicator._dtype(torch.empty(1, dtype=dt)) >= 0
+    with pytest.raises(TypeError):
+        rccl.Communicator._dtype(torch.empty(1, dtype=torch.int16))
+    with pytest.raises(ValueError):
+        rccl.Communicator(1, 0, b"short")
+
+
+def _gloo_direct_flag(rank, world, port, out_dir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import vqgnn_pkg
+    vqgnn_pkg.load()
+    from vq_gnn_amd.dist import CodebookSync
+    with open(os.path.join(out_dir, f"direct{rank}.txt"), "w") as f:
+        f.write(str(int(CodebookSync()._direct)))
+    dist.destroy_process_group()
+
+
+def test_codebook_sync_direct_rccl_only_on_nccl(tmp_path):
+    """The direct RCCL path is chosen only on the nccl backend: gloo groups
+    (the CPU tests, the one-GPU rehearsals) keep torch.distributed."""
+    mp.spawn(_gloo_direct_flag, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    assert [open(tmp_path / f"direct{r}.txt").read() for r in range(2)] == ["0", "0"]

@@ -31,6 +31,8 @@ SIGNATURES = {
     "vqgnn_bn_stats_workspace": (_size, [_i32, _i32]),
     "vqgnn_bn_stats": (ctypes.c_int, [_c_void_p, _i64, _c_void_p, _i64, _i32, _i32, _i32,
                                       _c_void_p, _c_void_p, _c_void_p]),
+    "vqgnn_bn_stats_count": (ctypes.c_int, [_c_void_p, _i64, _c_void_p, _i64, _i32, _i32, _i32,
+                                      _c_void_p, _c_void_p, _c_void_p]),
     "vqgnn_bn_finalize": (ctypes.c_int, [_c_void_p, _i64, _i32, _i32, _i32, _i32, _i32, _f64,
                                          _f64, _f64, _f64, _f64, _c_void_p, _c_void_p,
                                          _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,

@@ -161,11 +161,18 @@ bn_stats_partial_scalar_kernel(const float* __restrict__ X, int64_t ldx,
 // of squares of one data column); lanes stride the chunks, then a fixed
 // butterfly across the wave (deterministic).
 constexpr int kReduceWaves = 4;
+// Without gradients (C == F) the g half of sums is written as zeros; tail
+// (optional): tail[0] = count, tail[1] = 0 (the multi-GPU row count and
+// over-capacity flag that travel with the sums, vqgnn_bn_stats_count).
 __global__ void __launch_bounds__(kReduceWaves * 64)
 bn_stats_reduce_kernel(const double* __restrict__ part, int chunks, int F, int C,
-                       double* __restrict__ sums) {
+                       double* __restrict__ sums, double* __restrict__ tail, double count) {
   const int lane = threadIdx.x & 63;
   const int v = blockIdx.x * kReduceWaves + (threadIdx.x >> 6);   // value column in [0, 2C)
+  if (C == F && blockIdx.x == 0) {
+    for (int i = threadIdx.x; i < 2 * F; i += blockDim.x) sums[2 * F + i] = 0.0;
+  }
+  if (tail && blockIdx.x == 0 && threadIdx.x < 2) tail[threadIdx.x] = threadIdx.x == 0 ? count : 0.0;
   if (v >= 2 * C) return;
   double a = 0.0;
   for (int p = lane; p < chunks; p += 64) a += part[(int64_t)p * 2 * C + v];
@@ -2145,10 +2152,9 @@ extern "C" size_t vqgnn_bn_stats_workspace(int32_t B, int32_t F) {
   return std::max(fp64_ws_bytes(B, F), aten_ws_bytes(B, F));
 }
 
-extern "C" int vqgnn_bn_stats(const float* X, int64_t ldx, const float* G, int64_t ldg,
-                              int32_t B, int32_t F, int32_t with_grad, double* sums,
-                              void* workspace, vqgnn_stream_t stream) {
-  clear_error();
+static int bn_stats_launch(const float* X, int64_t ldx, const float* G, int64_t ldg, int32_t B,
+                           int32_t F, int32_t with_grad, double* sums, double* tail,
+                           void* workspace, vqgnn_stream_t stream) {
   VQGNN_REQUIRE(X && sums && workspace, "bn_stats: null pointer");
   VQGNN_REQUIRE(B > 0 && F > 0 && ldx >= F, "bn_stats: bad shape B=%d F=%d ldx=%lld", B, F,
                 (long long)ldx);
@@ -2170,8 +2176,24 @@ extern "C" int vqgnn_bn_stats(const float* X, int64_t ldx, const float* G, int64
   }
   hipLaunchKernelGGL(bn_stats_reduce_kernel, dim3((2 * C + kReduceWaves - 1) / kReduceWaves),
                      dim3(kReduceWaves * 64), 0, s, part,
-                     chunks, F, C, sums);
+                     chunks, F, C, sums, tail, (double)B);
   return check_launch("bn_stats");
+}
+
+extern "C" int vqgnn_bn_stats(const float* X, int64_t ldx, const float* G, int64_t ldg,
+                              int32_t B, int32_t F, int32_t with_grad, double* sums,
+                              void* workspace, vqgnn_stream_t stream) {
+  clear_error();
+  return bn_stats_launch(X, ldx, G, ldg, B, F, with_grad, sums, nullptr, workspace, stream);
+}
+
+extern "C" int vqgnn_bn_stats_count(const float* X, int64_t ldx, const float* G, int64_t ldg,
+                                    int32_t B, int32_t F, int32_t with_grad, double* sums,
+                                    void* workspace, vqgnn_stream_t stream) {
+  clear_error();
+  VQGNN_REQUIRE(sums, "bn_stats_count: null pointer");
+  return bn_stats_launch(X, ldx, G, ldg, B, F, with_grad, sums, sums + 4 * (int64_t)F,
+                         workspace, stream);
 }
 
 static BnArgs bn_args(int mode, int arith_x, int arith_g, double mom_f, double eps_f,

@@ -16,6 +16,8 @@ tests.  Codes travel as bytes: RCCL has no 16-bit integer type.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.distributed as dist
 
@@ -40,21 +42,76 @@ class CodebookSync:
     the normalised values to the coarser grid (include/vqgnn.h §3), within
     the EMA tolerance the tests use."""
 
-    def __init__(self, group=None, count_group=None, capacity=None):
+    def __init__(self, group=None, count_group=None, capacity=None, direct=None):
         self.group = group
         # host-integer collectives (max B when no capacity is given) run over a
         # CPU (gloo) group when given, so the device stream never syncs for them
         self.count_group = count_group
         self.world = dist.get_world_size(group)
         self.capacity = None if capacity is None else int(capacity)
-        self._overflow = None  # device sum of the over-capacity flags (allreduce_stats_)
+        self._overflow = None  # reduced over-capacity flags not yet read (allreduce_stats_)
         self._wire = {}       # persistent code-exchange buffers per shape
         self._inflight = {}   # buffer key -> the PendingWire still reading them
         self._epoch = {}      # buffer key -> exchanges issued on its winner table
+        # RCCL called directly on chosen streams (rccl.py): the default on the
+        # nccl backend (VQGNN_DIRECT_RCCL=0: through torch.distributed)
+        if direct is None:
+            direct = (dist.get_backend(group) == "nccl"
+                      and os.environ.get("VQGNN_DIRECT_RCCL", "1") != "0")
+        self._direct = bool(direct)
+        if self._direct:
+            self._init_direct()
+
+    def _init_direct(self):
+        """Two communicators over the world: A on the compute stream (the
+        BatchNorm all-reduce, in order), B on one side stream (the EMA
+        all-reduce and the code all-gather, overlapping the caller's work).
+        Rank 0's unique ids travel over the gloo count group."""
+        from . import rccl
+        ids = [rccl.unique_id(), rccl.unique_id()] if dist.get_rank(self.group) == 0 else None
+        box = [ids]
+        dist.broadcast_object_list(box, src=0, group=self.count_group or self.group)
+        rank = dist.get_rank(self.group)
+        self._ca = rccl.Communicator(self.world, rank, box[0][0])
+        self._cb = rccl.Communicator(self.world, rank, box[0][1])
+        self._side = torch.cuda.Stream()
+        # reused events (creating one per collective costs host time): an
+        # event is re-recorded only after its StreamWork was waited on (at
+        # most 2 exchanges + 2 all-reduces are in flight at once)
+        self._events = [torch.cuda.Event() for _ in range(16)]
+        self._ev_i = 0
+        import atexit
+        atexit.register(self._destroy_direct)
+
+    def _destroy_direct(self):
+        if getattr(self, "_ca", None) is not None:
+            torch.cuda.synchronize()
+            self._ca.destroy()
+            self._cb.destroy()
+            self._ca = self._cb = None
+
+    def _on_side(self, launch):
+        """Run ``launch(side_stream)`` after the current stream's work so far;
+        -> the StreamWork the current stream waits on later."""
+        from . import rccl
+        ev0, ev1 = self._events[self._ev_i], self._events[self._ev_i + 1]
+        self._ev_i = (self._ev_i + 2) % len(self._events)
+        ev0.record(torch.cuda.current_stream())
+        self._side.wait_event(ev0)
+        launch(self._side)
+        ev1.record(self._side)
+        return rccl.StreamWork(ev1)
 
     def allreduce_(self, t: torch.Tensor, async_op: bool = False):
         """In-place sum over the ranks; async_op=True returns the work (its
-        wait() orders the current stream after the collective)."""
+        wait() orders the current stream after the collective).  Direct RCCL:
+        synchronous calls run in order on the compute stream, asynchronous
+        ones on the side stream (tensors must stay alive until wait())."""
+        if self._direct:
+            if not async_op:
+                self._ca.all_reduce_(t, torch.cuda.current_stream())
+                return None
+            return self._on_side(lambda s: self._cb.all_reduce_(t, s))
         return dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=async_op)
 
     def rows_per_rank(self, B: int) -> int:
@@ -79,20 +136,24 @@ class CodebookSync:
             sums[-1:].fill_(1.0)
         self.allreduce_(sums)
         if self.capacity is not None:
+            # the reduced flag stays in the sums; read at the next check (no
+            # device op here: a torch launch right after the collective costs
+            # ~140 us of host time)
             if self._overflow is None:
-                self._overflow = torch.zeros(1, dtype=sums.dtype, device=sums.device)
-            self._overflow.add_(sums[-1:])
+                self._overflow = []
+            self._overflow.append(sums[-1:])
+            if len(self._overflow) >= 64:     # bounded: fold once per 64 updates
+                self._overflow = [torch.cat(self._overflow).sum(0, keepdim=True)]
             return self.capacity
         return self.global_max(B)
 
     def take_overflow(self) -> bool:
         """True (on every rank alike) when some rank's batch exceeded capacity
         in an update since the last call; one device read."""
-        if self._overflow is None:
+        if not self._overflow:
             return False
-        over = float(self._overflow.item()) > 0
-        self._overflow.zero_()
-        return over
+        flags, self._overflow = self._overflow, []
+        return float(torch.cat(flags).sum().item()) > 0
 
     def global_count(self, B: int) -> int:
         """Sum of B over the ranks (a blocking host collective; not on the
@@ -164,7 +225,10 @@ class CodebookSync:
             epoch = 1
         self._epoch[key] = epoch
         kernels.pack_codes(batch_idx, local, M, max_B, send, codes=codes)
-        work = dist.all_gather_into_tensor(recv, send, group=self.group, async_op=True)
+        if self._direct:
+            work = self._on_side(lambda s: self._cb.all_gather(send, recv, s))
+        else:
+            work = dist.all_gather_into_tensor(recv, send, group=self.group, async_op=True)
         pend = PendingWire(work, recv, self.world * max_B, nb, M, winner, codes, epoch)
         self._inflight[key] = pend
         return pend

@@ -47,13 +47,11 @@ def bn_stats(X: torch.Tensor, G: torch.Tensor | None, F: int,
     ws = workspace(L.vqgnn_bn_stats_workspace(B, F), X.device)
     flat = torch.empty(4 * F + 2 * int(with_count), dtype=torch.float64, device=X.device)
     sums = flat[:4 * F].view(4, F)
-    if G is None:
-        sums[2:].zero_()
-    if with_count:
-        flat[4 * F:].fill_(0.0)
-        flat[4 * F:4 * F + 1].fill_(float(B))
-    check(L.vqgnn_bn_stats(ptr(X), _ld(X), ptr(G), _ld(G) if G is not None else 0, B, F,
-                           int(G is not None), ptr(sums), ptr(ws), stream_ptr()), "bn_stats")
+    # the kernels write every element (zeros for the g half without G; with
+    # the count: flat[4F] = B, flat[4F + 1] = 0)
+    fn = L.vqgnn_bn_stats_count if with_count else L.vqgnn_bn_stats
+    check(fn(ptr(X), _ld(X), ptr(G), _ld(G) if G is not None else 0, B, F,
+             int(G is not None), ptr(flat), ptr(ws), stream_ptr()), "bn_stats")
     return flat if with_count else sums
 
 

@@ -152,6 +152,18 @@ class VQBank(nn.Module):
         self._pending_codes = self.comm.start_codes_exchange(batch_idx, local, codes,
                                                              max_B, self.M)
 
+    _local_cache = None
+
+    def _local_codes(self, B, nbr, device):
+        """This rank's codes of an exchanging update (multi-GPU): a buffer
+        reused across updates of one shape (the pack kernel reads it on the
+        stream before the next update overwrites it)."""
+        key = (B, nbr, str(device))
+        c = self._local_cache
+        if c is None or c[0] != key:
+            c = self._local_cache = (key, torch.empty(B, nbr, dtype=torch.int16, device=device))
+        return c[1]
+
     def _slab(self, W, b0, nbr):
         """Zeroed statistic slab [1, nbr, M, W+1] for branches [b0, b0+nbr)."""
         buf = self.stats_f if W == self.D else self.stats_u
@@ -226,7 +238,7 @@ class VQBank(nn.Module):
         slab = self._slab(D, b0, nbr) if training else None
         local = None
         if comm is not None and codes is not None:
-            local = torch.empty(B, nbr, dtype=torch.int16, device=X.device)
+            local = self._local_codes(B, nbr, X.device)
             stats = self._assign(X, None, coef, 1.0, self.emb[sl], D, D, idx_out=idx_out,
                                  codes=local, batch_idx=self._arange(B, X.device),
                                  want_stats=training, stat_count=count, stats_out=slab)
@@ -318,7 +330,7 @@ class VQBank(nn.Module):
         slab = self._slab(2 * D, b0, nbr) if training else None
         local = None
         if comm is not None and codes is not None:
-            local = torch.empty(B, nbr, dtype=torch.int16, device=X.device)
+            local = self._local_codes(B, nbr, X.device)
             stats = self._assign(X, G, coef, scale, self.emb[sl], D, 2 * D,
                                  idx_out=idx_out, codes=local,
                                  batch_idx=self._arange(B, X.device), want_stats=training,
@@ -333,9 +345,12 @@ class VQBank(nn.Module):
             if local is not None:
                 self.sync_codes()           # the previous exchange lands before ours
             if defer:
-                if local is not None:      # codes first: the all-reduce is waited on later
-                    self._exchange_codes(batch_idx, local, codes, max_B)
+                # the EMA all-reduce first: the finalize at the end of the
+                # step waits for it, the codes only land in the next update
+                # (both share one communicator's queue, so order matters)
                 work = comm.allreduce_(stats, async_op=True)
+                if local is not None:
+                    self._exchange_codes(batch_idx, local, codes, max_B)
             else:
                 comm.allreduce_(stats)
                 if local is not None:
