@@ -282,8 +282,7 @@ __device__ __forceinline__ void task_walk(const TaskArgs& a, int wv, int nwaves)
     int cw[U];      // weights (GAT: coefficients)
     int co[U];      // near: source-row byte offsets
   };
-  auto issue = [&](int2 rraw, int e, Blk& bk, float4 (&v)[U][NC]) {
-    const int2 rcur = mask_rec(rraw, e);
+  auto issue = [&](int2 rcur, int e, Blk& bk, float4 (&v)[U][NC]) {
     group_bcast<kAnd>(rcur.x, bk.cx, std::make_integer_sequence<int, U>{});
     if constexpr (!FAR) {
       const uint32_t x = (uint32_t)rcur.x;
@@ -363,7 +362,72 @@ __device__ __forceinline__ void task_walk(const TaskArgs& a, int wv, int nwaves)
 
   // wave-uniform (every lane holds the max): an SGPR loop, not an exec-masked one
   const int nblk = __builtin_amdgcn_readfirstlane((len + U - 1) / U);
-  {
+  if constexpr (GAT && G >= 16) {
+    // GAT, pipelined: records are loaded two blocks ahead and the coefficient
+    // inputs al[j], ar[i] one block ahead, both issued before the current
+    // block's gathers, so the gathers' wait covers them and no dependent load
+    // sits at a block start.  The row i of each edge comes from the group's
+    // row at the block start plus a prefix sum of the row-end increments
+    // (1 + empty rows skipped) of the earlier edges (DPP within the 16-lane
+    // record row), not from an erow load; a block holding a skip escape (31
+    // or more empty rows in a row) reads erow for it and for the next block.
+    const float s = a.params[2];
+    int rb = r;            // group's row at the next prepared block's first edge
+    bool known = true;     // rb is exact
+    auto prep = [&](int2 q, int eb, float& alv, float& arv) {
+      const int eu = eb + k;
+      const bool in = k < U && eu >= e0 && eu < e1;
+      const uint32_t x = in ? (uint32_t)q.x : 0u;
+      const uint32_t skip = (x >> kSkipShift) & kSkipEsc;
+      const int inc = (x & kEndBit) ? 1 + (int)skip : 0;
+      int incl = inc;
+      incl += __builtin_amdgcn_update_dpp(0, incl, 0x111, 0xF, 0xF, true);   // row_shr:1
+      incl += __builtin_amdgcn_update_dpp(0, incl, 0x112, 0xF, 0xF, true);   // row_shr:2
+      incl += __builtin_amdgcn_update_dpp(0, incl, 0x114, 0xF, 0xF, true);   // row_shr:4
+      incl += __builtin_amdgcn_update_dpp(0, incl, 0x118, 0xF, 0xF, true);   // row_shr:8
+      const int total = __builtin_amdgcn_ds_swizzle(incl, kAnd | (15 << 5));
+      const uint64_t em = __ballot((x & kEndBit) && skip == kSkipEsc);
+      const bool gesc = ((em >> (lane & ~(G - 1))) & (G == 64 ? ~0ull : ((1ull << G) - 1))) != 0;
+      int row;
+      if (known && !gesc) {
+        row = rb + incl - inc;
+      } else {               // exact rows from erow (rare)
+        row = in ? a.erow[eu] : 0;
+        rb = __builtin_amdgcn_ds_swizzle(row, kAnd);    // the group's first edge
+        row = in ? row : 0;
+      }
+      known = !gesc;
+      rb += total;
+      alv = in ? a.al[x & kColMask] : 0.f;
+      arv = in ? a.ar[row] : 0.f;
+    };
+    auto coef = [&](int2 q, int eb, float alv, float arv) -> int2 {
+      const int eu = eb + k;
+      if (!(k < U && eu >= e0 && eu < e1)) return make_int2(0, 0);
+      float z = __fadd_rn(__fdiv_rn(alv, s), __fdiv_rn(arv, s));
+      z = z > 0.f ? z : __fmul_rn(z, a.slope);
+      const float c = __fmul_rn(expf(z), __int_as_float(q.y));
+      if (a.coef && blockIdx.y == 0) a.coef[eu] = c;
+      return make_int2(q.x, __float_as_int(c));
+    };
+    int2 r0 = load_rec(e0), r1 = load_rec(e0 + U);
+    float al0, ar0;
+    prep(r0, e0, al0, ar0);
+    for (int bi = 0; bi < nblk; ++bi) {
+      const int e = e0 + bi * U;
+      const int2 r2 = load_rec(e + 2 * U);
+      float al1, ar1;
+      prep(r1, e + U, al1, ar1);
+      Blk bk;
+      float4 v[U][NC];
+      issue(coef(r0, e, al0, ar0), e, bk, v);
+      consume(e, bk, v);
+      r0 = r1;
+      r1 = r2;
+      al0 = al1;
+      ar0 = ar1;
+    }
+  } else {
     int2 rraw = load_rec(e0);
     for (int bi = 0; bi < nblk; ++bi) {
       const int e = e0 + bi * U;
@@ -371,7 +435,7 @@ __device__ __forceinline__ void task_walk(const TaskArgs& a, int wv, int nwaves)
       const int2 rnxt = load_rec(e + U);
       Blk bk;
       float4 v[U][NC];
-      issue(rraw, e, bk, v);
+      issue(mask_rec(rraw, e), e, bk, v);
       consume(e, bk, v);
       rraw = rnxt;
     }
@@ -391,8 +455,9 @@ __device__ __forceinline__ void task_walk(const TaskArgs& a, int wv, int nwaves)
   }
 }
 
+// at most 128 VGPRs: 4 waves per SIMD (64 gathers in flight per SIMD at U = 16)
 template <int G, int NC, int U, bool FAR, bool GAT = false, bool PART = false>
-__global__ void __launch_bounds__(kTaskThreads)
+__global__ void __launch_bounds__(kTaskThreads) __attribute__((amdgpu_waves_per_eu(4)))
 spmm_task_kernel(TaskArgs a) {
   const int nwaves = (int)gridDim.x * (kTaskThreads / 64);
   // wave-uniform in an SGPR: the record buffer resource built from it is then
