@@ -1271,6 +1271,14 @@ vq_assign_kernel(const float* __restrict__ X, int64_t ldx,
 // |e|^2, E0, keeps all of them out: (sqrt(E0) - |x|)^2 > score + Delta.
 // ---------------------------------------------------------------------------
 
+// (a & m) | o in one VOP3 (the compiler splits it when m and o are both
+// wave-uniform: one scalar operand per VOP3 on gfx950); o goes through a VGPR
+__device__ __forceinline__ uint32_t and_or_u32(uint32_t a, uint32_t m, uint32_t o) {
+  uint32_t r;
+  asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(m), "v"(o));
+  return r;
+}
+
 __device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
   uint32_t r;   // operands are VALU results (never raw MFMA results: no hazard)
   asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
@@ -1544,15 +1552,19 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
         __syncthreads();
       }
       uint32_t cb[4], s2[4];
-      int cp[4];
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         cb[g] = 0xffffffffu;
         s2[g] = 0xffffffffu;
-        cp[g] = 0;
       }
       const char* ap = lds + a_lane;
       const int mlim = min(mcount, m_sweep);
+      // the pair index rides in the low bits of each pair minimum (the score's
+      // last pb bits are replaced: |change| < 2^pb ulp, paid for in the
+      // acceptance margin below), so min() keeps the earliest pair of equal
+      // minima without a compare-and-select per pair
+      const int npair = (mlim + 31) >> 5;
+      const uint32_t pmask = npair > 1 ? (2u << (31 - __builtin_clz((uint32_t)npair - 1))) - 1 : 0u;
       const floatx4 zero = {0.f, 0.f, 0.f, 0.f};
       for (int p = 0; p * 32 < mlim; ++p, ap += 512) {
         const half8 a0 = *reinterpret_cast<const half8*>(ap);
@@ -1576,11 +1588,13 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
           for (int g = 0; g < 4; ++g) d[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, bop[g], zero, 0, 0, 0);
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
-            const uint32_t mt = min(min(m4[g], min(__float_as_uint(d[g][0]), __float_as_uint(d[g][1]))),
-                                    min(__float_as_uint(d[g][2]), __float_as_uint(d[g][3])));
+            // a chain, not a tree: two v_min3_u32 (the MFMA results are read by
+            // compiler-visible instructions, so its MFMA read hazards hold)
+            uint32_t mm = min(min(m4[g], __float_as_uint(d[g][0])), __float_as_uint(d[g][1]));
+            mm = min(min(mm, __float_as_uint(d[g][2])), __float_as_uint(d[g][3]));
+            const uint32_t mt = and_or_u32(mm, ~pmask, (uint32_t)p);
             s2[g] = umed3(mt, cb[g], s2[g]);            // min(s2, max(mt, cb)): cb <= s2
-            cp[g] = mt < cb[g] ? p : cp[g];             // strict: the earliest pair wins ties
-            cb[g] = min(mt, cb[g]);
+            cb[g] = min(mt, cb[g]);                     // equal scores: the earliest pair
           }
         }
       }
@@ -1589,7 +1603,7 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
       // = pair, then quad)
       uint32_t kk[4];
 #pragma unroll
-      for (int g = 0; g < 4; ++g) kk[g] = (uint32_t)(cp[g] * 4 + q);
+      for (int g = 0; g < 4; ++g) kk[g] = ((cb[g] & pmask) << 2) | (uint32_t)q;
       transpose_quads(cb);
       transpose_quads(s2);
       transpose_quads(kk);
@@ -1604,7 +1618,11 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
       const float fmin = __uint_as_float(rmin);
       const float fsec = __uint_as_float(sec);
       const float tmin = fmin - (sx + 1.f);
-      const float delta = (978.f * sx + 390.f * fabsf(tmin) + 489.f) * 5.9604645e-8f;
+      // + the pair-index bits: each of fmin, fsec is within pmask ulp
+      // (<= pmask * 2^-23 * value) of its score, so 2 (pmask + 1) 2^-23 fsec
+      // covers both
+      const float delta = (978.f * sx + 390.f * fabsf(tmin) + 489.f) * 5.9604645e-8f +
+                          (float)(pmask + 1) * 2.3841858e-7f * fsec;
       bool exact_ok = (fsec - fmin > delta) && (delta < 0.25f);
       const unsigned int bigm = s_bigmin;
       if (bigm != 0x7f800000u) {                      // out-of-range codewords staged
