@@ -332,8 +332,11 @@ int vqgnn_gat_edge_grad(const int32_t* rows, const int32_t* col, const float* co
  *     vqgnn_gat_coef + vqgnn_spmm_task + vqgnn_gat_normalize; the coefficients are
  *     never materialised unless coef (optional, [nnz], CSR order) is given for
  *     the backward; den (optional, [n_rows]) receives the sums.  erow: the
- *     COO row of every edge (vqgnn_csr_expand_rows).  Plan and workspace as
- *     6e (records hold the adjacency values w).                              */
+ *     COO row of every edge (vqgnn_csr_expand_rows); the default kernel
+ *     derives each edge's row from the plan's row-end records and reads erow
+ *     only for blocks after 31 or more consecutive empty rows (and the G = 8
+ *     shape), but it must always be valid.  Plan and workspace as 6e
+ *     (records hold the adjacency values w).                                 */
 int vqgnn_gat_spmm_task(const int32_t* rowptr, int32_t n_rows, int32_t n_cols, int64_t nnz,
                         int32_t B, const float* X, int64_t ldx, const float* X2, int64_t ldx2,
                         int32_t F, float* out, int64_t ldo, const int32_t* plan,
