@@ -152,12 +152,17 @@ def test_gat_reference_forward_dense_input():
     np.testing.assert_allclose(out.detach().cpu().numpy(), ref.numpy(), rtol=1e-5, atol=1e-6)
 
 
-def _hub_csr(n, B, rng):
+def _hub_csr(n, B, rng, empty_runs=False):
     """A batch-like CSR with hub rows (cut by the task split), empty rows and
-    single-edge rows; GAT-normalised (D^-1) positive weights."""
+    single-edge rows; GAT-normalised (D^-1) positive weights.  empty_runs:
+    also runs of 30-100 consecutive empty rows (the row-end records' skip
+    escape: the fused kernel then reads the rows from erow)."""
     deg = rng.integers(1, 20, size=n)
     deg[[5, n // 2, B - 1]] = [700, 333, 1200]
     deg[rng.random(n) < 0.05] = 0
+    if empty_runs:
+        for a, ln in ((100, 30), (200, 31), (300, 32), (1000, 100), (B - 40, 39), (n // 2 + 1, 64)):
+            deg[a:a + ln] = 0
     rowptr = np.zeros(n + 1, np.int64)
     rowptr[1:] = np.cumsum(deg)
     col = np.concatenate([np.sort(rng.choice(n, size=d, replace=d > n)) for d in deg])
@@ -165,8 +170,9 @@ def _hub_csr(n, B, rng):
     return rowptr, col.astype(np.int64), val
 
 
-@pytest.mark.parametrize("F", [32, 128, 256])
-def test_gat_fused_kernel_matches_coefficient_path(F):
+@pytest.mark.parametrize("F,empty_runs", [(32, False), (128, False), (256, False), (128, True),
+                                          (32, True)])
+def test_gat_fused_kernel_matches_coefficient_path(F, empty_runs):
     """vqgnn_gat_spmm_task (coefficients in the aggregation kernel) against the
     coefficient pass + task SpMM on coefficient records + normalise, on hub
     rows cut across tasks,
@@ -174,7 +180,7 @@ def test_gat_fused_kernel_matches_coefficient_path(F):
     vqgnn_gat_coef's."""
     rng = np.random.default_rng(F + 1)
     n, B = 3000, 1800
-    rowptr, col, val = _hub_csr(n, B, rng)
+    rowptr, col, val = _hub_csr(n, B, rng, empty_runs)
     adj = CSR(torch.as_tensor(rowptr), torch.as_tensor(col), torch.as_tensor(val),
               (n, n)).to(DEV)
     nnz = adj.nnz()
