@@ -455,9 +455,11 @@ __device__ __forceinline__ void task_walk(const TaskArgs& a, int wv, int nwaves)
   }
 }
 
-// at most 128 VGPRs: 4 waves per SIMD (64 gathers in flight per SIMD at U = 16)
+// the default shape (G = 32, NC = 1) at most 128 VGPRs: 4 waves per SIMD (64
+// gathers in flight per SIMD at U = 16); the wider experiment shapes unbounded
 template <int G, int NC, int U, bool FAR, bool GAT = false, bool PART = false>
-__global__ void __launch_bounds__(kTaskThreads) __attribute__((amdgpu_waves_per_eu(4)))
+__global__ void __launch_bounds__(kTaskThreads)
+__attribute__((amdgpu_waves_per_eu((G == 32 && NC == 1) ? 4 : 1)))
 spmm_task_kernel(TaskArgs a) {
   const int nwaves = (int)gridDim.x * (kTaskThreads / 64);
   // wave-uniform in an SGPR: the record buffer resource built from it is then
