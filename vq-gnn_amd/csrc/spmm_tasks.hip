@@ -334,13 +334,16 @@ __device__ __forceinline__ void task_walk(const TaskArgs& a, int wv, int nwaves)
           } else {
             if (a.den && k == 0 && blockIdx.y == 0) a.den[r] = den;
             if (r < a.norm_B) {            // models.py:188: out[:, :F] /= out[:, F] + 1e-16
-              const float q = __fadd_rn(den, 1e-16f);
+              // one v_rcp_f32 (1 ulp) and four multiplies instead of four IEEE
+              // divisions (≈ 2 ulp, inside the 1e-5 bound; the walker is
+              // VALU-bound and this path runs at every row end)
+              const float rq = __builtin_amdgcn_rcpf(__fadd_rn(den, 1e-16f));
 #pragma unroll
               for (int i = 0; i < NC; ++i) {
-                acc[i].x = __fdiv_rn(acc[i].x, q);
-                acc[i].y = __fdiv_rn(acc[i].y, q);
-                acc[i].z = __fdiv_rn(acc[i].z, q);
-                acc[i].w = __fdiv_rn(acc[i].w, q);
+                acc[i].x = __fmul_rn(acc[i].x, rq);
+                acc[i].y = __fmul_rn(acc[i].y, rq);
+                acc[i].z = __fmul_rn(acc[i].z, rq);
+                acc[i].w = __fmul_rn(acc[i].w, rq);
               }
             }
           }
