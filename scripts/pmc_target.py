@@ -1,6 +1,6 @@
 """Run one hot-path kernel a few times on a bench config's batch (PMC target).
 CONFIG=<bench config> (reddit configs build graph and batch on the device);
-argv[1]: step | vq | spmm."""
+argv[1]: step | vq | spmm | gat (the fused GAT aggregation of the bench)."""
 import os
 import sys
 
@@ -42,8 +42,16 @@ bank = bank.to(dev)
 bank.feature_update(X, 0, nb, True, codes=codes, batch_idx=bidx)
 xt, _ = kernels.gather_codewords(subset, b.B, codes, bank.emb_out, D)
 plan = adj.plan(F, B=b.B)
+gat = None
+if what == "gat":
+    from vq_gnn_amd.convs_gat import OurGATConv
+    torch.manual_seed(4)
+    gat = OurGATConv(F + 1, F + 1, bias=False, add_self_loops=False).to(dev)
 torch.cuda.synchronize()
 for _ in range(reps):
+    if gat is not None:
+        with torch.no_grad():
+            gat.fused_forward(X, adj, xt, b.B)
     if what in ("vq", "step"):
         bank.update(X, G, 0, nb, True, codes=codes, batch_idx=bidx)
     if what in ("spmm", "step"):
