@@ -300,7 +300,7 @@ def main():
     #  input row once (x and x_first_order) + the output rows.
     spmm_bytes = 4 * (n + 1) + 8 * nnz + 4 * n * F + 4 * n * F
     vq_flops = 2.0 * B * M * W * nb
-    pmc, pmc_note = load_pmc(args)
+    pmc, pmc_ctr, pmc_note = load_pmc(args)
     agg_name = ("gat aggregation (alpha + fused coefficient/SpMM/normalise walker)"
                 if gat is not None else "spmm_task_kernel+spmm_task_fixup_kernel")
     agg_pmc = "spmm_task_kernel"
@@ -325,16 +325,15 @@ def main():
                                    "(profiles/r03_reddit_spmm_pmc.txt)")
     asg_name = ("vq_filter_kernel" if W <= 8 and os.environ.get("VQGNN_ASSIGN_EXACT", "0") in ("", "0")
                 else "vq_assign_kernel")
-    rl_vq = dict(kernel=asg_name, bound="mfma",
-                 achieved=vq_flops / (assign_ms * 1e-3) / 1e12, peak=157.3, unit="TFLOP/s",
-                 flops_per_launch=vq_flops, ms_per_launch=assign_ms,
-                 flops_note="2*B*M*W*nb f32 distance flops over the f32 matrix peak",
-                 traffic=pmc.get(asg_name))
-    rl_vq["frac"] = rl_vq["achieved"] / rl_vq["peak"]
+    rl_vq = assign_roofline(asg_name, assign_ms, B, M, W, nb, vq_flops, pmc_ctr.get(asg_name))
+    rl_vq["traffic"] = pmc.get(asg_name)
     dominant = rl_spmm if spmm_ms >= assign_ms else rl_vq
     roofline = dict(bound=dominant["bound"], achieved=dominant["achieved"], peak=dominant["peak"],
                     unit=dominant["unit"], frac=dominant["frac"], traffic=dominant["traffic"],
                     kernel=dominant["kernel"], traffic_source=pmc_note)
+    for k in ("limiter", "valu_issue_frac", "wait_frac", "effective_f32_frac"):
+        if k in dominant:
+            roofline[k] = dominant[k]
 
     # measured device copy rate beside the 8 TB/s spec (a 1 GiB HBM -> HBM
     # copy, read + write bytes), after the timed region
@@ -380,6 +379,8 @@ def main():
             plan_ms=plan_ms,
         )
         print(json.dumps(out))
+    if comm is not None:
+        comm.close()            # direct RCCL communicators: a clean destroy on every rank
     if dist.is_initialized():
         dist.destroy_process_group()
 
@@ -404,23 +405,72 @@ FABRIC_CEILING = {"reddit_gcn": (27.2, 0.56, 7.39), "reddit_gcn_l1": (164.8, 0.5
 
 
 def load_pmc(args):
-    """Per-launch HBM bytes from profiles/pmc_latest.json (scripts/pmc_to_json.py)
-    -- only when it was captured on this config AND on the library this process
-    runs (its lib_sha256); otherwise traffic is null with the reason."""
+    """Per-launch HBM bytes and SQ counters from profiles/pmc_latest.json
+    (scripts/pmc_to_json.py) -- only when they were captured on this config
+    AND on the library this process runs (its lib_sha256); otherwise none,
+    with the reason."""
     if not os.path.exists(args.pmc_json):
-        return {}, "no PMC file"
+        return {}, {}, "no PMC file"
     try:
         pm = json.load(open(args.pmc_json))
     except (OSError, ValueError) as exc:
-        return {}, f"unreadable PMC file ({exc})"
+        return {}, {}, f"unreadable PMC file ({exc})"
     if pm.get("config") != args.config or pm.get("semantics", "update") != args.semantics:
-        return {}, f"PMC file is for {pm.get('config')}/{pm.get('semantics')}"
+        return {}, {}, f"PMC file is for {pm.get('config')}/{pm.get('semantics')}"
     lib_hash = lib_digest()
     if pm.get("lib_sha256") != lib_hash:
-        return {}, (f"PMC file from another build (lib {str(pm.get('lib_sha256'))[:12]}, "
-                    f"running {lib_hash[:12]}): traffic withheld")
-    return pm.get("hbm_bytes_per_launch", {}), (
+        return {}, {}, (f"PMC file from another build (lib {str(pm.get('lib_sha256'))[:12]}, "
+                        f"running {lib_hash[:12]}): traffic withheld")
+    return pm.get("hbm_bytes_per_launch", {}), pm.get("counters_per_launch", {}), (
         f"{os.path.relpath(args.pmc_json, ROOT)} (lib {lib_hash[:12]}, git {pm.get('git_head')})")
+
+
+# gfx950 (MI355X_MICROARCH.md): dense f16 matrix peak, f32 matrix peak, SIMDs,
+# nominal clock, cycles per wave64 VALU instruction on a SIMD32
+F16_PEAK_TF, F32_PEAK_TF, SIMDS, CLOCK_HZ, VALU_CYCLES = 2500.0, 157.3, 1024, 2.4e9, 2
+
+
+def assign_roofline(name, assign_ms, B, M, W, nb, f32_flops, ctr):
+    """The assign's roofline on the resources it issues:
+    vq_filter_kernel scores every codeword with v_mfma_f32_16x16x32_f16
+    (16,384 flops per instruction) and recomputes the candidates on the VALU,
+    so it is priced against the dense f16 matrix peak, with the VALU issue
+    fraction and the share of wave cycles spent waiting beside it, from the
+    hash-stamped PMC counters of this build (SQ_INSTS_MFMA, SQ_INSTS_VALU,
+    SQ_WAIT_ANY / SQ_WAVE_CYCLES).  Without counters the MFMA count is the
+    analytic lower bound (64 MFMAs per 64-row wave iteration per 256
+    codewords).  The exact f32 path (vq_assign_kernel, W > 8) is priced
+    against the f32 matrix peak.  f32-equivalent distance work over the f32
+    peak is reported only as effective_f32_frac."""
+    t = assign_ms * 1e-3
+    eff = f32_flops / t / 1e12 / F32_PEAK_TF
+    if name != "vq_filter_kernel":
+        return dict(kernel=name, bound="mfma", achieved=f32_flops / t / 1e12, peak=F32_PEAK_TF,
+                    unit="TFLOP/s", frac=eff, flops_per_launch=f32_flops, ms_per_launch=assign_ms,
+                    flops_note="2*B*M*W*nb f32 flops (exact sweep, v_mfma_f32_16x16x4_f32)",
+                    effective_f32_frac=eff)
+    if ctr and ctr.get("SQ_INSTS_MFMA"):
+        mfma = ctr["SQ_INSTS_MFMA"]
+        src = "SQ_INSTS_MFMA x 16384 (PMC, this build)"
+    else:
+        mfma = nb * -(-B // 64) * 4 * (M // 16)
+        src = "analytic lower bound: nb * ceil(B/64) * 4 groups * M/16 tiles (no PMC for this build)"
+    f16 = mfma * 16384.0
+    out = dict(kernel=name, bound="mfma", achieved=f16 / t / 1e12, peak=F16_PEAK_TF,
+               unit="TFLOP/s", flops_per_launch=f16, ms_per_launch=assign_ms,
+               flops_note=f"f16 MFMA flops issued: {src}; dense f16 peak",
+               effective_f32_frac=eff,
+               effective_f32_note="2*B*M*W*nb f32 distance flops / time / 157.3 TF/s (f32 peak): "
+                                  "what the exact path would need, not a roofline")
+    out["frac"] = out["achieved"] / out["peak"]
+    if ctr and ctr.get("SQ_INSTS_VALU") and ctr.get("SQ_WAVE_CYCLES"):
+        out["valu_issue_frac"] = ctr["SQ_INSTS_VALU"] * VALU_CYCLES / SIMDS / CLOCK_HZ / t
+        out["wait_frac"] = ctr.get("SQ_WAIT_ANY", 0.0) / ctr["SQ_WAVE_CYCLES"]
+        busiest = max(("f16 MFMA", out["frac"]), ("VALU issue", out["valu_issue_frac"]),
+                      key=lambda kv: kv[1])
+        out["limiter"] = (f"latency: {out['wait_frac']:.0%} of wave cycles waiting; busiest issue "
+                          f"port {busiest[0]} at {busiest[1]:.0%} (PMC)")
+    return out
 
 
 def time_plan(adj, n, nnz, reps=5):

@@ -294,13 +294,19 @@ int vqgnn_csr_expand_rows(const int32_t* rowptr, int32_t n_rows, int64_t nnz,
  *    gat_alpha: alpha_l/r[i] = x_in[i] . att_l/r (att length F + ones) and
  *      params[5] = {max_l, max_r, s, ds/dmax_l, ds/dmax_r} with
  *      s = sqrt(max_l^2+1) * sqrt(max_r^2+1)                  (convs.py:209-211)
- *    gat_coef: coef[e] = exp(leaky(alpha_l[col]/s + alpha_r[row]/s)) * val[e]
+ *      and, when alpha_l_s / alpha_r_s are given (both or neither), the
+ *      per-node scaled scalars alpha_l_s[i] = alpha_l[i] / s, alpha_r_s[i] =
+ *      alpha_r[i] / s, as the reference divides once per node
+ *      (convs.py:209-211) and only adds per edge (:256).  Every per-edge
+ *      consumer below takes these scaled arrays.
+ *    gat_coef: coef[e] = exp(leaky(alpha_l_s[col] + alpha_r_s[row])) * val[e]
  *      (no max shift, no softmax normalisation), den[i] = sum_e coef[e] in
  *      CSR order (the ones column of the aggregation)         (convs.py:249-266)
  *    (gat_coef + vqgnn_spmm_task on records of coef + gat_normalize is the
  *    unfused form of vqgnn_gat_spmm_task, 8b, kept as its test reference.)
  *    gat_normalize: rows < B: out[i][:F] /= den[i] + eps       (models.py:188)
  *    gat_edge_grad: backward of the coefficient chain for every edge:
+ *      a = alpha_l_s[col] + alpha_r_s[row] (s = params[2]);
  *      dcoef = dy[row] . x_in[col][:F] + dden[row];  da = dcoef*coef*leaky'(a);
  *      dalpha_l[col] += da/s; dalpha_r[row] += da/s; ds_row[row] += -da*a/s
  *      (atomic adds: the caller zeroes dalpha_l, dalpha_r, ds_row).
@@ -309,24 +315,24 @@ size_t vqgnn_gat_alpha_workspace(int32_t n);
 int vqgnn_gat_alpha(const float* X, int64_t ldx, const float* X2, int64_t ldx2,
                     int32_t B, int32_t n, int32_t F, int32_t ones,
                     const float* att_l, const float* att_r, float* alpha_l, float* alpha_r,
-                    float* params, void* workspace, vqgnn_stream_t stream);
+                    float* alpha_l_s, float* alpha_r_s, float* params, void* workspace,
+                    vqgnn_stream_t stream);
 int vqgnn_gat_coef(const int32_t* rowptr, const int32_t* col, const float* val,
-                   int32_t n_rows, int64_t nnz, const float* alpha_l, const float* alpha_r,
-                   const float* params, float negative_slope, float* coef, float* den,
-                   vqgnn_stream_t stream);
+                   int32_t n_rows, int64_t nnz, const float* alpha_l_s, const float* alpha_r_s,
+                   float negative_slope, float* coef, float* den, vqgnn_stream_t stream);
 int vqgnn_gat_normalize(float* out, int64_t ldo, int32_t B, int32_t F, const float* den,
                         float eps, vqgnn_stream_t stream);
 int vqgnn_gat_edge_grad(const int32_t* rows, const int32_t* col, const float* coef,
                         int64_t nnz, const float* X, int64_t ldx, const float* X2,
                         int64_t ldx2, int32_t B, int32_t F, const float* dy, int64_t lddy,
-                        const float* dden, const float* alpha_l, const float* alpha_r,
+                        const float* dden, const float* alpha_l_s, const float* alpha_r_s,
                         const float* params, float negative_slope, float* dalpha_l,
                         float* dalpha_r, float* ds_row, vqgnn_stream_t stream);
 
 /* 8b. Fused GAT aggregation (the default GAT forward): the task-split SpMM of
- *     6e with each edge's coefficient exp(leaky(alpha_l[j]/s + alpha_r[i]/s))
- *     * w computed in the kernel (the op order of vqgnn_gat_coef; s =
- *     params[2] of vqgnn_gat_alpha), the ones column as a per-row
+ *     6e with each edge's coefficient exp(leaky(alpha_l_s[j] + alpha_r_s[i]))
+ *     * w computed in the kernel (the op order of vqgnn_gat_coef; the scaled
+ *     scalars of vqgnn_gat_alpha), the ones column as a per-row
  *     coefficient sum, and rows < norm_B divided by that sum + 1e-16 before
  *     the store (models.py:188; norm_B = 0: no normalisation).  Replaces
  *     vqgnn_gat_coef + vqgnn_spmm_task + vqgnn_gat_normalize; the coefficients are
@@ -341,8 +347,8 @@ int vqgnn_gat_spmm_task(const int32_t* rowptr, int32_t n_rows, int32_t n_cols, i
                         int32_t B, const float* X, int64_t ldx, const float* X2, int64_t ldx2,
                         int32_t F, float* out, int64_t ldo, const int32_t* plan,
                         const int64_t* records, int32_t K, int32_t n_jobs, int32_t n_empty,
-                        const int32_t* erow, const float* alpha_l, const float* alpha_r,
-                        const float* params, float negative_slope, int32_t norm_B, float* den,
+                        const int32_t* erow, const float* alpha_l_s, const float* alpha_r_s,
+                        float negative_slope, int32_t norm_B, float* den,
                         float* coef, void* workspace, vqgnn_stream_t stream);
 
 /* 8b. GAT backward helper: vqgnn_gat_att_grad: d att_l / d att_r [F + ones]

@@ -5,12 +5,13 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-TAG=${TAG:-r03m}
+TAG=${TAG:-r04}
 O=gpurun_out/$TAG
 mkdir -p $O
 log() { echo "== $(date +%T) $1" | tee -a $O/progress.log; }
-log tests && timeout -k 10 400 python -u -m pytest tests/test_gpu_gat.py tests/test_gpu_spmm_task.py \
-     tests/test_gpu_spmm.py tests/test_gpu_configs.py -m gpu -x -v -p no:cacheprovider --timeout 120 \
+TESTS=${TESTS:-tests/test_gpu_gat.py tests/test_gpu_spmm_task.py tests/test_gpu_spmm.py tests/test_gpu_configs.py}
+log smoke && timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 \
+&& log tests && timeout -k 10 600 python -u -m pytest $TESTS -m gpu -x -v -p no:cacheprovider --timeout 120 \
      --timeout-method thread > $O/pytest.log 2>&1 \
 && log pmc && TAG=${TAG}_pmc TARGET=step bash scripts/gpu_pmc.sh > $O/pmc.log 2>&1 \
 && python scripts/pmc_summary.py gpurun_out/pmc_${TAG}_pmc > $O/pmc_summary.txt \
@@ -20,6 +21,7 @@ log tests && timeout -k 10 400 python -u -m pytest tests/test_gpu_gat.py tests/t
      -- python bench.py --steps 30 --warmup 5 --no-cpu-baseline --pmc-json $O/pmc_latest.json > $O/prof_bench.log 2>&1
 rc=$?
 log "chain rc=$rc"
+tail -2 $O/smoke.log
 grep -E "passed|failed" $O/pytest.log | tail -1
 grep -h '^{' $O/bench.log | cut -c1-300
 exit $rc

@@ -131,6 +131,32 @@ def main(out_dir):
     for r in range(world):
         for k in range(3):
             res[f"set_{r}_{k}"] = sets[r][k].numpy()
+    # a batch over the CodebookSync capacity (capacity 300, world 2): rank 0
+    # at 500 rows (the summed rows exceed world * capacity) and then at 700
+    # (over world * capacity itself).  Neither rank raises between the
+    # collectives (no hang), the EMA statistics stay inside the fixed-point
+    # row bound (finite, identical replicas), and both ranks raise together
+    # at the check after the update.
+    for tag, b_over in (("over500", 500), ("over700", 700)):
+        ob = fresh_bank()
+        ob.comm = CodebookSync(count_group=sync.count_group, capacity=300)
+        oc = codes0.to(dev)
+        nodes = perm[:b_over] if rank == 0 else perm[2000:2200]
+        go = torch.Generator().manual_seed(7 + rank)
+        Xo = torch.randn(nodes.numel(), F, generator=go).to(dev)
+        Go = (torch.randn(nodes.numel(), F, generator=go) * 1e-3).to(dev)
+        ob.update(Xo, Go, 0, nb, True, codes=oc, batch_idx=nodes.to(dev), defer=True)
+        ob.finish_update()
+        ob.sync_codes()
+        torch.cuda.synchronize()
+        try:
+            ob.check_bad_init()
+            res[f"{tag}_raised"] = 0
+        except ValueError as exc:
+            res[f"{tag}_raised"] = int("capacity" in str(exc))
+        for k in ("emb", "emb_out", "ema_w", "cs"):
+            res[f"{tag}_{k}"] = getattr(ob, k).cpu().numpy()
+        res[f"{tag}_codes"] = oc.cpu().numpy()
     np.savez(os.path.join(out_dir, f"r{rank}.npz"), **res)
     dist.barrier()
     dist.destroy_process_group()

@@ -114,6 +114,69 @@ def test_arxiv_gat_vq_update_vs_oracle(arxiv_gat):
     _vq_update_vs_oracle(g, b, 128, 1024, seed=5)
 
 
+@pytest.fixture(scope="module")
+def arxiv_gcn():
+    g, _, b = graph.make_batch(graph.CONFIGS["arxiv_gcn"])
+    return g, b
+
+
+def _compare_branches(idx, codes, bidx, states, sample, ref_call, bank, tag):
+    torch.cuda.synchronize()
+    idx_c = idx.cpu()
+    assert torch.equal(codes[bidx].long().cpu(), idx_c.T), f"{tag}: codes != indices"
+    for st, br in zip(states, sample):
+        ref = ref_call(st, br)
+        n_mis = int((idx_c[br] != ref[:, 0]).sum())
+        assert n_mis == 0, f"{tag} branch {br}: {n_mis} index mismatches"
+        _check_state(bank, st, br, tag)
+
+
+def test_arxiv_gcn_headline_vq_vs_oracle(arxiv_gcn):
+    """The headline config (BASELINE configs[1]: arxiv GCN, M = 256, D = 4, the
+    full 84,670-row cluster batch, nb = 32) through bench.py's exact sequence:
+    the warm-up feature_update (W = 4) on the fresh codebook, then the timed
+    step's update(defer=True) (W = 8) with the codeword gather queued before
+    finish_update(), then feature_update (W = 4) on the warm codebook.  At
+    M <= 512 the filter stages an f32 candidate copy in LDS and packs 3-bit
+    pair indices (a path no other full-size test takes).  Indices of 6 spread
+    branches bit-exact against vq_ref (vq.py:160-279), BatchNorm state
+    bit-identical, EMA state within 1e-5."""
+    g, b = arxiv_gcn
+    F, M = 128, 256
+    nb, B = F // D, b.B
+    assert B == 84_670
+    X = torch.randn(B, F, generator=torch.Generator().manual_seed(1))        # bench.py inputs
+    G = torch.randn(B, F, generator=torch.Generator().manual_seed(2)) * 1e-3
+    sample = [0, 5, 11, 17, 23, 31]
+    bank, states = _bank_and_states(nb, M, sample, seed=0)
+    bidx = torch.from_numpy(b.batch_idx).to(DEV)
+    _, subset, _ = graph.batch_to_device(b, DEV)
+    codes = torch.randint(0, M, (g.N, nb), dtype=torch.int16,
+                          generator=torch.Generator().manual_seed(5)).to(DEV)
+    Xd, Gd = X.to(DEV), G.to(DEV)
+    idx = torch.empty(nb, B, dtype=torch.long, device=DEV)
+    cols = lambda t, br: t[:, br * D:(br + 1) * D]      # noqa: E731 (strided slices, models.py:162)
+
+    bank.feature_update(Xd, 0, nb, True, idx_out=idx, codes=codes, batch_idx=bidx)
+    _compare_branches(idx, codes, bidx, states, sample,
+                      lambda st, br: vq_ref.feature_update(st, cols(X, br)), bank, "warm-up W=4")
+    # the warm codebook holds dead codewords (|e|^2 >= 2^15: scored +inf by
+    # the filter, DESIGN.md §4.1) -- the range path the update must take
+    assert int((bank.emb[:, :, :D].pow(2).sum(-1) >= 2 ** 15).sum()) > 0
+
+    bank.update(Xd, Gd, 0, nb, True, idx_out=idx, codes=codes, batch_idx=bidx, defer=True)
+    kernels.gather_codewords(subset, B, codes, bank.emb_out, D)   # queued as in the bench step
+    bank.finish_update()
+    _compare_branches(idx, codes, bidx, states, sample,
+                      lambda st, br: vq_ref.update(st, cols(X, br), cols(G, br))[0], bank,
+                      "update W=8")
+
+    bank.feature_update(Xd, 0, nb, True, idx_out=idx, codes=codes, batch_idx=bidx)
+    _compare_branches(idx, codes, bidx, states, sample,
+                      lambda st, br: vq_ref.feature_update(st, cols(X, br)), bank,
+                      "warm feature_update W=4")
+
+
 def _sampled_rows(rowptr, n_rows, k, seed, longest=16):
     lens = np.diff(rowptr[:n_rows + 1])
     rng = np.random.default_rng(seed)
@@ -202,11 +265,11 @@ def test_arxiv_gat_full_batch_vs_oracle(arxiv_gat):
     torch.manual_seed(4)
     conv = OurGATConv(F + 1, F + 1, bias=False, add_self_loops=False).to(DEV)
     x_d = torch.from_numpy(X).to(DEV)
-    al, ar, params = kernels.gat_alpha(x_d, conv.att_l.view(-1), conv.att_r.view(-1), F,
-                                       X2=xf_d, B=b.B, ones=True)
+    _, _, _, als, ars = kernels.gat_alpha(x_d, conv.att_l.view(-1), conv.att_r.view(-1), F,
+                                          X2=xf_d, B=b.B, ones=True)
     plan = adj.plan(F)
-    out, den, coef = kernels.gat_spmm(adj.rowptr, adj.col, adj.value, b.n, b.nnz, x_d, F, al,
-                                      ar, params, plan, adj.rows(), X2=xf_d, B=b.B, norm_B=b.B,
+    out, den, coef = kernels.gat_spmm(adj.rowptr, adj.col, adj.value, b.n, b.nnz, x_d, F, als,
+                                      ars, plan, adj.rows(), X2=xf_d, B=b.B, norm_B=b.B,
                                       want_den=True, want_coef=True)
     layer_out = conv.fused_forward(x_d, adj, xf_d, b.B)
     torch.cuda.synchronize()

@@ -86,6 +86,17 @@ def test_two_ranks_match_union_batch(tmp_path):
     for r in range(2):
         for k in range(3):
             np.testing.assert_array_equal(r0["stale_final"][sets[r][k]], own[r][k])
+    # over capacity: no hang, both ranks raise, the statistics stayed inside
+    # the fixed-point bound (finite state) and the replicas agree
+    for tag in ("over500", "over700"):
+        assert int(r0[f"{tag}_raised"]) == 1 and int(r1[f"{tag}_raised"]) == 1, tag
+        # (codes are not compared: the over-capacity rank's rows past the
+        # capacity are scattered into its own replica only, vq.py)
+        for k in ("emb", "emb_out", "ema_w", "cs"):
+            np.testing.assert_array_equal(r0[f"{tag}_{k}"], r1[f"{tag}_{k}"], err_msg=tag + k)
+        for k in ("emb_out", "ema_w", "cs"):
+            assert np.isfinite(r0[f"{tag}_{k}"]).all(), tag + k
+        assert np.abs(r0[f"{tag}_ema_w"]).max() < 1e3, tag   # no saturated fixed point
 
 
 def test_rccl_world1_deferred_update(tmp_path):

@@ -54,13 +54,17 @@ def test_gat_coefficients_and_alpha():
     conv = _conv(F, 2).to(DEV)
     _, _, adj = graph.batch_to_device(b, DEV)
     xd = torch.from_numpy(x).to(DEV)
-    al, ar, params = kernels.gat_alpha(xd[:b.B], conv.att_l.view(-1), conv.att_r.view(-1), F,
-                                       X2=xd[b.B:], B=b.B, ones=True)
+    al, ar, params, als, ars = kernels.gat_alpha(xd[:b.B], conv.att_l.view(-1),
+                                                 conv.att_r.view(-1), F, X2=xd[b.B:], B=b.B,
+                                                 ones=True)
     xin = torch.cat([torch.from_numpy(x), torch.ones(b.n, 1)], 1)
     al_ref = (xin * conv.att_l.detach().cpu().view(-1)).sum(-1)
     torch.testing.assert_close(al.cpu(), al_ref, rtol=1e-5, atol=1e-5)
     assert float(params[0]) == pytest.approx(float(al.max()), abs=0)
-    coef, den = kernels.gat_coef(adj.rowptr, adj.col, adj.value, b.n, b.nnz, al, ar, params)
+    # alpha / s per node: the reference's own division (convs.py:209-211)
+    s = params[2].cpu()
+    assert torch.equal(als.cpu(), al.cpu() / s) and torch.equal(ars.cpu(), ar.cpu() / s)
+    coef, den = kernels.gat_coef(adj.rowptr, adj.col, adj.value, b.n, b.nnz, als, ars)
     _, coef_ref = conv_ref.gat_forward(xin.numpy(), conv.att_l.detach().cpu().numpy(),
                                        conv.att_r.detach().cpu().numpy(), b.rowptr, b.col, b.val)
     np.testing.assert_allclose(coef.cpu().numpy(), coef_ref.numpy(), rtol=2e-6, atol=1e-7)
@@ -187,14 +191,14 @@ def test_gat_fused_kernel_matches_coefficient_path(F, empty_runs):
     x = torch.randn(B, F, device=DEV)
     xf = torch.randn(n - B, F, device=DEV)
     conv = _conv(F, 3).to(DEV)
-    al, ar, params = kernels.gat_alpha(x, conv.att_l.view(-1), conv.att_r.view(-1), F, X2=xf,
-                                       B=B, ones=True)
+    _, _, _, als, ars = kernels.gat_alpha(x, conv.att_l.view(-1), conv.att_r.view(-1), F, X2=xf,
+                                          B=B, ones=True)
     plan = adj.plan(F, B=B)
     assert isinstance(plan, kernels.TaskPlan)
-    out, den, coef = kernels.gat_spmm(adj.rowptr, adj.col, adj.value, n, nnz, x, F, al, ar,
-                                      params, plan, adj.rows(), X2=xf, B=B, norm_B=B,
+    out, den, coef = kernels.gat_spmm(adj.rowptr, adj.col, adj.value, n, nnz, x, F, als, ars,
+                                      plan, adj.rows(), X2=xf, B=B, norm_B=B,
                                       want_den=True, want_coef=True)
-    coef_ref, den_ref = kernels.gat_coef(adj.rowptr, adj.col, adj.value, n, nnz, al, ar, params)
+    coef_ref, den_ref = kernels.gat_coef(adj.rowptr, adj.col, adj.value, n, nnz, als, ars)
     assert torch.equal(coef, coef_ref)                    # same op order, same bits
     torch.testing.assert_close(den, den_ref, rtol=1e-6, atol=0)
     # the unfused chain: the same task plan with the coefficients as weights
@@ -214,11 +218,47 @@ def test_gat_fused_kernel_matches_coefficient_path(F, empty_runs):
         assert (err <= 1e-5 * sc + 1e-30).all(), f"rel err {(err / (sc + 1e-30)).max():.2e}"
     assert torch.equal(out[torch.as_tensor(np.diff(rowptr) == 0, device=DEV)],
                        torch.zeros_like(out[torch.as_tensor(np.diff(rowptr) == 0, device=DEV)]))
-    again, _, _ = kernels.gat_spmm(adj.rowptr, adj.col, adj.value, n, nnz, x, F, al, ar, params,
+    again, _, _ = kernels.gat_spmm(adj.rowptr, adj.col, adj.value, n, nnz, x, F, als, ars,
                                    plan, adj.rows(), X2=xf, B=B, norm_B=B)
     assert torch.equal(out, again)
     # the layer path runs the same fused kernel
     assert torch.equal(conv.fused_forward(x, adj, xf, B), out)
+
+
+def test_gat_cut_and_uncut_rows_share_the_normalisation():
+    """The walker (rows that end inside a task) and the fix-up (rows cut
+    across tasks) normalise a row the same way: every normalised row < B is
+    its raw coefficient-weighted sum times ONE reciprocal r_i of den_i +
+    1e-16 (v_rcp_f32, within 1 ulp of 1/(den_i + 1e-16)), so identical rows
+    get identical bits wherever the plan cuts them (an IEEE division in one
+    path and a reciprocal in the other would not satisfy this)."""
+    rng = np.random.default_rng(17)
+    n, B, F = 3000, 1800, 128
+    rowptr, col, val = _hub_csr(n, B, rng)
+    adj = CSR(torch.as_tensor(rowptr), torch.as_tensor(col), torch.as_tensor(val),
+              (n, n)).to(DEV)
+    nnz = adj.nnz()
+    x = torch.randn(B, F, device=DEV)
+    xf = torch.randn(n - B, F, device=DEV)
+    conv = _conv(F, 9).to(DEV)
+    _, _, _, als, ars = kernels.gat_alpha(x, conv.att_l.view(-1), conv.att_r.view(-1), F, X2=xf,
+                                          B=B, ones=True)
+    plan = adj.plan(F, B=B)
+    raw, _, _ = kernels.gat_spmm(adj.rowptr, adj.col, adj.value, n, nnz, x, F, als, ars, plan,
+                                 adj.rows(), X2=xf, B=B, norm_B=0)
+    out, den, _ = kernels.gat_spmm(adj.rowptr, adj.col, adj.value, n, nnz, x, F, als, ars, plan,
+                                   adj.rows(), X2=xf, B=B, norm_B=B, want_den=True)
+    raw, out, den = raw.cpu().numpy(), out.cpu().numpy(), den.cpu().numpy()
+    lens = np.diff(rowptr)
+    assert (lens[:B] > plan.K // 2).any()          # rows < B that the plan cuts across tasks
+    q = (den[:B] + np.float32(1e-16)).astype(np.float32)
+    r0 = (np.float32(1) / q).astype(np.float32)
+    ok = np.zeros(B, bool)
+    for step in (0, 1, -1):                        # r_i = 1/q_i or a neighbouring float
+        r = r0 if step == 0 else np.nextafter(r0, np.float32(np.inf * step)).astype(np.float32)
+        ok |= ((raw[:B] * r[:, None]).astype(np.float32) == out[:B]).all(1)
+    assert ok[lens[:B] > 0].all(), f"{int((~ok[lens[:B] > 0]).sum())} rows not raw * r_i"
+    assert np.array_equal(out[B:], raw[B:])        # rows >= B stay unnormalised
 
 
 @pytest.mark.parametrize("F", [32, 128, 36])
@@ -235,13 +275,13 @@ def test_gat_edge_grad_and_att_grad_kernels(F):
     x = torch.randn(B, F, device=DEV)
     xf = torch.randn(n - B, F, device=DEV)
     conv = _conv(F, 5).to(DEV)
-    al, ar, params = kernels.gat_alpha(x, conv.att_l.view(-1), conv.att_r.view(-1), F, X2=xf,
-                                       B=B, ones=True)
-    coef, den = kernels.gat_coef(adj.rowptr, adj.col, adj.value, n, adj.nnz(), al, ar, params)
+    al, ar, params, als, ars = kernels.gat_alpha(x, conv.att_l.view(-1), conv.att_r.view(-1), F,
+                                                 X2=xf, B=B, ones=True)
+    coef, den = kernels.gat_coef(adj.rowptr, adj.col, adj.value, n, adj.nnz(), als, ars)
     dy = torch.randn(n, F, device=DEV)
     dden = torch.randn(n, device=DEV)
     dal, dar, dsr = kernels.gat_edge_grad(adj.rows(), adj.col, coef, adj.nnz(), x, F, dy, dden,
-                                          al, ar, params, X2=xf, B=B)
+                                          als, ars, params, X2=xf, B=B)
     # fp64 chain: q_e = (x_in[j] . dy[i] + dden[i]) coef_e leaky'(a_e) / s
     rows, cols = adj.rows().long(), adj.col.long()
     xin = torch.cat([x, xf]).double()

@@ -71,7 +71,7 @@ SIGNATURES = {
     "vqgnn_gat_spmm_task": (ctypes.c_int, [_c_void_p, _i32, _i32, _i64, _i32, _c_void_p, _i64,
                                            _c_void_p, _i64, _i32, _c_void_p, _i64, _c_void_p,
                                            _c_void_p, _i32, _i32, _i32, _c_void_p, _c_void_p,
-                                           _c_void_p, _c_void_p, _f32, _i32, _c_void_p,
+                                           _c_void_p, _f32, _i32, _c_void_p,
                                            _c_void_p, _c_void_p, _c_void_p]),
     "vqgnn_csr_transpose_workspace": (_size, [_i32, _i32, _i64]),
     "vqgnn_csr_transpose": (ctypes.c_int, [_c_void_p, _c_void_p, _c_void_p, _i32, _i32, _i64,
@@ -81,10 +81,9 @@ SIGNATURES = {
     "vqgnn_gat_alpha_workspace": (_size, [_i32]),
     "vqgnn_gat_alpha": (ctypes.c_int, [_c_void_p, _i64, _c_void_p, _i64, _i32, _i32, _i32, _i32,
                                        _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
-                                       _c_void_p, _c_void_p]),
+                                       _c_void_p, _c_void_p, _c_void_p, _c_void_p]),
     "vqgnn_gat_coef": (ctypes.c_int, [_c_void_p, _c_void_p, _c_void_p, _i32, _i64, _c_void_p,
-                                      _c_void_p, _c_void_p, _f32, _c_void_p, _c_void_p,
-                                      _c_void_p]),
+                                      _c_void_p, _f32, _c_void_p, _c_void_p, _c_void_p]),
     "vqgnn_gat_normalize": (ctypes.c_int, [_c_void_p, _i64, _i32, _i32, _c_void_p, _f32,
                                            _c_void_p]),
     "vqgnn_gat_edge_grad": (ctypes.c_int, [_c_void_p, _c_void_p, _c_void_p, _i64, _c_void_p, _i64,

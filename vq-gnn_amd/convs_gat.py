@@ -7,7 +7,8 @@ no bias, ``att_l`` / ``att_r`` [1, heads, C], optional ``bias``) and their
 initialisation order, so the RNG stream at construction matches the reference.
 The arithmetic runs in HIP (include/vqgnn.h §8):
 
-  alpha_l/r = x_in . att_l/r (+ global max -> scale s)    vqgnn_gat_alpha
+  alpha_l/r = x_in . att_l/r (+ global max -> scale s,    vqgnn_gat_alpha
+              alpha / s once per node, convs.py:209-211)
   coef_e    = exp(leaky(alpha_l[j]/s + alpha_r[i]/s)) * w  } vqgnn_gat_spmm_task (one
   out       = sum_e coef_e * x_in[j]                       } fused kernel; the
   rows < B  : out /= sum_e coef_e + 1e-16                  } coefficients stay in
@@ -47,7 +48,8 @@ class GATFunction(torch.autograd.Function):
         n, nnz = adj.size(0), adj.nnz()
         F = x.shape[1]
         xc = x.contiguous()
-        al, ar, params = kernels.gat_alpha(xc, att_l, att_r, F, X2=x_first, B=B, ones=ones)
+        al, ar, params, als, ars = kernels.gat_alpha(xc, att_l, att_r, F, X2=x_first, B=B,
+                                                     ones=ones)
         # the fused attention path runs on the task plan (coefficients computed
         # per edge record), also for dense-block adjacencies
         plan = adj.plan(F, kind="task")
@@ -57,12 +59,12 @@ class GATFunction(torch.autograd.Function):
         # will need)
         grad = any(ctx.needs_input_grad[:4])
         out, den, coef = kernels.gat_spmm(
-            adj.rowptr, adj.col, adj.value, n, nnz, xc, F, al, ar, params, plan, adj.rows(),
+            adj.rowptr, adj.col, adj.value, n, nnz, xc, F, als, ars, plan, adj.rows(),
             X2=x_first, B=B if x_first is not None else None,
             norm_B=B if normalize else 0, negative_slope=slope, want_den=grad,
             want_coef=grad)
         ctx.save_for_backward(xc, x_first if x_first is not None else xc, att_l, att_r, al, ar,
-                              params, coef, den, out)
+                              als, ars, params, coef, den, out)
         ctx.has_first = x_first is not None
         ctx.adj, ctx.B, ctx.ones, ctx.normalize, ctx.slope, ctx.hook = \
             adj, B, ones, normalize, slope, hook
@@ -70,7 +72,7 @@ class GATFunction(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dz):
-        xc, x_first, att_l, att_r, al, ar, params, coef, den, z = ctx.saved_tensors
+        xc, x_first, att_l, att_r, al, ar, als, ars, params, coef, den, z = ctx.saved_tensors
         if not ctx.has_first:
             x_first = None
         adj, B, F = ctx.adj, ctx.B, xc.shape[1]
@@ -92,7 +94,7 @@ class GATFunction(torch.autograd.Function):
             ctx.hook(dy[:B])
         # coefficient chain -> d alpha_l, d alpha_r, d s
         dal, dar, dsr = kernels.gat_edge_grad(adj.rows(), adj.col, coef, nnz, xc, F, dy, dden,
-                                              al, ar, params, X2=x_first, B=B,
+                                              als, ars, params, X2=x_first, B=B,
                                               negative_slope=ctx.slope)
         ds = dsr.sum()
         # s = sqrt(max_l^2+1) sqrt(max_r^2+1); torch.max spreads its gradient

@@ -188,25 +188,39 @@ gat_scale_kernel(const float* __restrict__ block_max, int nblocks, float* __rest
   }
 }
 
-// coef[e] = exp(leaky(al[j]/s + ar[i]/s)) * w[e]; den[i] = sum_e coef[e] in
-// CSR order (the ones column of the aggregation).  One wave per row.
+// als[i] = alpha_l[i] / s, ars[i] = alpha_r[i] / s once per node: the
+// reference scales the attention scalars per node (convs.py:209-211, alpha_l =
+// alpha_l / scale) and only adds them per edge (:256), so every per-edge
+// consumer reads these instead of dividing twice per edge (bit-identical).
+__global__ void gat_div_kernel(const float* __restrict__ al, const float* __restrict__ ar, int n,
+                               const float* __restrict__ params, float* __restrict__ als,
+                               float* __restrict__ ars) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float s = params[2];
+  als[i] = __fdiv_rn(al[i], s);
+  ars[i] = __fdiv_rn(ar[i], s);
+}
+
+// coef[e] = exp(leaky(als[j] + ars[i])) * w[e] (als, ars: alpha / s per node);
+// den[i] = sum_e coef[e] in CSR order (the ones column of the aggregation).
+// One wave per row.
 __global__ void __launch_bounds__(kGatThreads)
 gat_coef_kernel(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
-                const float* __restrict__ val, int n_rows, const float* __restrict__ al,
-                const float* __restrict__ ar, const float* __restrict__ params, float slope,
-                float* __restrict__ coef, float* __restrict__ den) {
+                const float* __restrict__ val, int n_rows, const float* __restrict__ als,
+                const float* __restrict__ ars, float slope, float* __restrict__ coef,
+                float* __restrict__ den) {
   const int lane = threadIdx.x & 63;
   const int i = blockIdx.x * (kGatThreads / 64) + (threadIdx.x >> 6);
   if (i >= n_rows) return;
-  const float s = params[2];
-  const float ari = __fdiv_rn(ar[i], s);
+  const float ari = ars[i];
   const int rb = rowptr[i], re = rowptr[i + 1];
   float d = 0.f;
   for (int base = rb; base < re; base += 64) {
     const int e = base + lane;
     float c = 0.f;
     if (e < re) {
-      float a = __fadd_rn(__fdiv_rn(al[col[e]], s), ari);
+      float a = __fadd_rn(als[col[e]], ari);
       a = a > 0.f ? a : __fmul_rn(a, slope);
       c = __fmul_rn(expf(a), val[e]);
       coef[e] = c;
@@ -232,14 +246,15 @@ __global__ void gat_normalize_kernel(float* __restrict__ out, int64_t ldo, int B
 
 // Backward of the coefficient chain, one thread per edge e (row i, col j):
 //   dcoef = dy[i] . x_in[j][:F] + dden[i]      (dden = grad of the ones column)
-//   da    = dcoef * coef * (a > 0 ? 1 : slope),  a = al[j]/s + ar[i]/s
+//   da    = dcoef * coef * (a > 0 ? 1 : slope),  a = als[j] + ars[i]
+//   (als, ars = alpha / s per node, vqgnn_gat_alpha)
 //   dal[j] += da / s;  dar[i] += da / s;  dsrow[i] += -da * a / s
 __global__ void __launch_bounds__(kGatThreads)
 gat_edge_grad_kernel(const int32_t* __restrict__ rows, const int32_t* __restrict__ col,
                      const float* __restrict__ coef, int nnz, const float* __restrict__ X,
                      int64_t ldx, const float* __restrict__ X2, int64_t ldx2, int B, int F,
                      const float* __restrict__ dy, int64_t lddy, const float* __restrict__ dden,
-                     const float* __restrict__ al, const float* __restrict__ ar,
+                     const float* __restrict__ als, const float* __restrict__ ars,
                      const float* __restrict__ params, float slope, float* __restrict__ dal,
                      float* __restrict__ dar, float* __restrict__ dsrow) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
@@ -263,7 +278,7 @@ gat_edge_grad_kernel(const int32_t* __restrict__ rows, const int32_t* __restrict
   }
   const float dcoef = dot + (dden ? dden[i] : 0.f);
   const float s = params[2];
-  const float a = al[j] / s + ar[i] / s;
+  const float a = __fadd_rn(als[j], ars[i]);
   const float da = dcoef * coef[e] * (a > 0.f ? 1.f : slope);
   const float q = da / s;
   atomicAdd(dal + j, q);
@@ -282,8 +297,8 @@ gat_edge_grad_grp_kernel(const int32_t* __restrict__ rows, const int32_t* __rest
                          const float* __restrict__ coef, int nnz, const float* __restrict__ X,
                          int64_t ldx, const float* __restrict__ X2, int64_t ldx2, int B, int F,
                          const float* __restrict__ dy, int64_t lddy,
-                         const float* __restrict__ dden, const float* __restrict__ al,
-                         const float* __restrict__ ar, const float* __restrict__ params,
+                         const float* __restrict__ dden, const float* __restrict__ als,
+                         const float* __restrict__ ars, const float* __restrict__ params,
                          float slope, float* __restrict__ dal, float* __restrict__ dar,
                          float* __restrict__ dsrow) {
   constexpr int U = 4;
@@ -333,7 +348,7 @@ gat_edge_grad_grp_kernel(const int32_t* __restrict__ rows, const int32_t* __rest
     if (!ok[u]) continue;
     const int i = ii[u], j = jj[u];
     const float dcoef = dot[u] + (dden ? dden[i] : 0.f);
-    const float a = al[j] / s + ar[i] / s;
+    const float a = __fadd_rn(als[j], ars[i]);
     const float da = dcoef * coef[e0 + u] * (a > 0.f ? 1.f : slope);
     const float q = da / s;
     atomicAdd(dal + j, q);
@@ -458,8 +473,8 @@ extern "C" size_t vqgnn_gat_alpha_workspace(int32_t n) {
 extern "C" int vqgnn_gat_alpha(const float* X, int64_t ldx, const float* X2, int64_t ldx2,
                                int32_t B, int32_t n, int32_t F, int32_t ones,
                                const float* att_l, const float* att_r, float* alpha_l,
-                               float* alpha_r, float* params, void* workspace,
-                               vqgnn_stream_t stream) {
+                               float* alpha_r, float* alpha_l_s, float* alpha_r_s, float* params,
+                               void* workspace, vqgnn_stream_t stream) {
   clear_error();
   VQGNN_REQUIRE(n > 0 && F > 0 && B >= 0 && B <= n, "gat_alpha: bad shape (n=%d B=%d F=%d)",
                 n, B, F);
@@ -481,21 +496,26 @@ extern "C" int vqgnn_gat_alpha(const float* X, int64_t ldx, const float* X2, int
     hipLaunchKernelGGL(gat_alpha_kernel, dim3(nblocks), dim3(kGatThreads), 0, s, X, ldx, X2,
                        ldx2, B, n, F, ones, att_l, att_r, alpha_l, alpha_r, bm);
   hipLaunchKernelGGL(gat_scale_kernel, dim3(1), dim3(1024), 0, s, bm, nblocks, params);
+  VQGNN_REQUIRE((alpha_l_s == nullptr) == (alpha_r_s == nullptr),
+                "gat_alpha: alpha_l_s and alpha_r_s go together");
+  if (alpha_l_s)
+    hipLaunchKernelGGL(gat_div_kernel, dim3((n + 255) / 256), dim3(256), 0, s, alpha_l, alpha_r, n,
+                       params, alpha_l_s, alpha_r_s);
   return check_launch("gat_alpha");
 }
 
 extern "C" int vqgnn_gat_coef(const int32_t* rowptr, const int32_t* col, const float* val,
-                              int32_t n_rows, int64_t nnz, const float* alpha_l,
-                              const float* alpha_r, const float* params, float negative_slope,
-                              float* coef, float* den, vqgnn_stream_t stream) {
+                              int32_t n_rows, int64_t nnz, const float* alpha_l_s,
+                              const float* alpha_r_s, float negative_slope, float* coef,
+                              float* den, vqgnn_stream_t stream) {
   clear_error();
   VQGNN_REQUIRE(n_rows >= 0 && nnz >= 0 && nnz < (int64_t)INT32_MAX, "gat_coef: bad shape");
   if (n_rows == 0) return VQGNN_OK;
-  VQGNN_REQUIRE(rowptr && alpha_l && alpha_r && params && den && (nnz == 0 || (col && val && coef)),
+  VQGNN_REQUIRE(rowptr && alpha_l_s && alpha_r_s && den && (nnz == 0 || (col && val && coef)),
                 "gat_coef: null pointer");
   const int wpb = kGatThreads / 64;
   hipLaunchKernelGGL(gat_coef_kernel, dim3((n_rows + wpb - 1) / wpb), dim3(kGatThreads), 0,
-                     as_stream(stream), rowptr, col, val, n_rows, alpha_l, alpha_r, params,
+                     as_stream(stream), rowptr, col, val, n_rows, alpha_l_s, alpha_r_s,
                      negative_slope, coef, den);
   return check_launch("gat_coef");
 }
@@ -515,14 +535,14 @@ extern "C" int vqgnn_gat_normalize(float* out, int64_t ldo, int32_t B, int32_t F
 extern "C" int vqgnn_gat_edge_grad(const int32_t* rows, const int32_t* col, const float* coef,
                                    int64_t nnz, const float* X, int64_t ldx, const float* X2,
                                    int64_t ldx2, int32_t B, int32_t F, const float* dy,
-                                   int64_t lddy, const float* dden, const float* alpha_l,
-                                   const float* alpha_r, const float* params,
+                                   int64_t lddy, const float* dden, const float* alpha_l_s,
+                                   const float* alpha_r_s, const float* params,
                                    float negative_slope, float* dalpha_l, float* dalpha_r,
                                    float* ds_row, vqgnn_stream_t stream) {
   clear_error();
   VQGNN_REQUIRE(nnz >= 0 && nnz < (int64_t)INT32_MAX && F > 0, "gat_edge_grad: bad shape");
   if (nnz == 0) return VQGNN_OK;
-  VQGNN_REQUIRE(rows && col && coef && X && dy && alpha_l && alpha_r && params && dalpha_l &&
+  VQGNN_REQUIRE(rows && col && coef && X && dy && alpha_l_s && alpha_r_s && params && dalpha_l &&
                     dalpha_r && ds_row,
                 "gat_edge_grad: null pointer");
   VQGNN_REQUIRE((F & 3) != 0 || ((((uintptr_t)X | (uintptr_t)dy | (uintptr_t)X2) & 15) == 0 &&
@@ -538,7 +558,7 @@ extern "C" int vqgnn_gat_edge_grad(const int32_t* rows, const int32_t* col, cons
     const int P = (F / 4 + 15) / 16;
     auto go = [&](auto kern) {
       hipLaunchKernelGGL(kern, grid, dim3(kGatThreads), 0, as_stream(stream), rows, col, coef, n,
-                         X, ldx, X2, ldx2, B, F, dy, lddy, dden, alpha_l, alpha_r, params,
+                         X, ldx, X2, ldx2, B, F, dy, lddy, dden, alpha_l_s, alpha_r_s, params,
                          negative_slope, dalpha_l, dalpha_r, ds_row);
     };
     if (P <= 1) go(gat_edge_grad_grp_kernel<1>);
@@ -548,7 +568,7 @@ extern "C" int vqgnn_gat_edge_grad(const int32_t* rows, const int32_t* col, cons
   } else {
     hipLaunchKernelGGL(gat_edge_grad_kernel, dim3((n + kGatThreads - 1) / kGatThreads),
                        dim3(kGatThreads), 0, as_stream(stream), rows, col, coef, n, X, ldx, X2,
-                       ldx2, B, F, dy, lddy, dden, alpha_l, alpha_r, params, negative_slope,
+                       ldx2, B, F, dy, lddy, dden, alpha_l_s, alpha_r_s, params, negative_slope,
                        dalpha_l, dalpha_r, ds_row);
   }
   return check_launch("gat_edge_grad");

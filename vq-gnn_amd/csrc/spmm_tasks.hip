@@ -66,12 +66,11 @@ struct TaskArgs {
   uint32_t ldob;            // near path: ldo in bytes (rows addressed with a 24-bit multiply)
   int dbg;                  // experiments: 1 = no row stores (results invalid)
   // GAT mode (OurGATConv + the layer's ones-column normalisation): edge
-  // weight = exp(leaky(al[j]/s + ar[i]/s)) * w, rows < norm_B divided by
-  // their coefficient sum + 1e-16
+  // weight = exp(leaky(al[j] + ar[i])) * w with al, ar = alpha / s per node,
+  // rows < norm_B divided by their coefficient sum + 1e-16
   const int32_t* erow;      // [nnz] COO row of every edge
-  const float* al;          // [n] alpha_l, alpha_r of x_in rows
+  const float* al;          // [n] alpha_l / s, alpha_r / s of x_in rows
   const float* ar;
-  const float* params;      // params[2] = s
   float slope;
   int norm_B;
   float* den;               // [n_rows] optional: coefficient sums
@@ -183,10 +182,10 @@ __device__ __forceinline__ void group_bcast(int x, int (&out)[sizeof...(Us)],
 // i of lane k is float4 column G*i + k: a column tile of 4*G*NC floats), U
 // edges per block
 // GAT coefficient of one edge (convs.py:209-264, vq_softmax.py:33-57, the
-// op order of gat_coef_kernel): exp(leaky(al[j]/s + ar[i]/s)) * w
+// op order of gat_coef_kernel): exp(leaky(al[j] + ar[i])) * w, al / ar
+// already divided by s per node as the reference does (convs.py:209-211)
 __device__ __forceinline__ float gat_edge_coef(const TaskArgs& a, int e, uint32_t j, float w) {
-  const float s = a.params[2];
-  float x = __fadd_rn(__fdiv_rn(a.al[j], s), __fdiv_rn(a.ar[a.erow[e]], s));
+  float x = __fadd_rn(a.al[j], a.ar[a.erow[e]]);
   x = x > 0.f ? x : __fmul_rn(x, a.slope);
   return __fmul_rn(expf(x), w);
 }
@@ -374,7 +373,6 @@ __device__ __forceinline__ void task_walk(const TaskArgs& a, int wv, int nwaves)
     // (1 + empty rows skipped) of the earlier edges (DPP within the 16-lane
     // record row), not from an erow load; a block holding a skip escape (31
     // or more empty rows in a row) reads erow for it and for the next block.
-    const float s = a.params[2];
     int rb = r;            // group's row at the next prepared block's first edge
     bool known = true;     // rb is exact
     auto prep = [&](int2 q, int eb, float& alv, float& arv) {
@@ -407,7 +405,7 @@ __device__ __forceinline__ void task_walk(const TaskArgs& a, int wv, int nwaves)
     auto coef = [&](int2 q, int eb, float alv, float arv) -> int2 {
       const int eu = eb + k;
       if (!(k < U && eu >= e0 && eu < e1)) return make_int2(0, 0);
-      float z = __fadd_rn(__fdiv_rn(alv, s), __fdiv_rn(arv, s));
+      float z = __fadd_rn(alv, arv);        // alpha / s per node (convs.py:209-211, :256)
       z = z > 0.f ? z : __fmul_rn(z, a.slope);
       const float c = __fmul_rn(expf(z), __int_as_float(q.y));
       if (a.coef && blockIdx.y == 0) a.coef[eu] = c;
@@ -513,7 +511,9 @@ spmm_task_fixup_kernel(TaskArgs a) {
       d = __fadd_rn(d, a.carry[(int64_t)t * 2 * a.cf + a.F]);
       if (a.den && lane == 0) a.den[r] = d;
       norm = r < a.norm_B;
-      q = __fadd_rn(d, 1e-16f);
+      // the walker's normalisation (one v_rcp_f32, then multiplies), so a row
+      // gets the same bits whether or not the plan cuts it across tasks
+      q = __builtin_amdgcn_rcpf(__fadd_rn(d, 1e-16f));
     }
     for (int c = lane; c < ncol; c += L) {
       if (GAT && c == F4) continue;
@@ -529,10 +529,10 @@ spmm_task_fixup_kernel(TaskArgs a) {
       for (; u < t; ++u) sum = add4(sum, c4[((int64_t)u * 2 + 1) * C4 + c]);
       sum = add4(sum, c4[(int64_t)t * 2 * C4 + c]);
       if (norm) {
-        sum.x = __fdiv_rn(sum.x, q);
-        sum.y = __fdiv_rn(sum.y, q);
-        sum.z = __fdiv_rn(sum.z, q);
-        sum.w = __fdiv_rn(sum.w, q);
+        sum.x = __fmul_rn(sum.x, q);
+        sum.y = __fmul_rn(sum.y, q);
+        sum.z = __fmul_rn(sum.z, q);
+        sum.w = __fmul_rn(sum.w, q);
       }
       reinterpret_cast<float4*>(a.out + (int64_t)r * a.ldo)[c] = sum;
     }
@@ -782,9 +782,8 @@ extern "C" int vqgnn_gat_spmm_task(const int32_t* rowptr, int32_t n_rows, int32_
                                    const float* X2, int64_t ldx2, int32_t F, float* out,
                                    int64_t ldo, const int32_t* plan, const int64_t* records,
                                    int32_t K, int32_t n_jobs, int32_t n_empty,
-                                   const int32_t* erow, const float* alpha_l,
-                                   const float* alpha_r, const float* params,
-                                   float negative_slope, int32_t norm_B, float* den, float* coef,
+                                   const int32_t* erow, const float* alpha_l_s,
+                                   const float* alpha_r_s, float negative_slope, int32_t norm_B, float* den, float* coef,
                                    void* workspace, vqgnn_stream_t stream) {
   clear_error();
   TaskArgs a{};
@@ -792,12 +791,11 @@ extern "C" int vqgnn_gat_spmm_task(const int32_t* rowptr, int32_t n_rows, int32_
   const int rc = task_setup(a, rowptr, n_rows, n_cols, nnz, B, X, ldx, X2, ldx2, F, out, ldo,
                             plan, records, K, n_jobs, n_empty, workspace, &near);
   if (rc != VQGNN_OK) return rc;
-  VQGNN_REQUIRE(nnz == 0 || (erow && alpha_l && alpha_r && params), "gat_spmm_task: null pointer");
+  VQGNN_REQUIRE(nnz == 0 || (erow && alpha_l_s && alpha_r_s), "gat_spmm_task: null pointer");
   VQGNN_REQUIRE(norm_B >= 0, "gat_spmm_task: norm_B=%d", norm_B);
   a.erow = erow;
-  a.al = alpha_l;
-  a.ar = alpha_r;
-  a.params = params;
+  a.al = alpha_l_s;
+  a.ar = alpha_r_s;
   a.slope = negative_slope;
   a.norm_B = norm_B;
   a.den = den;

@@ -67,10 +67,18 @@ class CodebookSync:
         BatchNorm all-reduce, in order), B on one side stream (the EMA
         all-reduce and the code all-gather, overlapping the caller's work).
         Rank 0's unique ids travel over the gloo count group."""
+        import weakref
+
         from . import rccl
-        ids = [rccl.unique_id(), rccl.unique_id()] if dist.get_rank(self.group) == 0 else None
+        bgroup = self.count_group or self.group
+        if dist.get_world_size(bgroup) != self.world:
+            raise ValueError("CodebookSync: count_group must span the ranks of group")
+        # broadcast_object_list takes a GLOBAL source rank: the global rank of
+        # the broadcast group's rank 0, which creates the ids
+        src = dist.get_global_rank(bgroup, 0) if bgroup is not None else 0
+        ids = [rccl.unique_id(), rccl.unique_id()] if dist.get_rank(bgroup) == 0 else None
         box = [ids]
-        dist.broadcast_object_list(box, src=0, group=self.count_group or self.group)
+        dist.broadcast_object_list(box, src=src, group=bgroup)
         rank = dist.get_rank(self.group)
         self._ca = rccl.Communicator(self.world, rank, box[0][0])
         self._cb = rccl.Communicator(self.world, rank, box[0][1])
@@ -80,15 +88,20 @@ class CodebookSync:
         # most 2 exchanges + 2 all-reduces are in flight at once)
         self._events = [torch.cuda.Event() for _ in range(16)]
         self._ev_i = 0
-        import atexit
-        atexit.register(self._destroy_direct)
+        # no strong reference from an exit hook: a dropped CodebookSync frees
+        # its communicators and side stream at once
+        self._finalizer = weakref.finalize(self, _release_comms, self._ca, self._cb)
 
-    def _destroy_direct(self):
-        if getattr(self, "_ca", None) is not None:
+    def close(self):
+        """Destroy the direct communicators after this rank's work drained
+        (call on every rank at a clean shutdown).  Without it they are
+        released when the object is collected or at exit -- by ncclCommAbort
+        when the process exits on an uncaught exception, so a rank whose
+        peer died mid-collective exits instead of hanging in a destroy."""
+        if getattr(self, "_finalizer", None) is not None and self._finalizer.alive:
             torch.cuda.synchronize()
-            self._ca.destroy()
-            self._cb.destroy()
-            self._ca = self._cb = None
+            self._finalizer()
+        self._ca = self._cb = None
 
     def _on_side(self, launch):
         """Run ``launch(side_stream)`` after the current stream's work so far;
@@ -280,6 +293,18 @@ class PendingWire:
             self.work = None
             kernels.scatter_wire(self.recv, self.n, self.nb, self.M, self.winner, self.codes,
                                  self.epoch)
+
+
+def _release_comms(ca, cb):
+    """Finalizer of CodebookSync's direct communicators.  An uncaught
+    exception (sys.last_type set by the interpreter's error print) may have
+    left a collective waiting for a peer that will never come: abort them.
+    Otherwise destroy them (the collectives have completed or will)."""
+    import sys
+    failing = getattr(sys, "last_type", None) is not None
+    for c in (ca, cb):
+        if c is not None:
+            c.abort() if failing else c.destroy()
 
 
 def _device_of(group):

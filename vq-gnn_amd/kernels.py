@@ -353,37 +353,42 @@ def csr_expand_rows(rowptr, n_rows, nnz):
 # ---- GAT (include/vqgnn.h §8) ----
 
 def gat_alpha(X, att_l, att_r, F, X2=None, B=None, ones=True):
-    """alpha_l, alpha_r [n] and params [5] = (max_l, max_r, s, ds/dmax_l, ds/dmax_r)."""
+    """-> (alpha_l, alpha_r [n], params [5] = (max_l, max_r, s, ds/dmax_l,
+    ds/dmax_r), alpha_l / s, alpha_r / s [n]).  The scaled scalars are what
+    every per-edge consumer reads (convs.py:209-211 divides once per node)."""
     require_gpu(X, "gat_alpha")
     dev = X.device
     Bv = int(B) if X2 is not None else X.shape[0]
     n = Bv + (X2.shape[0] if X2 is not None else 0)
     al = torch.empty(n, dtype=torch.float32, device=dev)
     ar = torch.empty(n, dtype=torch.float32, device=dev)
+    als = torch.empty(n, dtype=torch.float32, device=dev)
+    ars = torch.empty(n, dtype=torch.float32, device=dev)
     params = torch.empty(5, dtype=torch.float32, device=dev)
     L = lib()
     ws = workspace(L.vqgnn_gat_alpha_workspace(n), dev)
     check(L.vqgnn_gat_alpha(ptr(X), _ld(X), ptr(X2), _ld(X2) if X2 is not None else 0, Bv, n,
                             int(F), int(bool(ones)), ptr(att_l), ptr(att_r), ptr(al), ptr(ar),
-                            ptr(params), ptr(ws), stream_ptr()), "gat_alpha")
-    return al, ar, params
+                            ptr(als), ptr(ars), ptr(params), ptr(ws), stream_ptr()), "gat_alpha")
+    return al, ar, params, als, ars
 
 
-def gat_coef(rowptr, col, val, n_rows, nnz, al, ar, params, negative_slope=0.2):
-    """-> (coef [nnz], den [n_rows])."""
-    dev = al.device
+def gat_coef(rowptr, col, val, n_rows, nnz, als, ars, negative_slope=0.2):
+    """als, ars: alpha / s per node (gat_alpha) -> (coef [nnz], den [n_rows])."""
+    dev = als.device
     coef = torch.empty(max(nnz, 1), dtype=torch.float32, device=dev)
     den = torch.empty(n_rows, dtype=torch.float32, device=dev)
-    check(lib().vqgnn_gat_coef(ptr(rowptr), ptr(col), ptr(val), int(n_rows), int(nnz), ptr(al),
-                               ptr(ar), ptr(params), float(negative_slope), ptr(coef), ptr(den),
+    check(lib().vqgnn_gat_coef(ptr(rowptr), ptr(col), ptr(val), int(n_rows), int(nnz), ptr(als),
+                               ptr(ars), float(negative_slope), ptr(coef), ptr(den),
                                stream_ptr()), "gat_coef")
     return coef[:nnz], den
 
 
-def gat_spmm(rowptr, col, val, n_rows, nnz, X, F, al, ar, params, plan, erow, X2=None,
+def gat_spmm(rowptr, col, val, n_rows, nnz, X, F, als, ars, plan, erow, X2=None,
              B=None, norm_B=0, negative_slope=0.2, want_den=False, want_coef=False, out=None):
     """Fused GAT aggregation (include/vqgnn.h §8b) on a task plan built from
-    this CSR's values: coefficients in the kernel, the ones column as the
+    this CSR's values (als, ars: alpha / s per node from gat_alpha):
+    coefficients in the kernel, the ones column as the
     per-row sum, rows < norm_B normalised.  -> (out [n_rows, F], den or None,
     coef [nnz] (CSR order) or None)."""
     require_gpu(X, "gat_spmm")
@@ -403,8 +408,8 @@ def gat_spmm(rowptr, col, val, n_rows, nnz, X, F, al, ar, params, plan, erow, X2
     check(L.vqgnn_gat_spmm_task(ptr(rowptr), int(n_rows), int(n_cols), int(nnz), Bv, ptr(X),
                                 _ld(X), ptr(X2), _ld(X2) if X2 is not None else 0, F, ptr(out),
                                 _ld(out), ptr(plan.plan), ptr(plan.records), plan.K,
-                                plan.n_jobs, plan.n_empty, ptr(erow), ptr(al), ptr(ar),
-                                ptr(params), float(negative_slope), int(norm_B), ptr(den),
+                                plan.n_jobs, plan.n_empty, ptr(erow), ptr(als), ptr(ars),
+                                float(negative_slope), int(norm_B), ptr(den),
                                 ptr(coef), ptr(ws), stream_ptr()), "gat_spmm")
     return out, (den[:n_rows] if den is not None else None), \
         (coef[:nnz] if coef is not None else None)
@@ -415,18 +420,19 @@ def gat_normalize(out, B, F, den, eps=1e-16):
                                     stream_ptr()), "gat_normalize")
 
 
-def gat_edge_grad(rows, col, coef, nnz, X, F, dy, dden, al, ar, params, X2=None, B=None,
+def gat_edge_grad(rows, col, coef, nnz, X, F, dy, dden, als, ars, params, X2=None, B=None,
                   negative_slope=0.2):
-    """-> (dalpha_l [n], dalpha_r [n], ds_row [n]) for the coefficient chain."""
+    """-> (dalpha_l [n], dalpha_r [n], ds_row [n]) for the coefficient chain
+    (als, ars: alpha / s per node; params[2] = s)."""
     dev = X.device
-    n = al.shape[0]
+    n = als.shape[0]
     dal = torch.zeros(n, dtype=torch.float32, device=dev)
     dar = torch.zeros(n, dtype=torch.float32, device=dev)
     dsr = torch.zeros(n, dtype=torch.float32, device=dev)
     Bv = int(B) if X2 is not None else X.shape[0]
     check(lib().vqgnn_gat_edge_grad(ptr(rows), ptr(col), ptr(coef), int(nnz), ptr(X), _ld(X),
                                     ptr(X2), _ld(X2) if X2 is not None else 0, Bv, int(F),
-                                    ptr(dy), _ld(dy), ptr(dden), ptr(al), ptr(ar), ptr(params),
+                                    ptr(dy), _ld(dy), ptr(dden), ptr(als), ptr(ars), ptr(params),
                                     float(negative_slope), ptr(dal), ptr(dar), ptr(dsr),
                                     stream_ptr()), "gat_edge_grad")
     return dal, dar, dsr

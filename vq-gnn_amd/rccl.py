@@ -52,10 +52,11 @@ def _lib():
         L.ncclAllReduce.argtypes = [vp, vp, sz, i, i, vp, vp]
         L.ncclAllGather.argtypes = [vp, vp, sz, i, vp, vp]
         L.ncclCommDestroy.argtypes = [vp]
+        L.ncclCommAbort.argtypes = [vp]
         L.ncclGetErrorString.argtypes = [i]
         L.ncclGetErrorString.restype = ctypes.c_char_p
         for f in ("ncclGetUniqueId", "ncclCommInitRank", "ncclAllReduce", "ncclAllGather",
-                  "ncclCommDestroy"):
+                  "ncclCommDestroy", "ncclCommAbort"):
             getattr(L, f).restype = i
         _LIB = L
     return _LIB
@@ -113,8 +114,17 @@ class Communicator:
                "ncclAllGather")
 
     def destroy(self):
+        """ncclCommDestroy: waits for this communicator's outstanding
+        collectives (a clean shutdown)."""
         if self.comm:
             _lib().ncclCommDestroy(self.comm)
+            self.comm = ctypes.c_void_p()
+
+    def abort(self):
+        """ncclCommAbort: frees the communicator without waiting for its
+        outstanding collectives (an error exit whose peers may be gone)."""
+        if self.comm:
+            _lib().ncclCommAbort(self.comm)
             self.comm = ctypes.c_void_p()
 
 

@@ -189,6 +189,35 @@ class VQBank(nn.Module):
         self.assign_events.append(ev)
         return out
 
+    def _assign_capped(self, X, G, coef, scale, emb, W, idx_out, codes, batch_idx, training,
+                       count, slab, cap):
+        """The assign.  A multi-GPU batch over the CodebookSync capacity (an
+        error every rank raises together at the next check) takes its EMA
+        statistics from its first ``cap`` rows only: the summed rows then
+        never exceed the fixed-point row bound world * capacity (no
+        saturation, no corrupted codebook), and no rank raises on its own
+        between two collectives (the others would wait forever).  Its other
+        rows are still assigned (indices and codes)."""
+        D = self.D
+        B = X.shape[0]
+        if cap is None or B <= cap or not training:
+            return self._assign(X, G, coef, scale, emb, D, W, idx_out=idx_out, codes=codes,
+                                batch_idx=batch_idx, want_stats=training, stat_count=count,
+                                stats_out=slab)
+        parts = []
+        for lo, hi, stats in ((0, cap, True), (cap, B, False)):
+            io = None if idx_out is None else torch.empty(idx_out.shape[0], hi - lo,
+                                                          dtype=idx_out.dtype, device=X.device)
+            st = self._assign(X[lo:hi], None if G is None else G[lo:hi], coef, scale, emb, D, W,
+                              idx_out=io, codes=codes,
+                              batch_idx=None if batch_idx is None else batch_idx[lo:hi],
+                              want_stats=stats, stat_count=count,
+                              stats_out=slab if stats else None)
+            if io is not None:
+                idx_out[:, lo:hi].copy_(io)
+            parts.append(st)
+        return parts[0]
+
     def _sel(self, b0, nbr):
         return slice(b0, b0 + nbr)
 
@@ -237,15 +266,14 @@ class VQBank(nn.Module):
                                           self.rm_f[sl], self.rv_f[sl], arith_x=ax_eval)
         slab = self._slab(D, b0, nbr) if training else None
         local = None
+        cap = max_B if comm is not None else None
         if comm is not None and codes is not None:
             local = self._local_codes(B, nbr, X.device)
-            stats = self._assign(X, None, coef, 1.0, self.emb[sl], D, D, idx_out=idx_out,
-                                 codes=local, batch_idx=self._arange(B, X.device),
-                                 want_stats=training, stat_count=count, stats_out=slab)
+            stats = self._assign_capped(X, None, coef, 1.0, self.emb[sl], D, idx_out, local,
+                                        self._arange(B, X.device), training, count, slab, cap)
         else:
-            stats = self._assign(X, None, coef, 1.0, self.emb[sl], D, D, idx_out=idx_out,
-                                 codes=codes, batch_idx=batch_idx, want_stats=training,
-                                 stat_count=count, stats_out=slab)
+            stats = self._assign_capped(X, None, coef, 1.0, self.emb[sl], D, idx_out, codes,
+                                        batch_idx, training, count, slab, cap)
         if comm is not None:
             stats = kernels.vq_ema_reduce(stats)
             comm.allreduce_(stats)
@@ -329,16 +357,14 @@ class VQBank(nn.Module):
         scale = float(self.grad_normalize_scale[0])
         slab = self._slab(2 * D, b0, nbr) if training else None
         local = None
+        cap = max_B if comm is not None else None
         if comm is not None and codes is not None:
             local = self._local_codes(B, nbr, X.device)
-            stats = self._assign(X, G, coef, scale, self.emb[sl], D, 2 * D,
-                                 idx_out=idx_out, codes=local,
-                                 batch_idx=self._arange(B, X.device), want_stats=training,
-                                 stat_count=count, stats_out=slab)
+            stats = self._assign_capped(X, G, coef, scale, self.emb[sl], 2 * D, idx_out, local,
+                                        self._arange(B, X.device), training, count, slab, cap)
         else:
-            stats = self._assign(X, G, coef, scale, self.emb[sl], D, 2 * D,
-                                 idx_out=idx_out, codes=codes, batch_idx=batch_idx,
-                                 want_stats=training, stat_count=count, stats_out=slab)
+            stats = self._assign_capped(X, G, coef, scale, self.emb[sl], 2 * D, idx_out, codes,
+                                        batch_idx, training, count, slab, cap)
         work = None
         if comm is not None:
             stats = kernels.vq_ema_reduce(stats)
