@@ -7,7 +7,10 @@ workload shape:
   and layer 2 at F = 256 (nb = 64), D^-1 A weights (utils/misc.py:21-25) and
   the host fc_sage (models.py:203-204);
 - arxiv GAT (configs[4], convs.py:165-266, models.py:176-189): the full
-  84,670-row arxiv batch, M = 1,024, C = F + 1 = 129.
+  84,670-row arxiv batch, M = 1,024, C = F + 1 = 129;
+- arxiv GCN, the headline (configs[1]): M = 256, the full batch, through
+  bench.py's own update sequence (feature_update warm-up, update(defer=True)
+  + finish_update(), feature_update, and dead codewords).
 
 Bounds: codeword indices and BatchNorm state bit-exact against the oracle
 (vq_ref, pinned to the reference's vq.py by the golden fixtures) on a spread
@@ -160,10 +163,6 @@ def test_arxiv_gcn_headline_vq_vs_oracle(arxiv_gcn):
     bank.feature_update(Xd, 0, nb, True, idx_out=idx, codes=codes, batch_idx=bidx)
     _compare_branches(idx, codes, bidx, states, sample,
                       lambda st, br: vq_ref.feature_update(st, cols(X, br)), bank, "warm-up W=4")
-    # the warm codebook holds dead codewords (|e|^2 >= 2^15: scored +inf by
-    # the filter) -- the range path the update must take
-    assert int((bank.emb[:, :, :D].pow(2).sum(-1) >= 2 ** 15).sum()) > 0
-
     bank.update(Xd, Gd, 0, nb, True, idx_out=idx, codes=codes, batch_idx=bidx, defer=True)
     kernels.gather_codewords(subset, B, codes, bank.emb_out, D)   # queued as in the bench step
     bank.finish_update()
@@ -175,6 +174,21 @@ def test_arxiv_gcn_headline_vq_vs_oracle(arxiv_gcn):
     _compare_branches(idx, codes, bidx, states, sample,
                       lambda st, br: vq_ref.feature_update(st, cols(X, br)), bank,
                       "warm feature_update W=4")
+
+    # dead codewords (a trained codebook's unused ones reach |e|^2 ~ 1e10:
+    # scored +inf by the filter, the range path of DESIGN.md §4.1), injected
+    # alike into the bank and the oracle states, then the bench step again
+    dead = torch.arange(3, M, 17)
+    for st, br in zip(states, sample):
+        st["embedding"][dead] *= 1e5
+    bank.emb[:, dead] *= 1e5
+    assert int((bank.emb[:, :, :D].pow(2).sum(-1) >= 2 ** 15).sum()) >= nb * dead.numel()
+    bank.update(Xd, Gd, 0, nb, True, idx_out=idx, codes=codes, batch_idx=bidx, defer=True)
+    kernels.gather_codewords(subset, B, codes, bank.emb_out, D)
+    bank.finish_update()
+    _compare_branches(idx, codes, bidx, states, sample,
+                      lambda st, br: vq_ref.update(st, cols(X, br), cols(G, br))[0], bank,
+                      "update W=8, dead codewords")
 
 
 def _sampled_rows(rowptr, n_rows, k, seed, longest=16):
