@@ -30,6 +30,7 @@
 
 #include "common.h"
 
+#include <type_traits>
 #include <utility>
 
 namespace vqgnn {
@@ -608,9 +609,8 @@ static void launch_task_u(const TaskArgs& a, int tiles, int U, bool near, hipStr
 // Hot records: the task records with bits 0-24 = source column, or (bit 25
 // set) the row's LDS slot; bits 26-31 as above (skip count, row end).
 
-constexpr int kHotThreads = 1024;             // 16 waves: one workgroup per CU (LDS)
-constexpr int kHotSlice4 = 8;                 // float4 per slice row: 8 lanes x 16 B
-constexpr int kHotMaxC = 1024;                // LDS rows: 1024 x 128 B = 128 KiB
+constexpr int kHotLdsBytes = 128 * 1024;      // staged hot slices per workgroup (at most)
+constexpr int kHotMaxC = 1024;                // hot rows per tile (128-byte slices)
 constexpr uint32_t kLocalBit = 1u << 25;
 constexpr uint32_t kHotColMask = (1u << 25) - 1;
 constexpr int kHotTab = 24576;                // plan hash table (keys 96 KiB + u16 counts 48 KiB)
@@ -698,8 +698,25 @@ hot_scan_kernel(const int32_t* __restrict__ rowptr, int T, int K, int C, int Et,
   }
 }
 
-// tasks inside each tile: nominal starts every K edges from the tile's first
-// edge, snapped past rows of at most K/2 edges (as task_first_row_kernel)
+// start of task kk (of ntask) of a tile [te0, te1): nominal starts every K
+// edges from the tile's first edge, snapped past rows of at most K/2 edges
+// (as task_first_row_kernel); kk == ntask: the tile's end
+__device__ __forceinline__ int hot_task_start(const int32_t* __restrict__ rowptr, int n_rows,
+                                              int K, int te0, int te1, int kk, int ntask) {
+  if (kk >= ntask) return te1;
+  int st = te0 + kk * K;
+  if (kk > 0) {
+    const int r = upper_bound_i32(rowptr, n_rows, st) - 1;
+    const int rs = rowptr[r], re = rowptr[r + 1];
+    if (rs < st && re - rs <= K / 2) st = re;
+  }
+  return st;
+}
+
+// task x: its first edge, and its first row with two flags: bit 31 "head"
+// (the row began in an earlier task), bit 30 "open" (the task's last row
+// continues in the next task) -- so the SpMM reads no rowptr per task
+constexpr uint32_t kHeadBit = 1u << 31, kOpenBit = 1u << 30, kRowMask = (1u << 30) - 1;
 __global__ void hot_tasks_kernel(const int32_t* __restrict__ rowptr, int n_rows, int nnz, int K,
                                  int T, const int32_t* __restrict__ tile_row,
                                  const int32_t* __restrict__ tile_task,
@@ -714,15 +731,19 @@ __global__ void hot_tasks_kernel(const int32_t* __restrict__ rowptr, int n_rows,
   }
   const int t = upper_bound_i32(tile_task, T, x) - 1;
   const int kk = x - tile_task[t];
-  const int te1 = rowptr[tile_row[t + 1]];
-  int st = rowptr[tile_row[t]] + kk * K;
-  if (kk > 0) {
-    const int r = upper_bound_i32(rowptr, n_rows, st) - 1;
-    const int rs = rowptr[r], re = rowptr[r + 1];
-    if (rs < st && re - rs <= K / 2) st = re;
-  }
+  const int ntask = tile_task[t + 1] - tile_task[t];
+  const int te0 = rowptr[tile_row[t]], te1 = rowptr[tile_row[t + 1]];
+  const int st = hot_task_start(rowptr, n_rows, K, te0, te1, kk, ntask);
+  const int en = hot_task_start(rowptr, n_rows, K, te0, te1, kk + 1, ntask);
   task_start[x] = st;
-  task_row[x] = st < te1 ? upper_bound_i32(rowptr, n_rows, st) - 1 : tile_row[t + 1] - 1;
+  uint32_t row = (uint32_t)(tile_row[t + 1] - 1), flags = 0;
+  if (st < en) {
+    row = (uint32_t)(upper_bound_i32(rowptr, n_rows, st) - 1);
+    if (rowptr[row] < st) flags |= kHeadBit;
+    const int rl = upper_bound_i32(rowptr, n_rows, en - 1) - 1;   // the row of the last edge
+    if (rowptr[rl + 1] > en) flags |= kOpenBit;
+  }
+  task_row[x] = (int)(row | flags);
 }
 
 __device__ __forceinline__ int hot_hash(int c) {
@@ -885,7 +906,7 @@ struct HotArgs {
   int cf;
   const char* ubase;
   uint32_t span, offx, ldxb, offx2, ldx2b, ldob;
-  int dbg;    // experiments (VQGNN_HOT_DBG): 1 no cut-row sums, 2 no stores, 4 all edges global
+  int dbg;    // experiments (VQGNN_HOT_DBG): 1 no fix-up kernel, 2 no stores, 4 all edges global
 };
 
 // Byte offset (near) / address (far) of source row j's slice piece.
@@ -895,11 +916,16 @@ __device__ __forceinline__ const char* hot_far_row(const HotArgs& a, int j) {
   return reinterpret_cast<const char*>(row);
 }
 
-template <bool FAR, bool PART>
-__global__ void __launch_bounds__(kHotThreads) __attribute__((amdgpu_waves_per_eu(4)))
+// G lanes per task, one float4 each: a column slice of 4G floats (G = 32:
+// 512-byte slices, two tasks per wave as the task kernel walks them; G = 8:
+// 128-byte slices, eight tasks per wave).  NW waves per workgroup: 16 (one
+// workgroup per CU) or 8 (two per CU: one's staging overlaps the other's walk).
+template <int G, bool FAR, bool PART, int NW>
+__global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4)))
 spmm_hot_kernel(HotArgs a) {
-  __shared__ float4 lds[kHotMaxC * kHotSlice4];
-  constexpr int G = kHotSlice4, U = 16;
+  extern __shared__ float4 lds[];                    // [C][G] float4
+  constexpr int U = 16, NT = NW * 64;
+  constexpr int TPW = 64 / G;                        // tasks per wave and round
   const int L = xcd_remap(blockIdx.x, gridDim.x);   // a tile's slices: one XCD, consecutive
   const int t = L / a.S, sl = L - t * a.S;
   const int r0 = a.tile_row[t];
@@ -908,7 +934,7 @@ spmm_hot_kernel(HotArgs a) {
   const int nlim = a.rowptr[r1];                     // edges of the rows computed here
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int g = lane >> 3, k = lane & 7;
+  const int g = lane / G, k = lane % G;
   const int F4 = a.F >> 2;
   const int c4 = sl * G + k;                         // this lane's float4 column
   const bool pv = c4 < F4;
@@ -917,14 +943,33 @@ spmm_hot_kernel(HotArgs a) {
   const __amdgpu_buffer_rsrc_t rsx =
       __builtin_amdgcn_make_buffer_rsrc((void*)a.ubase, 0, FAR ? 0 : (int)a.span, 0x00020000);
 
-  // 1. stage the tile's hot rows (this slice) in LDS: 8 lanes per row
+  // this wave's first round of tasks: its metadata is issued before the
+  // staging, so the two latencies overlap; every later round's metadata is
+  // issued one round ahead
+  const int x0 = a.tile_task[t], x1 = a.tile_task[t + 1];
+  struct Meta { int ws, s0, s1, tr; };
+  auto meta = [&](int xbb) {
+    Meta m{0, 0, 0, 0};
+    const int x = xbb + g;
+    if (xbb < x1) m.ws = a.task_start[xbb];
+    if (x < x1) {
+      m.s0 = a.task_start[x];
+      m.s1 = a.task_start[x + 1];
+      m.tr = a.task_row[x];
+    }
+    return m;
+  };
+  int xb = x0 + wv * TPW;
+  Meta cur = meta(xb);
+
+  // 1. stage the tile's hot rows (this slice) in LDS: G lanes per row
   const int nh = min(a.hot_n[t], a.C);
   const int32_t* hot = a.hot + (int64_t)t * a.C;
-  for (int s0 = tid >> 3; s0 < nh; s0 += 8 * (kHotThreads / G)) {
+  for (int s0 = tid / G; s0 < nh; s0 += 8 * (NT / G)) {
     float4 v[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const int s = s0 + i * (kHotThreads / G);
+      const int s = s0 + i * (NT / G);
       v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
       if (s < nh && pv) {
         const int j = hot[s];
@@ -940,25 +985,32 @@ spmm_hot_kernel(HotArgs a) {
     }
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const int s = s0 + i * (kHotThreads / G);
+      const int s = s0 + i * (NT / G);
       if (s < nh) lds[s * G + k] = v[i];
     }
   }
   __syncthreads();
 
-  // 2. the tile's tasks: a wave takes 8 consecutive tasks per round
-  const int x0 = a.tile_task[t], x1 = a.tile_task[t + 1];
+  // 2. the tile's tasks: a wave takes TPW consecutive tasks per round; the
+  //    rows cut across tasks are summed by spmm_hot_fixup_kernel
   constexpr int kAnd = 0x1F & ~(G - 1);
   const char* ldsb = reinterpret_cast<const char*>(lds);
-  for (int xb = x0 + wv * (64 / G); xb < x1; xb += (kHotThreads / 64) * (64 / G)) {
+  int2 pq0 = make_int2(0, 0), pq1 = make_int2(0, 0);   // next round's first records, loaded
+  bool pre = false;                                    // during this round's last block
+  for (; xb < x1; xb += NW * TPW) {
+    const Meta nxt = meta(xb + NW * TPW);            // next round's metadata in flight
     const int x = xb + g;
     const bool tv = x < x1;
-    const int wbase = min(a.task_start[xb], nlim);
-    const int e0 = tv ? min(a.task_start[x], nlim) : nlim;
-    const int e1 = tv ? min(a.task_start[x + 1], nlim) : e0;
+    const int wbase = __builtin_amdgcn_readfirstlane(min(cur.ws, nlim));
+    const int e0 = tv ? min(cur.s0, nlim) : nlim;
+    const int e1 = tv ? min(cur.s1, nlim) : e0;
     const bool valid = e0 < e1;
-    int r = valid ? a.task_row[x] : 0;
-    bool head = valid && a.rowptr[r] < e0;
+    const uint32_t trw = (uint32_t)cur.tr;
+    int r = (int)(trw & kRowMask);
+    bool head = valid && (trw & kHeadBit);
+    // a task clipped at the caller's last row ends at a row end
+    const bool open = valid && (trw & kOpenBit) && cur.s1 <= nlim;
+    cur = nxt;
     const __amdgpu_buffer_rsrc_t rsr = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(a.rec + wbase), 0,
         (int)(uint32_t)min((int64_t)(a.nnz - wbase) * 8, (int64_t)0x7FFFFFFF), 0x00020000);
@@ -967,63 +1019,86 @@ spmm_hot_kernel(HotArgs a) {
 #pragma unroll
     for (int o = G; o < 64; o <<= 1) len = max(len, __shfl_xor(len, o));
     const int nblk = __builtin_amdgcn_readfirstlane((len + U - 1) / U);
-    // lane k of a group holds the records of edges e + k and e + 8 + k
+    // lane k of a group holds the record of edge e + k (and, when a block
+    // holds more edges than the group has lanes, of edge e + G + k)
     auto load_rec = [&](int e, int2& q0, int2& q1) {
       q0 = __builtin_bit_cast(int2, __builtin_amdgcn_raw_buffer_load_b64(
                                         rsr, (uint32_t)(e - wbase + k) * 8u, 0, 0));
-      q1 = __builtin_bit_cast(int2, __builtin_amdgcn_raw_buffer_load_b64(
-                                        rsr, (uint32_t)(e - wbase + G + k) * 8u, 0, 0));
+      if constexpr (G < U)
+        q1 = __builtin_bit_cast(int2, __builtin_amdgcn_raw_buffer_load_b64(
+                                          rsr, (uint32_t)(e - wbase + G + k) * 8u, 0, 0));
+      else
+        q1 = make_int2(0, 0);
     };
     int2 q0, q1;
-    load_rec(e0, q0, q1);
+    if (pre) {
+      q0 = pq0;
+      q1 = pq1;
+    } else {
+      load_rec(e0, q0, q1);
+    }
+    pre = false;
+    const int xn = xb + NW * TPW;                      // the next round (cur: its metadata)
     for (int bi = 0; bi < nblk; ++bi) {
       const int e = e0 + bi * U;
       int2 n0, n1;
-      load_rec(e + U, n0, n1);
-      const bool in0 = e + k >= e0 && e + k < e1, in1 = e + G + k >= e0 && e + G + k < e1;
+      if (bi + 1 < nblk) {
+        load_rec(e + U, n0, n1);
+      } else if (xn < x1) {
+        // the next round's first block, issued under this block's gathers
+        const int nwb = __builtin_amdgcn_readfirstlane(min(cur.ws, nlim));
+        const int ne0 = xn + g < x1 ? min(cur.s0, nlim) : nlim;
+        const __amdgpu_buffer_rsrc_t rn = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(a.rec + nwb), 0,
+            (int)(uint32_t)min((int64_t)(a.nnz - nwb) * 8, (int64_t)0x7FFFFFFF), 0x00020000);
+        pq0 = __builtin_bit_cast(int2, __builtin_amdgcn_raw_buffer_load_b64(
+                                           rn, (uint32_t)(ne0 - nwb + k) * 8u, 0, 0));
+        if constexpr (G < U)
+          pq1 = __builtin_bit_cast(int2, __builtin_amdgcn_raw_buffer_load_b64(
+                                             rn, (uint32_t)(ne0 - nwb + G + k) * 8u, 0, 0));
+        pre = true;
+      }
+      const bool in0 = k < U && e + k >= e0 && e + k < e1;
+      const bool in1 = e + G + k >= e0 && e + G + k < e1;
       int2 m0 = in0 ? q0 : make_int2(0, 0), m1 = in1 ? q1 : make_int2(0, 0);
-      // the record lane's source offset: LDS byte offset of a hot row, else
-      // the global row's byte offset (near path)
       if (a.dbg & 4) {               // experiment: every edge from memory
         m0.x &= ~(int)kLocalBit;
         m1.x &= ~(int)kLocalBit;
       }
-      auto src_off = [&](int2 m) -> int {
-        const uint32_t xw = (uint32_t)m.x;
-        if (xw & kLocalBit) return (int)((xw & kHotColMask & 0xFFFFu) * (uint32_t)(G * 16));
-        if constexpr (FAR) return 0;
-        const uint32_t j = xw & kHotColMask;
-        const bool s1 = (int)j < a.B;
-        return (int)(__umul24(j, s1 ? a.ldxb : a.ldx2b) +
-                     (s1 ? a.offx : a.offx2 - (uint32_t)a.B * a.ldx2b));
-      };
-      int cx[U], cw[U], co[U];
-      group_bcast<kAnd>(m0.x, *reinterpret_cast<int(*)[G]>(cx), std::make_integer_sequence<int, G>{});
-      group_bcast<kAnd>(m1.x, *reinterpret_cast<int(*)[G]>(cx + G), std::make_integer_sequence<int, G>{});
-      group_bcast<kAnd>(m0.y, *reinterpret_cast<int(*)[G]>(cw), std::make_integer_sequence<int, G>{});
-      group_bcast<kAnd>(m1.y, *reinterpret_cast<int(*)[G]>(cw + G), std::make_integer_sequence<int, G>{});
-      group_bcast<kAnd>(src_off(m0), *reinterpret_cast<int(*)[G]>(co), std::make_integer_sequence<int, G>{});
-      group_bcast<kAnd>(src_off(m1), *reinterpret_cast<int(*)[G]>(co + G), std::make_integer_sequence<int, G>{});
+      int cx[U], cw[U];
+      constexpr int UB = G < U ? G : U;              // edges broadcast per record register
+      group_bcast<kAnd>(m0.x, *reinterpret_cast<int(*)[UB]>(cx), std::make_integer_sequence<int, UB>{});
+      group_bcast<kAnd>(m0.y, *reinterpret_cast<int(*)[UB]>(cw), std::make_integer_sequence<int, UB>{});
+      if constexpr (G < U) {
+        group_bcast<kAnd>(m1.x, *reinterpret_cast<int(*)[UB]>(cx + G), std::make_integer_sequence<int, UB>{});
+        group_bcast<kAnd>(m1.y, *reinterpret_cast<int(*)[UB]>(cw + G), std::make_integer_sequence<int, UB>{});
+      }
       // every lane reads LDS first (a global edge reads slot 0, overwritten
       // below), then the global edges load under their exec mask: a global
-      // load only waits for the LDS read of its own register, issued 16 reads
-      // earlier, instead of a divergent branch per edge with a full LDS drain
-      // before each global load (the register WAW between the two paths)
+      // load waits only for the LDS reads ahead of it, not a full LDS drain
+      // per divergent edge (the register WAW between the two paths).  Each
+      // lane derives the source offset from the broadcast record word (LDS
+      // slot, or a 24-bit multiply-add for the global row).
       float4 v[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const bool loc = (uint32_t)cx[u] & kLocalBit;
-        v[u] = *reinterpret_cast<const float4*>(ldsb + (loc ? co[u] : 0) + k * 16);
+        const uint32_t xw = (uint32_t)cx[u];
+        const uint32_t lo = xw & kLocalBit ? (xw & 0xFFFFu) * (uint32_t)(G * 16) : 0u;
+        v[u] = *reinterpret_cast<const float4*>(ldsb + lo + k * 16);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        if (!((uint32_t)cx[u] & kLocalBit)) {
+        const uint32_t xw = (uint32_t)cx[u];
+        if (!(xw & kLocalBit)) {
           if constexpr (FAR) {
             v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
             if (pv) v[u] = *reinterpret_cast<const float4*>(
-                        hot_far_row<FAR>(a, (int)((uint32_t)cx[u] & kHotColMask)) + lane_off);
+                        hot_far_row<FAR>(a, (int)(xw & kHotColMask)) + lane_off);
           } else {
-            const uint32_t o = ((uint32_t)co[u] + lane_off) | kill;
+            const uint32_t j = xw & kHotColMask;
+            const bool s1 = (int)j < a.B;
+            const uint32_t o = (__umul24(j, s1 ? a.ldxb : a.ldx2b) +
+                                (s1 ? a.offx : a.offx2 - (uint32_t)a.B * a.ldx2b) + lane_off) | kill;
             v[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsx, o, 0, 0));
           }
         }
@@ -1049,50 +1124,59 @@ spmm_hot_kernel(HotArgs a) {
           head = false;
         }
       }
-      q0 = n0;
-      q1 = n1;
+      if (bi + 1 < nblk) {
+        q0 = n0;
+        q1 = n1;
+      }
     }
-    // the task's last row continues in the next task unless its last edge
-    // ends a row
-    const bool open = valid && !(__builtin_amdgcn_raw_buffer_load_b32(
-                                     rsr, (uint32_t)(e1 - 1 - wbase) * 8u, 0, 0) & (int)kEndBit);
     if (open && pv) *reinterpret_cast<float4*>(a.carry + ((int64_t)x * 2 + 1) * a.cf + 4 * c4) = acc;
   }
-  __syncthreads();   // the carries of every task of the tile are written
+}
 
-  // 3. cut rows that end in a task of this tile: tail[first task] + ... +
-  //    tail[last - 1] + head[last], in task order (8 lanes per row)
-  const float4* c4p = reinterpret_cast<const float4*>(a.carry);
-  const int C4 = a.cf >> 2;
-  auto add4 = [](float4 p, float4 q) {
-    return make_float4(__fadd_rn(p.x, q.x), __fadd_rn(p.y, q.y), __fadd_rn(p.z, q.z),
-                       __fadd_rn(p.w, q.w));
-  };
-  for (int x = x0 + (tid >> 3); x < x1 && !(a.dbg & 1); x += kHotThreads / G) {
+// Rows cut across tasks: 8 lanes per task whose first row began in an
+// earlier task and ends in it -> tail[ts] + ... + tail[x-1] + head[x], in
+// task order, all columns (the tasks inside a row longer than K/2 start every
+// K edges, so ts = x - ceil((e0 - row start) / K)).  Then one thread per row:
+// empty rows get zeros.
+__global__ void __launch_bounds__(256)
+spmm_hot_fixup_kernel(HotArgs a, int task_blocks) {
+  const int F4 = a.F >> 2, C4 = a.cf >> 2;
+  const int nlim = a.rowptr[a.n_rows];
+  if ((int)blockIdx.x < task_blocks) {
+    const int x = (blockIdx.x * 256 + threadIdx.x) >> 3, k = threadIdx.x & 7;
+    if (x >= a.tile_task[a.T]) return;
     const int e0 = min(a.task_start[x], nlim), e1 = min(a.task_start[x + 1], nlim);
-    if (e0 >= e1) continue;
-    const int r = a.task_row[x];
+    const uint32_t trw = (uint32_t)a.task_row[x];
+    if (e0 >= e1 || !(trw & kHeadBit)) return;
+    const int r = (int)(trw & kRowMask);
     const int rs = a.rowptr[r], re = a.rowptr[r + 1];
-    if (!(rs < e0 && re <= e1)) continue;
-    const int ts = x0 + upper_bound_i32(a.task_start + x0, x - x0, rs) - 1;
-    if (!pv) continue;
-    float4 sum = c4p[((int64_t)ts * 2 + 1) * C4 + c4];
-    int u = ts + 1;
-    for (; u + 8 <= x; u += 8) {               // loads 8 tasks ahead of the in-order adds
-      float4 qq[8];
+    if (re > e1) return;                             // the row continues: a later task sums it
+    const int ts = x - (e0 - rs + a.K - 1) / a.K;
+    const float4* c4p = reinterpret_cast<const float4*>(a.carry);
+    auto add4 = [](float4 p, float4 q) {
+      return make_float4(__fadd_rn(p.x, q.x), __fadd_rn(p.y, q.y), __fadd_rn(p.z, q.z),
+                         __fadd_rn(p.w, q.w));
+    };
+    for (int c = k; c < F4; c += 8) {
+      float4 sum = c4p[((int64_t)ts * 2 + 1) * C4 + c];
+      int u = ts + 1;
+      for (; u + 8 <= x; u += 8) {                   // loads 8 tasks ahead of the in-order adds
+        float4 qq[8];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) qq[i] = c4p[((int64_t)(u + i) * 2 + 1) * C4 + c4];
+        for (int i = 0; i < 8; ++i) qq[i] = c4p[((int64_t)(u + i) * 2 + 1) * C4 + c];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) sum = add4(sum, qq[i]);
+        for (int i = 0; i < 8; ++i) sum = add4(sum, qq[i]);
+      }
+      for (; u < x; ++u) sum = add4(sum, c4p[((int64_t)u * 2 + 1) * C4 + c]);
+      sum = add4(sum, c4p[(int64_t)x * 2 * C4 + c]);
+      reinterpret_cast<float4*>(a.out + (int64_t)r * a.ldo)[c] = sum;
     }
-    for (; u < x; ++u) sum = add4(sum, c4p[((int64_t)u * 2 + 1) * C4 + c4]);
-    sum = add4(sum, c4p[(int64_t)x * 2 * C4 + c4]);
-    *reinterpret_cast<float4*>(a.out + (int64_t)r * a.ldo + 4 * c4) = sum;
+  } else {
+    const int r = (blockIdx.x - task_blocks) * 256 + threadIdx.x;
+    if (r >= a.n_rows || a.rowptr[r] != a.rowptr[r + 1]) return;
+    float4* o = reinterpret_cast<float4*>(a.out + (int64_t)r * a.ldo);
+    for (int c = 0; c < F4; ++c) o[c] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
-  // 4. empty rows of the tile: zeros
-  for (int r = r0 + (tid >> 3); r < r1; r += kHotThreads / G)
-    if (pv && a.rowptr[r] == a.rowptr[r + 1])
-      *reinterpret_cast<float4*>(a.out + (int64_t)r * a.ldo + 4 * c4) = make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
 // the records' weights replaced (same structure and hot slots: the GAT
@@ -1399,6 +1483,7 @@ extern "C" int vqgnn_spmm_hot(const int32_t* rowptr, int32_t n_rows, int32_t n_c
   VQGNN_REQUIRE(C >= 0 && C <= kHotMaxC && Et >= K, "spmm_hot: bad plan geometry");
   VQGNN_REQUIRE(n_cols <= (int32_t)kHotColMask, "spmm_hot: %d columns exceed 2^25", n_cols);
   if (n_rows == 0) return VQGNN_OK;
+  VQGNN_REQUIRE(n_rows < (1 << 30), "spmm_hot: %d rows exceed 2^30", n_rows);
   const int T = hot_tiles(nnz, Et);
   const int NT = hot_ntasks_max(nnz, K, T);
   HotView v = hot_view(const_cast<int32_t*>(plan), T, NT, C);
@@ -1416,7 +1501,12 @@ extern "C" int vqgnn_spmm_hot(const int32_t* rowptr, int32_t n_rows, int32_t n_c
   a.K = K;
   a.T = T;
   a.C = C;
-  a.S = (F / 4 + kHotSlice4 - 1) / kHotSlice4;
+  // slices of 4G floats: G = 32 (512-byte rows, at most 256 hot rows) when
+  // the plan's hot rows fit, else G = 8 (128-byte slices, up to 1,024)
+  const int G = task_env("VQGNN_HOT_G", C <= kHotLdsBytes / 512 ? 32 : 8) >= 32 ? 32 : 8;
+  VQGNN_REQUIRE((size_t)C * G * 16 <= (size_t)kHotLdsBytes,
+                "spmm_hot: %d hot rows of %d bytes exceed the LDS", C, G * 16);
+  a.S = (F / 4 + G - 1) / G;
   a.B = ta.B;
   a.X = ta.X;
   a.ldx = ta.ldx;
@@ -1437,9 +1527,50 @@ extern "C" int vqgnn_spmm_hot(const int32_t* rowptr, int32_t n_rows, int32_t n_c
   a.dbg = task_env("VQGNN_HOT_DBG", 0);
   hipStream_t s = as_stream(stream);
   const dim3 grid((unsigned)((int64_t)T * a.S));
-  const bool part = (F / 4) % kHotSlice4 != 0;
-  if (!near) hipLaunchKernelGGL((spmm_hot_kernel<true, false>), grid, dim3(kHotThreads), 0, s, a);
-  else if (part) hipLaunchKernelGGL((spmm_hot_kernel<false, true>), grid, dim3(kHotThreads), 0, s, a);
-  else hipLaunchKernelGGL((spmm_hot_kernel<false, false>), grid, dim3(kHotThreads), 0, s, a);
+  const bool part = (F / 4) % G != 0;
+  const size_t lds = (size_t)(C > 0 ? C : 1) * G * 16;
+  // 16-wave workgroups (one per CU) when the slices take more than half the
+  // LDS, else 8-wave workgroups two per CU; VQGNN_HOT_WAVES forces 8 or 16
+  const int nw_env = task_env("VQGNN_HOT_WAVES", 0);
+  const bool wide = nw_env ? nw_env >= 16 : lds > (size_t)kHotLdsBytes / 2;
+  // dynamic LDS above 64 KiB: allowed once per kernel instance
+  static const bool attrs = [] {
+    void (*ks[])(HotArgs) = {
+        spmm_hot_kernel<8, true, false, 16>,  spmm_hot_kernel<8, false, true, 16>,
+        spmm_hot_kernel<8, false, false, 16>, spmm_hot_kernel<8, true, false, 8>,
+        spmm_hot_kernel<8, false, true, 8>,   spmm_hot_kernel<8, false, false, 8>,
+        spmm_hot_kernel<32, true, false, 16>,  spmm_hot_kernel<32, false, true, 16>,
+        spmm_hot_kernel<32, false, false, 16>, spmm_hot_kernel<32, true, false, 8>,
+        spmm_hot_kernel<32, false, true, 8>,   spmm_hot_kernel<32, false, false, 8>};
+    for (auto k : ks)
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, kHotLdsBytes);
+    return true;
+  }();
+  (void)attrs;
+  auto go = [&](void (*kern)(HotArgs), int threads) {
+    hipLaunchKernelGGL(kern, grid, dim3(threads), lds, s, a);
+  };
+  auto pick = [&](auto gtag) {
+    constexpr int GG = decltype(gtag)::value;
+    if (wide) {
+      if (!near) go(spmm_hot_kernel<GG, true, false, 16>, 1024);
+      else if (part) go(spmm_hot_kernel<GG, false, true, 16>, 1024);
+      else go(spmm_hot_kernel<GG, false, false, 16>, 1024);
+    } else {
+      if (!near) go(spmm_hot_kernel<GG, true, false, 8>, 512);
+      else if (part) go(spmm_hot_kernel<GG, false, true, 8>, 512);
+      else go(spmm_hot_kernel<GG, false, false, 8>, 512);
+    }
+  };
+  if (G == 32) pick(std::integral_constant<int, 32>{});
+  else pick(std::integral_constant<int, 8>{});
+  // rows cut across tasks and empty rows (unless VQGNN_HOT_DBG bit 0)
+  if (!(a.dbg & 1)) {
+    const int task_blocks = (NT * 8 + 255) / 256;
+    const int row_blocks = (n_rows + 255) / 256;
+    hipLaunchKernelGGL(spmm_hot_fixup_kernel, dim3(task_blocks + row_blocks), dim3(256), 0, s, a,
+                       task_blocks);
+  }
   return check_launch("spmm_hot");
 }
