@@ -53,9 +53,6 @@ def parse():
     # kernel events inside the timed region (the roofline kernel's launches);
     # off only to measure what they cost
     p.add_argument("--no-kernel-events", action="store_true")
-    # SpMM plan of the GCN/SAGE aggregation: hot-column tiles (include/vqgnn.h
-    # §6h) or the task plan (§6); default: CSR.plan's (sparse.DEFAULT_PLAN)
-    p.add_argument("--spmm", choices=["hot", "task"], default=None)
     return p.parse_args()
 
 
@@ -166,10 +163,8 @@ def main():
     # per-batch adjacency preparation (like the reference's SparseTensor build
     # in the data loader): the SpMM task plan, built once per batch before the
     # timed region; its cost is reported as plan_ms
-    from vq_gnn_amd.sparse import DEFAULT_PLAN
-    spmm_kind = args.spmm or DEFAULT_PLAN
-    spmm_plan = adj.plan(F, B=B, kind=spmm_kind)
-    plan_ms = time_plan(adj, n, nnz, spmm_kind)
+    spmm_plan = adj.plan(F, B=B)
+    plan_ms = time_plan(adj, n, nnz)
     # codebook state = one feature_update warm pass
     bank.feature_update(Xd, 0, nb, True, codes=codes, batch_idx=bidx)
     torch.cuda.synchronize()
@@ -307,10 +302,8 @@ def main():
     vq_flops = 2.0 * B * M * W * nb
     pmc, pmc_ctr, pmc_note = load_pmc(args)
     agg_name = ("gat aggregation (alpha + fused coefficient/SpMM/normalise walker)"
-                if gat is not None else
-                "spmm_hot_kernel (hot-column tiles, in-workgroup cut rows)" if spmm_kind == "hot"
-                else "spmm_task_kernel+spmm_task_fixup_kernel")
-    agg_pmc = "spmm_hot_kernel" if gat is None and spmm_kind == "hot" else "spmm_task_kernel"
+                if gat is not None else "spmm_task_kernel+spmm_task_fixup_kernel")
+    agg_pmc = "spmm_task_kernel"
     rl_spmm = dict(kernel=agg_name, bound="hbm",
                    achieved=spmm_bytes / (spmm_ms * 1e-3) / 1e9, peak=8000.0, unit="GB/s",
                    bytes_per_launch=spmm_bytes, ms_per_launch=spmm_ms,
@@ -318,7 +311,7 @@ def main():
     rl_spmm["frac"] = rl_spmm["achieved"] / rl_spmm["peak"]
     if rl_spmm["traffic"]:
         rl_spmm["traffic_over_algorithmic"] = rl_spmm["traffic"] / spmm_bytes
-    if gat is None and spmm_kind == "task":
+    if gat is None:
         # the kernel's own floor: the same plan shape with every column folded
         # onto 1,024 hot rows (all gathers hit L2), DESIGN.md §4.2
         rl_spmm["floor_ms"], rl_spmm["floor_note"] = spmm_floor(kernels, adj, Xd, B, n, nnz, F)
@@ -374,7 +367,6 @@ def main():
                                  f"codeword gather, "
                                  f"{'GAT attention aggregation' if gat is not None else 'SpMM'})",
                         B=B, B_prime=n - B, nnz=nnz, F=F, M=M, D=D, W=W,
-                        spmm_plan=(None if gat is not None else spmm_kind),
                         parallelism=f"dp{world}", world=world,
                         backend=(args.backend if comm is not None else None),
                         rccl_ranks=(world if comm is not None and args.backend == "nccl" else 0),
@@ -481,20 +473,15 @@ def assign_roofline(name, assign_ms, B, M, W, nb, f32_flops, ctr):
     return out
 
 
-def time_plan(adj, n, nnz, kind="task", reps=5):
-    """Device time of one SpMM plan build (task plan: records, task starts,
-    fix-up jobs and the job-count readback; hot plan: records, tiles, tasks
-    and the per-tile hot rows), the per-batch preparation outside the timed
-    step."""
+def time_plan(adj, n, nnz, reps=5):
+    """Device time of one task-plan build (records, task starts, fix-up jobs and
+    the job-count readback), the per-batch preparation outside the timed step."""
     from vq_gnn_amd import kernels
     ts = []
     for _ in range(reps + 1):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        if kind == "hot":
-            kernels.spmm_hot_plan(adj.rowptr, adj.col, adj.value, n, nnz, n_cols=adj.size(1))
-        else:
-            kernels.spmm_task_plan(adj.rowptr, adj.col, adj.value, n, nnz)
+        kernels.spmm_task_plan(adj.rowptr, adj.col, adj.value, n, nnz)
         torch.cuda.synchronize()
         ts.append(time.perf_counter() - t0)
     return float(np.median(ts[1:])) * 1e3

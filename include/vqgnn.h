@@ -272,37 +272,6 @@ int vqgnn_spmm_task(const int32_t* rowptr, int32_t n_rows, int32_t n_cols, int64
                     const int64_t* records, int32_t K, int32_t n_jobs, int32_t n_empty,
                     void* workspace, vqgnn_stream_t stream);
 
-/* 6h. Hot-column tile SpMM: the same product and arguments as 6 (xin = [X ;
- *    X2], same per-row arithmetic: a sequential fma chain in CSR order, cut
- *    rows' partials added in task order), for cluster-sampled batches whose
- *    row tiles reuse source rows (convs.py:95 over dataloader.py:28-38's
- *    batches).  vqgnn_spmm_hot_plan cuts the rows into row-aligned tiles of
- *    about Et edges (K <= Et <= 16384), tasks of K edges inside each tile,
- *    and picks per tile the (at most C <= 1024) source rows its edges
- *    reference most (used at least twice); records [nnz] int64 hold the
- *    source column or, for those rows, an LDS slot.  plan
- *    [vqgnn_spmm_hot_size(nnz, K, Et, C)] int32; n_cols < 2^25; no host read.
- *    vqgnn_spmm_hot: one workgroup per (tile, 32-float column slice) stages
- *    the tile's hot rows' slices in LDS, walks its tasks (8 lanes per task)
- *    reading hot rows from LDS and the others from memory, and adds its cut
- *    rows itself (no fix-up launch).  Which rows are hot changes where a value
- *    is read from, never its bits.  A call may cover the first n_rows rows of
- *    the planned CSR (as 6).  Workspace: vqgnn_spmm_hot_workspace(nnz, K, Et,
- *    F) bytes.  vqgnn_spmm_records_set_values copies records with other
- *    weights (same structure and hot slots; out may not alias records).     */
-int64_t vqgnn_spmm_hot_size(int64_t nnz, int32_t K, int32_t Et, int32_t C);
-size_t vqgnn_spmm_hot_workspace(int64_t nnz, int32_t K, int32_t Et, int32_t F);
-int vqgnn_spmm_hot_plan(const int32_t* rowptr, const int32_t* col, const float* val,
-                        int32_t n_rows, int32_t n_cols, int64_t nnz, int32_t K, int32_t Et,
-                        int32_t C, int32_t* plan, int64_t* records, vqgnn_stream_t stream);
-int vqgnn_spmm_records_set_values(const int64_t* records, const float* val, int64_t nnz,
-                                  int64_t* out, vqgnn_stream_t stream);
-int vqgnn_spmm_hot(const int32_t* rowptr, int32_t n_rows, int32_t n_cols, int64_t nnz,
-                   int32_t B, const float* X, int64_t ldx, const float* X2, int64_t ldx2,
-                   int32_t F, float* out, int64_t ldo, const int32_t* plan,
-                   const int64_t* records, int32_t K, int32_t Et, int32_t C, void* workspace,
-                   vqgnn_stream_t stream);
-
 /* 7. CSR transpose (structure + values) for the backward product
  *    dX = A^T dOut (torch_sparse matmul autograd, convs.py:95).  Output CSR of
  *    A^T with rows sorted by column of A; within a row, entries ordered by

@@ -64,15 +64,6 @@ SIGNATURES = {
     "vqgnn_spmm_task": (ctypes.c_int, [_c_void_p, _i32, _i32, _i64, _i32, _c_void_p, _i64,
                                        _c_void_p, _i64, _i32, _c_void_p, _i64, _c_void_p,
                                        _c_void_p, _i32, _i32, _i32, _c_void_p, _c_void_p]),
-    "vqgnn_spmm_hot_size": (_i64, [_i64, _i32, _i32, _i32]),
-    "vqgnn_spmm_hot_workspace": (_size, [_i64, _i32, _i32, _i32]),
-    "vqgnn_spmm_hot_plan": (ctypes.c_int, [_c_void_p, _c_void_p, _c_void_p, _i32, _i32, _i64,
-                                           _i32, _i32, _i32, _c_void_p, _c_void_p, _c_void_p]),
-    "vqgnn_spmm_records_set_values": (ctypes.c_int, [_c_void_p, _c_void_p, _i64, _c_void_p,
-                                                     _c_void_p]),
-    "vqgnn_spmm_hot": (ctypes.c_int, [_c_void_p, _i32, _i32, _i64, _i32, _c_void_p, _i64,
-                                      _c_void_p, _i64, _i32, _c_void_p, _i64, _c_void_p,
-                                      _c_void_p, _i32, _i32, _i32, _c_void_p, _c_void_p]),
     "vqgnn_gat_att_grad_workspace": (_size, [_i32, _i32, _i32]),
     "vqgnn_gat_att_grad": (ctypes.c_int, [_c_void_p, _i64, _c_void_p, _i64, _i32, _i32, _i32,
                                           _i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p,

@@ -30,7 +30,6 @@
 
 #include "common.h"
 
-#include <type_traits>
 #include <utility>
 
 namespace vqgnn {
@@ -588,606 +587,6 @@ static void launch_task_u(const TaskArgs& a, int tiles, int U, bool near, hipStr
 }
 
 
-// ---- hot-column tiles: the default GCN/SAGE aggregation --------------------
-//
-// The task kernel above gathers every edge's 512-byte source row from the L2
-// (1.06 GB per arxiv launch) and sits on the per-CU gather rate (DESIGN.md
-// §4.2).  The batch comes from a cluster sampler (dataloader.py:28-38) over a
-// graph with Zipf-weighted hubs, so the rows of a contiguous row tile reuse
-// a small set of source rows many times (arxiv: the 1,024 most referenced
-// source rows of a 16 k-edge tile carry 64 % of its edges, ~10 uses each).
-// The hot plan cuts the rows into row-aligned tiles of about Et edges and
-// picks, per tile, its (at most C) most referenced source rows used at least
-// twice.  A workgroup = (tile, 32-float column slice): it stages those rows'
-// slices in LDS (C x 128 B), walks the tile's tasks (K edges each, 8 lanes per
-// task, one float4 per lane) reading hot rows from LDS and the others from
-// global memory, then sums the tile's cut rows itself (rows never span
-// tiles: no fix-up kernel).  Per-row arithmetic is the task kernel's: a
-// sequential fma chain in CSR order, cut rows' partials added in task order;
-// which rows are hot changes where a value is read from, never its bits.
-//
-// Hot records: the task records with bits 0-24 = source column, or (bit 25
-// set) the row's LDS slot; bits 26-31 as above (skip count, row end).
-
-constexpr int kHotLdsBytes = 128 * 1024;      // staged hot slices per workgroup (at most)
-constexpr int kHotMaxC = 1024;                // hot rows per tile (128-byte slices)
-constexpr uint32_t kLocalBit = 1u << 25;
-constexpr uint32_t kHotColMask = (1u << 25) - 1;
-constexpr int kHotTab = 24576;                // plan hash table (keys 96 KiB + u16 counts 48 KiB)
-constexpr int kHotProbe = 64;
-constexpr int kHotHeader = 8;                 // plan ints: T, C, Et, ntasks, K, 0, 0, 0
-
-struct HotView {
-  int32_t* head;
-  int32_t* tile_row;    // [T + 1] first row of each tile (row-aligned)
-  int32_t* tile_task;   // [T + 1] first task of each tile
-  int32_t* hot_n;       // [T] hot rows per tile
-  int32_t* task_start;  // [NT + 1]
-  int32_t* task_row;    // [NT]
-  int32_t* hot;         // [T][C] source column of each LDS slot
-};
-
-inline int hot_tiles(int64_t nnz, int Et) { return nnz > 0 ? (int)((nnz + Et - 1) / Et) : 1; }
-inline int hot_ntasks_max(int64_t nnz, int K, int T) { return (int)(nnz / K) + T + 1; }
-
-inline HotView hot_view(int32_t* base, int T, int NT, int C) {
-  HotView v;
-  v.head = base;
-  v.tile_row = base + kHotHeader;
-  v.tile_task = v.tile_row + T + 1;
-  v.hot_n = v.tile_task + T + 1;
-  v.task_start = v.hot_n + T;
-  v.task_row = v.task_start + NT + 1;
-  v.hot = v.task_row + NT;
-  return v;
-}
-
-__device__ __forceinline__ int lower_bound_i32(const int32_t* __restrict__ a, int n, int key) {
-  // first i in [0, n) with a[i] >= key (n if none)
-  int lo = 0, hi = n;
-  while (lo < hi) {
-    const int mid = (lo + hi) >> 1;
-    if (a[mid] < key) lo = mid + 1; else hi = mid;
-  }
-  return lo;
-}
-
-// tile t starts at the first row whose first edge is at or past t * Et
-__global__ void hot_tiles_kernel(const int32_t* __restrict__ rowptr, int n_rows, int nnz, int Et,
-                                 int T, int32_t* __restrict__ tile_row) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t > T) return;
-  tile_row[t] = t == 0 ? 0 : t == T ? n_rows
-                      : lower_bound_i32(rowptr, n_rows + 1, (int)min((int64_t)t * Et, (int64_t)nnz));
-}
-
-// tile_task = exclusive scan of ceil(edges / K) over the tiles (one block)
-__global__ void __launch_bounds__(1024)
-hot_scan_kernel(const int32_t* __restrict__ rowptr, int T, int K, int C, int Et,
-                const int32_t* __restrict__ tile_row, int32_t* __restrict__ tile_task,
-                int32_t* __restrict__ head) {
-  __shared__ int part[1024];
-  const int per = (T + 1023) / 1024;
-  const int t0 = threadIdx.x * per, t1 = min(T, t0 + per);
-  auto ntask = [&](int t) {
-    const int E = rowptr[tile_row[t + 1]] - rowptr[tile_row[t]];
-    return (E + K - 1) / K;
-  };
-  int sum = 0;
-  for (int t = t0; t < t1; ++t) sum += ntask(t);
-  part[threadIdx.x] = sum;
-  __syncthreads();
-  for (int o = 1; o < 1024; o <<= 1) {
-    const int v = (int)threadIdx.x >= o ? part[threadIdx.x - o] : 0;
-    __syncthreads();
-    part[threadIdx.x] += v;
-    __syncthreads();
-  }
-  int run = threadIdx.x ? part[threadIdx.x - 1] : 0;
-  for (int t = t0; t < t1; ++t) {
-    tile_task[t] = run;
-    run += ntask(t);
-  }
-  if (threadIdx.x == 1023) {
-    tile_task[T] = part[1023];
-    head[0] = T;
-    head[1] = C;
-    head[2] = Et;
-    head[3] = part[1023];        // tasks in all tiles
-    head[4] = K;
-  }
-}
-
-// start of task kk (of ntask) of a tile [te0, te1): nominal starts every K
-// edges from the tile's first edge, snapped past rows of at most K/2 edges
-// (as task_first_row_kernel); kk == ntask: the tile's end
-__device__ __forceinline__ int hot_task_start(const int32_t* __restrict__ rowptr, int n_rows,
-                                              int K, int te0, int te1, int kk, int ntask) {
-  if (kk >= ntask) return te1;
-  int st = te0 + kk * K;
-  if (kk > 0) {
-    const int r = upper_bound_i32(rowptr, n_rows, st) - 1;
-    const int rs = rowptr[r], re = rowptr[r + 1];
-    if (rs < st && re - rs <= K / 2) st = re;
-  }
-  return st;
-}
-
-// task x: its first edge, and its first row with two flags: bit 31 "head"
-// (the row began in an earlier task), bit 30 "open" (the task's last row
-// continues in the next task) -- so the SpMM reads no rowptr per task
-constexpr uint32_t kHeadBit = 1u << 31, kOpenBit = 1u << 30, kRowMask = (1u << 30) - 1;
-__global__ void hot_tasks_kernel(const int32_t* __restrict__ rowptr, int n_rows, int nnz, int K,
-                                 int T, const int32_t* __restrict__ tile_row,
-                                 const int32_t* __restrict__ tile_task,
-                                 const int32_t* __restrict__ head, int32_t* __restrict__ task_start,
-                                 int32_t* __restrict__ task_row) {
-  const int x = blockIdx.x * blockDim.x + threadIdx.x;
-  const int total = head[3];
-  if (x > total) return;
-  if (x == total) {
-    task_start[x] = nnz;
-    return;
-  }
-  const int t = upper_bound_i32(tile_task, T, x) - 1;
-  const int kk = x - tile_task[t];
-  const int ntask = tile_task[t + 1] - tile_task[t];
-  const int te0 = rowptr[tile_row[t]], te1 = rowptr[tile_row[t + 1]];
-  const int st = hot_task_start(rowptr, n_rows, K, te0, te1, kk, ntask);
-  const int en = hot_task_start(rowptr, n_rows, K, te0, te1, kk + 1, ntask);
-  task_start[x] = st;
-  uint32_t row = (uint32_t)(tile_row[t + 1] - 1), flags = 0;
-  if (st < en) {
-    row = (uint32_t)(upper_bound_i32(rowptr, n_rows, st) - 1);
-    if (rowptr[row] < st) flags |= kHeadBit;
-    const int rl = upper_bound_i32(rowptr, n_rows, en - 1) - 1;   // the row of the last edge
-    if (rowptr[rl + 1] > en) flags |= kOpenBit;
-  }
-  task_row[x] = (int)(row | flags);
-}
-
-__device__ __forceinline__ int hot_hash(int c) {
-  return (int)(((uint64_t)((uint32_t)c * 2654435761u) * kHotTab) >> 32);
-}
-
-// One workgroup per tile: count the tile's source columns in an LDS hash
-// table, keep the (at most C) most referenced ones used at least twice (a
-// count threshold from a histogram; ties at the threshold in table order),
-// number them in table order, and rewrite the tile's records (bit 25 + slot
-// for a hot column).  Columns the table cannot place within kHotProbe probes
-// stay global (speed only).
-__global__ void __launch_bounds__(1024)
-hot_select_kernel(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col, int C,
-                  const int32_t* __restrict__ tile_row, int32_t* __restrict__ hot_n,
-                  int32_t* __restrict__ hot, int2* __restrict__ rec) {
-  __shared__ int32_t keys[kHotTab];
-  __shared__ uint32_t cnt[kHotTab / 2];        // u16 counts, then u16 slots (0xFFFF: none)
-  __shared__ int32_t sc[1024];
-  __shared__ int32_t hist[1024];
-  __shared__ int32_t vstar_s;
-  const int tid = threadIdx.x;
-  const int t = blockIdx.x;
-  const int e0 = rowptr[tile_row[t]], e1 = rowptr[tile_row[t + 1]];
-  for (int i = tid; i < kHotTab; i += 1024) keys[i] = -1;
-  for (int i = tid; i < kHotTab / 2; i += 1024) cnt[i] = 0;
-  hist[tid] = 0;
-  if (tid == 0) vstar_s = 1024;
-  __syncthreads();
-  for (int e = e0 + tid; e < e1; e += 1024) {
-    const int c = col[e];
-    int i = hot_hash(c);
-    for (int p = 0; p < kHotProbe; ++p) {
-      int k = keys[i];
-      if (k == -1) {
-        k = atomicCAS(&keys[i], -1, c);
-        if (k == -1) k = c;
-      }
-      if (k == c) {
-        atomicAdd(&cnt[i >> 1], 1u << (16 * (i & 1)));
-        break;
-      }
-      i = i + 1 == kHotTab ? 0 : i + 1;
-    }
-  }
-  __syncthreads();
-  auto count_of = [&](int i) { return (int)((cnt[i >> 1] >> (16 * (i & 1))) & 0xFFFFu); };
-  for (int i = tid; i < kHotTab; i += 1024) {
-    const int n = count_of(i);
-    if (n >= 2) atomicAdd(&hist[min(n, 1023)], 1);
-  }
-  __syncthreads();
-  // ge(v) = entries with capped count >= v: a suffix scan of the histogram
-  sc[tid] = hist[1023 - tid];
-  __syncthreads();
-  for (int o = 1; o < 1024; o <<= 1) {
-    const int v = tid >= o ? sc[tid - o] : 0;
-    __syncthreads();
-    sc[tid] += v;
-    __syncthreads();
-  }
-  auto ge = [&](int v) { return v >= 1024 ? 0 : sc[1023 - v]; };
-  // v*: the smallest count >= 2 whose class and above fit in C
-  if (tid >= 2 && ge(tid) <= C && (tid == 2 || ge(tid - 1) > C)) vstar_s = tid;
-  __syncthreads();
-  const int vstar = vstar_s;
-  const int tie = vstar - 1;                     // the partly taken class (if >= 2)
-  const int quota = tie >= 2 ? C - ge(vstar) : 0;
-  constexpr int kPer = kHotTab / 1024;           // 24 entries per thread, in table order
-  const int i0 = tid * kPer;
-  int nties = 0;
-  for (int i = i0; i < i0 + kPer; ++i) nties += min(count_of(i), 1023) == tie;
-  __syncthreads();
-  sc[tid] = nties;
-  __syncthreads();
-  for (int o = 1; o < 1024; o <<= 1) {
-    const int v = tid >= o ? sc[tid - o] : 0;
-    __syncthreads();
-    sc[tid] += v;
-    __syncthreads();
-  }
-  int tie_rank = sc[tid] - nties;
-  bool sel[kPer];
-  int nsel = 0;
-  for (int j = 0; j < kPer; ++j) {
-    const int n = min(count_of(i0 + j), 1023);
-    bool s = n >= 2 && n >= vstar;
-    if (n == tie && tie >= 2) {
-      s = tie_rank < quota;
-      ++tie_rank;
-    }
-    sel[j] = s;
-    nsel += s;
-  }
-  __syncthreads();
-  sc[tid] = nsel;
-  __syncthreads();
-  for (int o = 1; o < 1024; o <<= 1) {
-    const int v = tid >= o ? sc[tid - o] : 0;
-    __syncthreads();
-    sc[tid] += v;
-    __syncthreads();
-  }
-  int slot = sc[tid] - nsel;
-  const int total = sc[1023];
-  __syncthreads();
-  for (int j = 0; j < kPer; j += 2) {            // this thread's u16 pairs (i0 even)
-    uint32_t w = 0;
-    for (int h = 0; h < 2; ++h) {
-      uint32_t v = 0xFFFFu;
-      if (sel[j + h]) {
-        hot[(int64_t)t * C + slot] = keys[i0 + j + h];
-        v = (uint32_t)slot++;
-      }
-      w |= v << (16 * h);
-    }
-    cnt[(i0 + j) >> 1] = w;
-  }
-  if (tid == 0) hot_n[t] = min(total, C);
-  __syncthreads();
-  for (int e = e0 + tid; e < e1; e += 1024) {
-    const int c = col[e];
-    int i = hot_hash(c);
-    uint32_t low = (uint32_t)c & kHotColMask;
-    for (int p = 0; p < kHotProbe; ++p) {
-      const int k = keys[i];
-      if (k == c) {
-        const uint32_t sl = (cnt[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
-        if (sl != 0xFFFFu) low = kLocalBit | sl;
-        break;
-      }
-      if (k == -1) break;
-      i = i + 1 == kHotTab ? 0 : i + 1;
-    }
-    int2 v = rec[e];
-    v.x = (int)(((uint32_t)v.x & ~kColMask) | low);
-    rec[e] = v;
-  }
-}
-
-struct HotArgs {
-  const int2* rec;
-  const int32_t* tile_row;
-  const int32_t* tile_task;
-  const int32_t* hot_n;
-  const int32_t* task_start;
-  const int32_t* task_row;
-  const int32_t* hot;
-  const int32_t* rowptr;
-  int n_rows, nnz, K, T, C, S;
-  int B;
-  const float* X;
-  int64_t ldx;
-  const float* X2;
-  int64_t ldx2;
-  int F;
-  float* out;
-  int64_t ldo;
-  float* carry;
-  int cf;
-  const char* ubase;
-  uint32_t span, offx, ldxb, offx2, ldx2b, ldob;
-  int dbg;    // experiments (VQGNN_HOT_DBG): 1 no fix-up kernel, 2 no stores, 4 all edges global
-};
-
-// Byte offset (near) / address (far) of source row j's slice piece.
-template <bool FAR>
-__device__ __forceinline__ const char* hot_far_row(const HotArgs& a, int j) {
-  const float* row = j < a.B ? a.X + (int64_t)j * a.ldx : a.X2 + (int64_t)(j - a.B) * a.ldx2;
-  return reinterpret_cast<const char*>(row);
-}
-
-// G lanes per task, one float4 each: a column slice of 4G floats (G = 32:
-// 512-byte slices, two tasks per wave as the task kernel walks them; G = 8:
-// 128-byte slices, eight tasks per wave).  NW waves per workgroup: 16 (one
-// workgroup per CU) or 8 (two per CU: one's staging overlaps the other's walk).
-template <int G, bool FAR, bool PART, int NW>
-__global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4)))
-spmm_hot_kernel(HotArgs a) {
-  extern __shared__ float4 lds[];                    // [C][G] float4
-  constexpr int U = 16, NT = NW * 64;
-  constexpr int TPW = 64 / G;                        // tasks per wave and round
-  const int L = xcd_remap(blockIdx.x, gridDim.x);   // a tile's slices: one XCD, consecutive
-  const int t = L / a.S, sl = L - t * a.S;
-  const int r0 = a.tile_row[t];
-  const int r1 = min(a.tile_row[t + 1], a.n_rows);
-  if (r0 >= r1) return;                              // workgroup-uniform
-  const int nlim = a.rowptr[r1];                     // edges of the rows computed here
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int g = lane / G, k = lane % G;
-  const int F4 = a.F >> 2;
-  const int c4 = sl * G + k;                         // this lane's float4 column
-  const bool pv = c4 < F4;
-  const uint32_t lane_off = (uint32_t)c4 * 16u;
-  const uint32_t kill = PART && !pv ? 0x80000000u : 0u;
-  const __amdgpu_buffer_rsrc_t rsx =
-      __builtin_amdgcn_make_buffer_rsrc((void*)a.ubase, 0, FAR ? 0 : (int)a.span, 0x00020000);
-
-  // this wave's first round of tasks: its metadata is issued before the
-  // staging, so the two latencies overlap; every later round's metadata is
-  // issued one round ahead
-  const int x0 = a.tile_task[t], x1 = a.tile_task[t + 1];
-  struct Meta { int ws, s0, s1, tr; };
-  auto meta = [&](int xbb) {
-    Meta m{0, 0, 0, 0};
-    const int x = xbb + g;
-    if (xbb < x1) m.ws = a.task_start[xbb];
-    if (x < x1) {
-      m.s0 = a.task_start[x];
-      m.s1 = a.task_start[x + 1];
-      m.tr = a.task_row[x];
-    }
-    return m;
-  };
-  int xb = x0 + wv * TPW;
-  Meta cur = meta(xb);
-
-  // 1. stage the tile's hot rows (this slice) in LDS: G lanes per row
-  const int nh = min(a.hot_n[t], a.C);
-  const int32_t* hot = a.hot + (int64_t)t * a.C;
-  for (int s0 = tid / G; s0 < nh; s0 += 8 * (NT / G)) {
-    float4 v[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int s = s0 + i * (NT / G);
-      v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (s < nh && pv) {
-        const int j = hot[s];
-        if constexpr (FAR) {
-          v[i] = *reinterpret_cast<const float4*>(hot_far_row<FAR>(a, j) + lane_off);
-        } else {
-          const bool s1 = j < a.B;
-          const uint32_t off = __umul24((uint32_t)j, s1 ? a.ldxb : a.ldx2b) +
-                               (s1 ? a.offx : a.offx2 - (uint32_t)a.B * a.ldx2b) + lane_off;
-          v[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsx, off, 0, 0));
-        }
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int s = s0 + i * (NT / G);
-      if (s < nh) lds[s * G + k] = v[i];
-    }
-  }
-  __syncthreads();
-
-  // 2. the tile's tasks: a wave takes TPW consecutive tasks per round; the
-  //    rows cut across tasks are summed by spmm_hot_fixup_kernel
-  constexpr int kAnd = 0x1F & ~(G - 1);
-  const char* ldsb = reinterpret_cast<const char*>(lds);
-  int2 pq0 = make_int2(0, 0), pq1 = make_int2(0, 0);   // next round's first records, loaded
-  bool pre = false;                                    // during this round's last block
-  for (; xb < x1; xb += NW * TPW) {
-    const Meta nxt = meta(xb + NW * TPW);            // next round's metadata in flight
-    const int x = xb + g;
-    const bool tv = x < x1;
-    const int wbase = __builtin_amdgcn_readfirstlane(min(cur.ws, nlim));
-    const int e0 = tv ? min(cur.s0, nlim) : nlim;
-    const int e1 = tv ? min(cur.s1, nlim) : e0;
-    const bool valid = e0 < e1;
-    const uint32_t trw = (uint32_t)cur.tr;
-    int r = (int)(trw & kRowMask);
-    bool head = valid && (trw & kHeadBit);
-    // a task clipped at the caller's last row ends at a row end
-    const bool open = valid && (trw & kOpenBit) && cur.s1 <= nlim;
-    cur = nxt;
-    const __amdgpu_buffer_rsrc_t rsr = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(a.rec + wbase), 0,
-        (int)(uint32_t)min((int64_t)(a.nnz - wbase) * 8, (int64_t)0x7FFFFFFF), 0x00020000);
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    int len = e1 - e0;
-#pragma unroll
-    for (int o = G; o < 64; o <<= 1) len = max(len, __shfl_xor(len, o));
-    const int nblk = __builtin_amdgcn_readfirstlane((len + U - 1) / U);
-    // lane k of a group holds the record of edge e + k (and, when a block
-    // holds more edges than the group has lanes, of edge e + G + k)
-    auto load_rec = [&](int e, int2& q0, int2& q1) {
-      q0 = __builtin_bit_cast(int2, __builtin_amdgcn_raw_buffer_load_b64(
-                                        rsr, (uint32_t)(e - wbase + k) * 8u, 0, 0));
-      if constexpr (G < U)
-        q1 = __builtin_bit_cast(int2, __builtin_amdgcn_raw_buffer_load_b64(
-                                          rsr, (uint32_t)(e - wbase + G + k) * 8u, 0, 0));
-      else
-        q1 = make_int2(0, 0);
-    };
-    int2 q0, q1;
-    if (pre) {
-      q0 = pq0;
-      q1 = pq1;
-    } else {
-      load_rec(e0, q0, q1);
-    }
-    pre = false;
-    const int xn = xb + NW * TPW;                      // the next round (cur: its metadata)
-    for (int bi = 0; bi < nblk; ++bi) {
-      const int e = e0 + bi * U;
-      int2 n0, n1;
-      if (bi + 1 < nblk) {
-        load_rec(e + U, n0, n1);
-      } else if (xn < x1) {
-        // the next round's first block, issued under this block's gathers
-        const int nwb = __builtin_amdgcn_readfirstlane(min(cur.ws, nlim));
-        const int ne0 = xn + g < x1 ? min(cur.s0, nlim) : nlim;
-        const __amdgpu_buffer_rsrc_t rn = __builtin_amdgcn_make_buffer_rsrc(
-            (void*)(a.rec + nwb), 0,
-            (int)(uint32_t)min((int64_t)(a.nnz - nwb) * 8, (int64_t)0x7FFFFFFF), 0x00020000);
-        pq0 = __builtin_bit_cast(int2, __builtin_amdgcn_raw_buffer_load_b64(
-                                           rn, (uint32_t)(ne0 - nwb + k) * 8u, 0, 0));
-        if constexpr (G < U)
-          pq1 = __builtin_bit_cast(int2, __builtin_amdgcn_raw_buffer_load_b64(
-                                             rn, (uint32_t)(ne0 - nwb + G + k) * 8u, 0, 0));
-        pre = true;
-      }
-      const bool in0 = k < U && e + k >= e0 && e + k < e1;
-      const bool in1 = e + G + k >= e0 && e + G + k < e1;
-      int2 m0 = in0 ? q0 : make_int2(0, 0), m1 = in1 ? q1 : make_int2(0, 0);
-      if (a.dbg & 4) {               // experiment: every edge from memory
-        m0.x &= ~(int)kLocalBit;
-        m1.x &= ~(int)kLocalBit;
-      }
-      int cx[U], cw[U];
-      constexpr int UB = G < U ? G : U;              // edges broadcast per record register
-      group_bcast<kAnd>(m0.x, *reinterpret_cast<int(*)[UB]>(cx), std::make_integer_sequence<int, UB>{});
-      group_bcast<kAnd>(m0.y, *reinterpret_cast<int(*)[UB]>(cw), std::make_integer_sequence<int, UB>{});
-      if constexpr (G < U) {
-        group_bcast<kAnd>(m1.x, *reinterpret_cast<int(*)[UB]>(cx + G), std::make_integer_sequence<int, UB>{});
-        group_bcast<kAnd>(m1.y, *reinterpret_cast<int(*)[UB]>(cw + G), std::make_integer_sequence<int, UB>{});
-      }
-      // every lane reads LDS first (a global edge reads slot 0, overwritten
-      // below), then the global edges load under their exec mask: a global
-      // load waits only for the LDS reads ahead of it, not a full LDS drain
-      // per divergent edge (the register WAW between the two paths).  Each
-      // lane derives the source offset from the broadcast record word (LDS
-      // slot, or a 24-bit multiply-add for the global row).
-      float4 v[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const uint32_t xw = (uint32_t)cx[u];
-        const uint32_t lo = xw & kLocalBit ? (xw & 0xFFFFu) * (uint32_t)(G * 16) : 0u;
-        v[u] = *reinterpret_cast<const float4*>(ldsb + lo + k * 16);
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const uint32_t xw = (uint32_t)cx[u];
-        if (!(xw & kLocalBit)) {
-          if constexpr (FAR) {
-            v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (pv) v[u] = *reinterpret_cast<const float4*>(
-                        hot_far_row<FAR>(a, (int)(xw & kHotColMask)) + lane_off);
-          } else {
-            const uint32_t j = xw & kHotColMask;
-            const bool s1 = (int)j < a.B;
-            const uint32_t o = (__umul24(j, s1 ? a.ldxb : a.ldx2b) +
-                                (s1 ? a.offx : a.offx2 - (uint32_t)a.B * a.ldx2b) + lane_off) | kill;
-            v[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsx, o, 0, 0));
-          }
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const float w = __int_as_float(cw[u]);
-        acc.x = fmaf(w, v[u].x, acc.x);
-        acc.y = fmaf(w, v[u].y, acc.y);
-        acc.z = fmaf(w, v[u].z, acc.z);
-        acc.w = fmaf(w, v[u].w, acc.w);
-        const uint32_t xw = (uint32_t)cx[u];
-        if (xw & kEndBit) {
-          float* dst = head ? a.carry + (int64_t)x * 2 * a.cf
-                     : FAR  ? a.out + (int64_t)r * a.ldo
-                            : reinterpret_cast<float*>(reinterpret_cast<char*>(a.out) +
-                                                       (uint64_t)(uint32_t)__umul24((uint32_t)r, a.ldob));
-          if (pv && !(a.dbg & 2)) *reinterpret_cast<float4*>(dst + 4 * c4) = acc;
-          acc = make_float4(0.f, 0.f, 0.f, 0.f);
-          const uint32_t skip = (xw >> kSkipShift) & kSkipEsc;
-          r = skip == kSkipEsc ? upper_bound_i32(a.rowptr, a.n_rows, e + u + 1) - 1
-                               : r + 1 + (int)skip;
-          head = false;
-        }
-      }
-      if (bi + 1 < nblk) {
-        q0 = n0;
-        q1 = n1;
-      }
-    }
-    if (open && pv) *reinterpret_cast<float4*>(a.carry + ((int64_t)x * 2 + 1) * a.cf + 4 * c4) = acc;
-  }
-}
-
-// Rows cut across tasks: 8 lanes per task whose first row began in an
-// earlier task and ends in it -> tail[ts] + ... + tail[x-1] + head[x], in
-// task order, all columns (the tasks inside a row longer than K/2 start every
-// K edges, so ts = x - ceil((e0 - row start) / K)).  Then one thread per row:
-// empty rows get zeros.
-__global__ void __launch_bounds__(256)
-spmm_hot_fixup_kernel(HotArgs a, int task_blocks) {
-  const int F4 = a.F >> 2, C4 = a.cf >> 2;
-  const int nlim = a.rowptr[a.n_rows];
-  if ((int)blockIdx.x < task_blocks) {
-    const int x = (blockIdx.x * 256 + threadIdx.x) >> 3, k = threadIdx.x & 7;
-    if (x >= a.tile_task[a.T]) return;
-    const int e0 = min(a.task_start[x], nlim), e1 = min(a.task_start[x + 1], nlim);
-    const uint32_t trw = (uint32_t)a.task_row[x];
-    if (e0 >= e1 || !(trw & kHeadBit)) return;
-    const int r = (int)(trw & kRowMask);
-    const int rs = a.rowptr[r], re = a.rowptr[r + 1];
-    if (re > e1) return;                             // the row continues: a later task sums it
-    const int ts = x - (e0 - rs + a.K - 1) / a.K;
-    const float4* c4p = reinterpret_cast<const float4*>(a.carry);
-    auto add4 = [](float4 p, float4 q) {
-      return make_float4(__fadd_rn(p.x, q.x), __fadd_rn(p.y, q.y), __fadd_rn(p.z, q.z),
-                         __fadd_rn(p.w, q.w));
-    };
-    for (int c = k; c < F4; c += 8) {
-      float4 sum = c4p[((int64_t)ts * 2 + 1) * C4 + c];
-      int u = ts + 1;
-      for (; u + 8 <= x; u += 8) {                   // loads 8 tasks ahead of the in-order adds
-        float4 qq[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) qq[i] = c4p[((int64_t)(u + i) * 2 + 1) * C4 + c];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) sum = add4(sum, qq[i]);
-      }
-      for (; u < x; ++u) sum = add4(sum, c4p[((int64_t)u * 2 + 1) * C4 + c]);
-      sum = add4(sum, c4p[(int64_t)x * 2 * C4 + c]);
-      reinterpret_cast<float4*>(a.out + (int64_t)r * a.ldo)[c] = sum;
-    }
-  } else {
-    const int r = (blockIdx.x - task_blocks) * 256 + threadIdx.x;
-    if (r >= a.n_rows || a.rowptr[r] != a.rowptr[r + 1]) return;
-    float4* o = reinterpret_cast<float4*>(a.out + (int64_t)r * a.ldo);
-    for (int c = 0; c < F4; ++c) o[c] = make_float4(0.f, 0.f, 0.f, 0.f);
-  }
-}
-
-// the records' weights replaced (same structure and hot slots: the GAT
-// backward's coefficient records on the transpose's hot plan)
-__global__ void records_set_values_kernel(const int2* __restrict__ src, const float* __restrict__ val,
-                                          int nnz, int2* __restrict__ dst) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= nnz) return;
-  dst[e] = make_int2(src[e].x, val ? __float_as_int(val[e]) : __float_as_int(1.f));
-}
-
 
 }  // namespace vqgnn
 
@@ -1406,171 +805,3 @@ extern "C" int vqgnn_gat_spmm_task(const int32_t* rowptr, int32_t n_rows, int32_
   return check_launch("gat_spmm_task");
 }
 
-// ---- hot-column tile plan / SpMM (include/vqgnn.h §6h) ----
-extern "C" int64_t vqgnn_spmm_hot_size(int64_t nnz, int32_t K, int32_t Et, int32_t C) {
-  if (K <= 0) K = 64;
-  if (Et <= 0) Et = 16384;
-  if (C <= 0) C = kHotMaxC;
-  const int T = hot_tiles(nnz, Et);
-  const int NT = hot_ntasks_max(nnz, K, T);
-  return kHotHeader + 3 * (int64_t)(T + 1) + (int64_t)NT + 1 + NT + (int64_t)T * C;
-}
-
-extern "C" size_t vqgnn_spmm_hot_workspace(int64_t nnz, int32_t K, int32_t Et, int32_t F) {
-  if (K <= 0) K = 64;
-  if (Et <= 0) Et = 16384;
-  const int T = hot_tiles(nnz, Et);
-  return align_up((size_t)hot_ntasks_max(nnz, K, T) * 2 * (F + 4) * sizeof(float), 256) + 256;
-}
-
-extern "C" int vqgnn_spmm_hot_plan(const int32_t* rowptr, const int32_t* col, const float* val,
-                                   int32_t n_rows, int32_t n_cols, int64_t nnz, int32_t K,
-                                   int32_t Et, int32_t C, int32_t* plan, int64_t* records,
-                                   vqgnn_stream_t stream) {
-  clear_error();
-  VQGNN_REQUIRE(rowptr && plan && n_rows > 0 && nnz >= 0 && nnz < (int64_t)1 << 31,
-                "spmm_hot_plan: bad arguments");
-  VQGNN_REQUIRE(K >= 8 && K % 4 == 0 && K <= 4096,
-                "spmm_hot_plan: K=%d must be a multiple of 4 in [8, 4096]", K);
-  VQGNN_REQUIRE(Et >= K && Et <= kHotTab * 2 / 3,
-                "spmm_hot_plan: Et=%d must be in [K, %d]", Et, kHotTab * 2 / 3);
-  VQGNN_REQUIRE(C >= 0 && C <= kHotMaxC, "spmm_hot_plan: C=%d must be in [0, %d]", C, kHotMaxC);
-  VQGNN_REQUIRE(n_cols >= 0 && n_cols <= (int32_t)kHotColMask,
-                "spmm_hot_plan: %d columns exceed 2^25", n_cols);
-  VQGNN_REQUIRE(nnz == 0 || (col && records), "spmm_hot_plan: null pointer");
-  hipStream_t s = as_stream(stream);
-  const int T = hot_tiles(nnz, Et);
-  const int NT = hot_ntasks_max(nnz, K, T);
-  HotView v = hot_view(plan, T, NT, C);
-  task_records(rowptr, col, val, n_rows, nnz, reinterpret_cast<int2*>(records), s);
-  hipLaunchKernelGGL(hot_tiles_kernel, dim3((T + 256) / 256), dim3(256), 0, s, rowptr, n_rows,
-                     (int)nnz, Et, T, v.tile_row);
-  hipLaunchKernelGGL(hot_scan_kernel, dim3(1), dim3(1024), 0, s, rowptr, T, K, C, Et,
-                     v.tile_row, v.tile_task, v.head);
-  hipLaunchKernelGGL(hot_tasks_kernel, dim3((NT + 256) / 256), dim3(256), 0, s, rowptr, n_rows,
-                     (int)nnz, K, T, v.tile_row, v.tile_task, v.head, v.task_start, v.task_row);
-  // (also for nnz == 0: every tile's hot_n is written)
-  hipLaunchKernelGGL(hot_select_kernel, dim3(T), dim3(1024), 0, s, rowptr, col, C, v.tile_row,
-                     v.hot_n, v.hot, reinterpret_cast<int2*>(records));
-  return check_launch("spmm_hot_plan");
-}
-
-extern "C" int vqgnn_spmm_records_set_values(const int64_t* records, const float* val, int64_t nnz,
-                                             int64_t* out, vqgnn_stream_t stream) {
-  clear_error();
-  VQGNN_REQUIRE(nnz >= 0 && nnz < (int64_t)1 << 31, "spmm_records_set_values: bad nnz");
-  if (nnz == 0) return VQGNN_OK;
-  VQGNN_REQUIRE(records && out, "spmm_records_set_values: null pointer");
-  hipLaunchKernelGGL(records_set_values_kernel, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0,
-                     as_stream(stream), reinterpret_cast<const int2*>(records), val, (int)nnz,
-                     reinterpret_cast<int2*>(out));
-  return check_launch("spmm_records_set_values");
-}
-
-extern "C" int vqgnn_spmm_hot(const int32_t* rowptr, int32_t n_rows, int32_t n_cols, int64_t nnz,
-                              int32_t B, const float* X, int64_t ldx, const float* X2,
-                              int64_t ldx2, int32_t F, float* out, int64_t ldo,
-                              const int32_t* plan, const int64_t* records, int32_t K, int32_t Et,
-                              int32_t C, void* workspace, vqgnn_stream_t stream) {
-  clear_error();
-  TaskArgs ta{};
-  bool near = false;
-  // validation and the near / far source path shared with the task kernel
-  // (its task geometry fields are unused here)
-  int rc = task_setup(ta, rowptr, n_rows, n_cols, nnz, B, X, ldx, X2, ldx2, F, out, ldo, plan,
-                      records, K, 0, 0, workspace, &near);
-  if (rc != VQGNN_OK) return rc;
-  VQGNN_REQUIRE(C >= 0 && C <= kHotMaxC && Et >= K, "spmm_hot: bad plan geometry");
-  VQGNN_REQUIRE(n_cols <= (int32_t)kHotColMask, "spmm_hot: %d columns exceed 2^25", n_cols);
-  if (n_rows == 0) return VQGNN_OK;
-  VQGNN_REQUIRE(n_rows < (1 << 30), "spmm_hot: %d rows exceed 2^30", n_rows);
-  const int T = hot_tiles(nnz, Et);
-  const int NT = hot_ntasks_max(nnz, K, T);
-  HotView v = hot_view(const_cast<int32_t*>(plan), T, NT, C);
-  HotArgs a{};
-  a.rec = reinterpret_cast<const int2*>(records);
-  a.tile_row = v.tile_row;
-  a.tile_task = v.tile_task;
-  a.hot_n = v.hot_n;
-  a.task_start = v.task_start;
-  a.task_row = v.task_row;
-  a.hot = v.hot;
-  a.rowptr = rowptr;
-  a.n_rows = n_rows;
-  a.nnz = (int)nnz;
-  a.K = K;
-  a.T = T;
-  a.C = C;
-  // slices of 4G floats: G = 32 (512-byte rows, at most 256 hot rows) when
-  // the plan's hot rows fit, else G = 8 (128-byte slices, up to 1,024)
-  const int G = task_env("VQGNN_HOT_G", C <= kHotLdsBytes / 512 ? 32 : 8) >= 32 ? 32 : 8;
-  VQGNN_REQUIRE((size_t)C * G * 16 <= (size_t)kHotLdsBytes,
-                "spmm_hot: %d hot rows of %d bytes exceed the LDS", C, G * 16);
-  a.S = (F / 4 + G - 1) / G;
-  a.B = ta.B;
-  a.X = ta.X;
-  a.ldx = ta.ldx;
-  a.X2 = ta.X2;
-  a.ldx2 = ta.ldx2;
-  a.F = F;
-  a.out = out;
-  a.ldo = ldo;
-  a.carry = reinterpret_cast<float*>(workspace);
-  a.cf = F + 4;
-  a.ubase = ta.ubase;
-  a.span = ta.span;
-  a.offx = ta.offx;
-  a.ldxb = ta.ldxb;
-  a.offx2 = ta.offx2;
-  a.ldx2b = ta.ldx2b;
-  a.ldob = ta.ldob;
-  a.dbg = task_env("VQGNN_HOT_DBG", 0);
-  hipStream_t s = as_stream(stream);
-  const dim3 grid((unsigned)((int64_t)T * a.S));
-  const bool part = (F / 4) % G != 0;
-  const size_t lds = (size_t)(C > 0 ? C : 1) * G * 16;
-  // 16-wave workgroups (one per CU) when the slices take more than half the
-  // LDS, else 8-wave workgroups two per CU; VQGNN_HOT_WAVES forces 8 or 16
-  const int nw_env = task_env("VQGNN_HOT_WAVES", 0);
-  const bool wide = nw_env ? nw_env >= 16 : lds > (size_t)kHotLdsBytes / 2;
-  // dynamic LDS above 64 KiB: allowed once per kernel instance
-  static const bool attrs = [] {
-    void (*ks[])(HotArgs) = {
-        spmm_hot_kernel<8, true, false, 16>,  spmm_hot_kernel<8, false, true, 16>,
-        spmm_hot_kernel<8, false, false, 16>, spmm_hot_kernel<8, true, false, 8>,
-        spmm_hot_kernel<8, false, true, 8>,   spmm_hot_kernel<8, false, false, 8>,
-        spmm_hot_kernel<32, true, false, 16>,  spmm_hot_kernel<32, false, true, 16>,
-        spmm_hot_kernel<32, false, false, 16>, spmm_hot_kernel<32, true, false, 8>,
-        spmm_hot_kernel<32, false, true, 8>,   spmm_hot_kernel<32, false, false, 8>};
-    for (auto k : ks)
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, kHotLdsBytes);
-    return true;
-  }();
-  (void)attrs;
-  auto go = [&](void (*kern)(HotArgs), int threads) {
-    hipLaunchKernelGGL(kern, grid, dim3(threads), lds, s, a);
-  };
-  auto pick = [&](auto gtag) {
-    constexpr int GG = decltype(gtag)::value;
-    if (wide) {
-      if (!near) go(spmm_hot_kernel<GG, true, false, 16>, 1024);
-      else if (part) go(spmm_hot_kernel<GG, false, true, 16>, 1024);
-      else go(spmm_hot_kernel<GG, false, false, 16>, 1024);
-    } else {
-      if (!near) go(spmm_hot_kernel<GG, true, false, 8>, 512);
-      else if (part) go(spmm_hot_kernel<GG, false, true, 8>, 512);
-      else go(spmm_hot_kernel<GG, false, false, 8>, 512);
-    }
-  };
-  if (G == 32) pick(std::integral_constant<int, 32>{});
-  else pick(std::integral_constant<int, 8>{});
-  // rows cut across tasks and empty rows (unless VQGNN_HOT_DBG bit 0)
-  if (!(a.dbg & 1)) {
-    const int task_blocks = (NT * 8 + 255) / 256;
-    const int row_blocks = (n_rows + 255) / 256;
-    hipLaunchKernelGGL(spmm_hot_fixup_kernel, dim3(task_blocks + row_blocks), dim3(256), 0, s, a,
-                       task_blocks);
-  }
-  return check_launch("spmm_hot");
-}

@@ -682,7 +682,6 @@ static size_t flt_lds_bytes(int chunk) {
 // filtered assignment for W <= 8 (section 3b)
 template <bool FUSED, int WM, int WV>
 __global__ void __launch_bounds__(WV * 64)
-__attribute__((amdgpu_waves_per_eu(WV == 10 ? 5 : 1)))   // 10 waves: two workgroups per CU at 5/SIMD
 vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restrict__ Gr,
                  int64_t ldg, int B, int nb, int D, int M, int W,
                  const float* __restrict__ coef, float grad_scale,
@@ -712,8 +711,7 @@ static const void* flt_fn_wv(bool fused, int wm) {
                  : (const void*)vq_filter_kernel<false, 0, WV>;
 }
 static const void* flt_fn(bool fused, int wm, int wv) {
-  return wv == 16 ? flt_fn_wv<16>(fused, wm)
-       : wv == 10 ? flt_fn_wv<10>(fused, wm) : flt_fn_wv<8>(fused, wm);
+  return wv == 16 ? flt_fn_wv<16>(fused, wm) : flt_fn_wv<8>(fused, wm);
 }
 
 // the filtered path serves W <= 8 (VQGNN_ASSIGN_EXACT=1: the exact f32 sweep
@@ -807,17 +805,15 @@ static AssignGeom assign_geom(int B, int nb, int M, int W) {
   if (g.fused) lds += acc;
   const size_t scr8 = 0;   // (the filter hands fragments over by permlane swaps: no scratch)
   const int wm = g.filter ? (W == 8 ? 2 : (W == 4 ? 1 : 0)) : (W == 4 * g.kc ? 2 : 0);
-  // waves per workgroup: the choice with more resident waves per CU (ties:
-  // the smaller workgroup).  The filter may also take 10 waves: at 5 waves
-  // per SIMD (its register budget) and two workgroups per CU that is 20
-  // resident waves where 8-wave workgroups leave 16.
+  // waves per workgroup: the choice with more resident waves per CU (ties: 8).
+  // (10-wave filter workgroups -- 20 resident waves at 5 per SIMD instead of
+  // 16 -- measured 1.9x slower at arxiv update, 188 vs 98 us, and 1.4x at
+  // feature_update: profiles/r04d_assign_waves_ab.txt)
   const int cap8 = assign_capacity(g.kc, g.fused, wm, lds + scr8, 8, g.filter);
   const int cap16 = assign_capacity(g.kc, g.fused, wm, lds + 2 * scr8, 16, g.filter);
   const int wenv = env_int_vq("VQGNN_ASG_WAVES", 0);
-  // (10-wave workgroups only on request until measured: VQGNN_ASG_WAVES=10)
-  const int cap10 = g.filter && wenv == 10 ? assign_capacity(g.kc, g.fused, wm, lds, 10, true) : 0;
   g.wv = cap16 * 16 > cap8 * 8 ? 16 : 8;
-  if (wenv == 8 || wenv == 16 || (wenv == 10 && g.filter)) g.wv = wenv;
+  if (wenv == 8 || wenv == 16) g.wv = wenv;
   g.lds = lds + (g.wv == 16 ? 2 * scr8 : scr8);
   // the filter's f32 codebook copy, when it fits without costing resident
   // workgroups and the sweep leaves the LDS room: at chunks above 512
@@ -829,7 +825,7 @@ static AssignGeom assign_geom(int B, int nb, int M, int W) {
   if (g.filter) {
     const size_t ef = (size_t)(g.chunk + kFltSlack) * 32;
     const int wmv = wm;
-    const int cap = g.wv == 16 ? cap16 : g.wv == 10 ? cap10 : cap8;
+    const int cap = g.wv == 16 ? cap16 : cap8;
     const int env = env_int_vq("VQGNN_FLT_ELDS", -1);
     if (g.lds + ef <= kLdsBudget && env != 0 &&
         (env == 1 || (g.chunk <= 512 &&
@@ -843,7 +839,7 @@ static AssignGeom assign_geom(int B, int nb, int M, int W) {
   const int row_blocks = (B + rows_per_iter - 1) / rows_per_iter;
   // one full round of resident workgroups: parts x nb <= what the device
   // holds at once (every part has the same row count, so no tail round)
-  const int target = env_int_vq("VQGNN_ASG_TARGET", g.wv == 16 ? cap16 : g.wv == 10 ? cap10 : cap8);
+  const int target = env_int_vq("VQGNN_ASG_TARGET", g.wv == 16 ? cap16 : cap8);
   int parts = target / nb;
   if (parts < 1) parts = 1;
   if (parts > row_blocks) parts = row_blocks;
@@ -1380,7 +1376,6 @@ __device__ __forceinline__ void transpose_quads(uint32_t (&r)[4]) {
 // swaps, VALU) hands the owner lane the four quads' minima of its row.
 template <bool FUSED, int WM, int WV>
 __global__ void __launch_bounds__(WV * 64)
-__attribute__((amdgpu_waves_per_eu(WV == 10 ? 5 : 1)))   // 10 waves: two workgroups per CU at 5/SIMD
 vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restrict__ Gr,
                  int64_t ldg, int B, int nb, int D_, int M, int W_,
                  const float* __restrict__ coef, float grad_scale,
@@ -2556,7 +2551,6 @@ static int launch_filter(const float* X, int64_t ldx, const float* G, int64_t ld
 #define FLT_LAUNCH_WV(FU, WMV)                                                                \
   do {                                                                                        \
     if (g.wv == 16) FLT_LAUNCH(FU, WMV, 16);                                                  \
-    else if (g.wv == 10) FLT_LAUNCH(FU, WMV, 10);                                             \
     else FLT_LAUNCH(FU, WMV, 8);                                                              \
   } while (0)
 #define FLT_LAUNCH_WM(FU)                                                                     \

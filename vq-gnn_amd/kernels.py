@@ -293,67 +293,6 @@ def spmm_task_plan(rowptr, col, val, n_rows, nnz, K=None):
     return TaskPlan(plan, records, K, int(nnz), int(n_rows), val, n_jobs, n_empty, rowptr)
 
 
-class HotPlan:
-    """Hot-column tile plan of a CSR for vqgnn_spmm_hot (include/vqgnn.h §6h):
-    row-aligned tiles of about Et edges, each with the (at most C) source rows
-    its edges reference most (staged in LDS by the SpMM), tasks of K edges
-    inside each tile, and per-edge records (column or LDS slot, row-end flag,
-    weight).  Built once per batch adjacency on the device, no host read;
-    valid for any F and any leading row count."""
-
-    def __init__(self, plan, records, K, Et, C, nnz, n_rows, n_cols, val, rowptr=None):
-        self.plan, self.records = plan, records
-        self.K, self.Et, self.C = K, Et, C
-        self.nnz, self.n_rows, self.n_cols = nnz, n_rows, n_cols
-        self.val_ptr = val.data_ptr() if val is not None else 0
-        self.rowptr = rowptr
-
-    def with_values(self, col, val, records=None):
-        """The same tiles, tasks and hot rows over other edge values on the
-        same structure (GAT's coefficients on the transpose): the records'
-        weights replaced (vqgnn_spmm_records_set_values)."""
-        if records is None:
-            records = torch.empty(max(self.nnz, 1), dtype=torch.int64, device=val.device)
-        check(lib().vqgnn_spmm_records_set_values(ptr(self.records), ptr(val), self.nnz,
-                                                  ptr(records), stream_ptr()),
-              "spmm_records_set_values")
-        return HotPlan(self.plan, records, self.K, self.Et, self.C, self.nnz, self.n_rows,
-                       self.n_cols, val, self.rowptr)
-
-    def tile_info(self):
-        """(tile_row [T+1], tile_task [T+1], hot_n [T], hot [T, C]) host copies
-        (tests, diagnostics)."""
-        T = -(-self.nnz // self.Et) if self.nnz > 0 else 1
-        NT = self.nnz // self.K + T + 1
-        p = self.plan.cpu()
-        o = 8
-        tile_row = p[o:o + T + 1]
-        tile_task = p[o + T + 1:o + 2 * T + 2]
-        hot_n = p[o + 2 * T + 2:o + 3 * T + 2]
-        hot_off = o + 3 * T + 2 + 2 * NT + 1
-        hot = p[hot_off:hot_off + T * self.C].view(T, self.C)
-        return tile_row, tile_task, hot_n, hot
-
-
-HOT_ET = 16384          # tile size in edges (include/vqgnn.h §6h)
-HOT_C = 1024            # hot rows per tile: 1024 x 128-byte slices = 128 KiB of LDS
-
-
-def spmm_hot_plan(rowptr, col, val, n_rows, nnz, n_cols=None, K=None, Et=None, C=None):
-    L = lib()
-    K, Et, C = int(K or TASK_K), int(Et or HOT_ET), int(HOT_C if C is None else C)
-    dev = rowptr.device
-    if n_cols is None:
-        n_cols = int(n_rows)
-    m = L.vqgnn_spmm_hot_size(int(nnz), K, Et, C)
-    plan = torch.empty(max(m, 1), dtype=torch.int32, device=dev)
-    records = torch.empty(max(int(nnz), 1), dtype=torch.int64, device=dev)
-    check(L.vqgnn_spmm_hot_plan(ptr(rowptr), ptr(col), ptr(val), int(n_rows), int(n_cols),
-                                int(nnz), K, Et, C, ptr(plan), ptr(records), stream_ptr()),
-          "spmm_hot_plan")
-    return HotPlan(plan, records, K, Et, C, int(nnz), int(n_rows), int(n_cols), val, rowptr)
-
-
 def spmm(rowptr, col, val, n_rows, nnz, X, F, X2=None, B=None, out=None, plan=None):
     """out[i] = sum_e val[e] * xin[col[e]]; xin = X rows (< B), X2 rows (>= B).
     Every column index must be < the rows of xin (X rows, or B + X2 rows)."""
@@ -383,19 +322,7 @@ def spmm(rowptr, col, val, n_rows, nnz, X, F, X2=None, B=None, out=None, plan=No
                                 _ld(out), ptr(plan.plan), ptr(plan.records), plan.K,
                                 plan.n_jobs, plan.n_empty, ptr(ws), stream_ptr()), "spmm_task")
         return out
-    if isinstance(plan, HotPlan):
-        if (val.data_ptr() if val is not None else 0) != plan.val_ptr:
-            raise ValueError("spmm: the hot plan's records hold other values than val")
-        if plan.nnz != int(nnz) or int(n_rows) > plan.n_rows:
-            raise ValueError(f"spmm: hot plan for nnz={plan.nnz}, rows={plan.n_rows}; called "
-                             f"with nnz={nnz}, n_rows={n_rows}")
-        ws = workspace(L.vqgnn_spmm_hot_workspace(int(nnz), plan.K, plan.Et, F), dev)
-        check(L.vqgnn_spmm_hot(ptr(rowptr), int(n_rows), int(n_cols), int(nnz), Bv, ptr(X),
-                               _ld(X), ptr(X2), _ld(X2) if X2 is not None else 0, F, ptr(out),
-                               _ld(out), ptr(plan.plan), ptr(plan.records), plan.K, plan.Et,
-                               plan.C, ptr(ws), stream_ptr()), "spmm_hot")
-        return out
-    raise TypeError(f"spmm: plan must be a TaskPlan or HotPlan (CSR.plan), got {type(plan)}")
+    raise TypeError(f"spmm: plan must be a TaskPlan (CSR.plan), got {type(plan)}")
 
 
 def csr_transpose(rowptr, col, val, n_rows, n_cols, nnz, want_perm=False):

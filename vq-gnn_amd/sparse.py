@@ -12,8 +12,6 @@ pass it unchanged.
 """
 from __future__ import annotations
 
-import os
-
 import torch
 
 
@@ -121,29 +119,23 @@ class CSR:
         return self._t
 
     def plan(self, F=None, B=None, n_rows=None, kind=None):
-        """SpMM plan, cached like torch_sparse's storage caches, valid for any
-        F and any leading row count (products with other values on the same
-        structure, e.g. GAT's coefficients: ``plan().with_values(col,
-        values)``):
-          kind "hot"  -- the hot-column tile plan (include/vqgnn.h §6h): the
-                         GCN/SAGE default (DEFAULT_PLAN);
-          kind "task" -- the task plan (§6), which the fused GAT kernel walks.
-        F, B and n_rows are accepted for call-site symmetry and do not change
-        the plan."""
+        """SpMM plan, cached like torch_sparse's storage caches: the task plan
+        (include/vqgnn.h §6) -- per-edge records of this CSR's values, task
+        starts and fix-up jobs, valid for any F and any leading row count
+        (products with other values on the same structure, e.g. GAT's
+        coefficients: ``plan().with_values(col, values)``).  F, B, n_rows and
+        kind are accepted for call-site symmetry and do not change the plan
+        (kind must be None or "task"; the dense-block and hot-column tile
+        plans were measured slower and removed)."""
         from . import kernels
-        kind = kind or DEFAULT_PLAN
-        if kind not in ("task", "hot"):
-            raise ValueError(f"CSR.plan: unknown kind {kind!r} (task or hot; the dense-block "
-                             "tiled path was removed, DESIGN.md §4.2b)")
-        p = self._plans.get(kind)
+        if kind not in (None, "task"):
+            raise ValueError(f"CSR.plan: unknown kind {kind!r} (only the task plan remains, "
+                             "DESIGN.md §4.2b, §4.2c)")
+        p = self._plans.get("task")
         if p is None:
-            if kind == "hot":
-                p = kernels.spmm_hot_plan(self.rowptr, self.col, self.value, self._sizes[0],
-                                          self._host_nnz, n_cols=self._sizes[1])
-            else:
-                p = kernels.spmm_task_plan(self.rowptr, self.col, self.value, self._sizes[0],
-                                           self._host_nnz)
-            self._plans[kind] = p
+            p = kernels.spmm_task_plan(self.rowptr, self.col, self.value, self._sizes[0],
+                                       self._host_nnz)
+            self._plans["task"] = p
         return p
 
     def rows(self):
@@ -155,10 +147,6 @@ class CSR:
 
     def __repr__(self):
         return f"CSR(sizes={self._sizes}, nnz={self._host_nnz}, device={self.device})"
-
-
-# the plan CSR.plan() builds when no kind is named (VQGNN_SPMM_PLAN overrides)
-DEFAULT_PLAN = os.environ.get("VQGNN_SPMM_PLAN", "task")
 
 
 def as_csr(adj) -> CSR:
