@@ -53,6 +53,15 @@ def parse():
     # kernel events inside the timed region (the roofline kernel's launches);
     # off only to measure what they cost
     p.add_argument("--no-kernel-events", action="store_true")
+    # the GCN/SAGE aggregation's out-of-batch rows from an LDS image of the
+    # codebook (kernels.spmm_codebook) where the shape allows
+    # it; --gather-rows: materialise x_first_order and run the two-source SpMM
+    p.add_argument("--gather-rows", action="store_true")
+    # one rank, codebook source: the aggregation runs before the VQ update, the
+    # reference layer's own order (the forward's aggregation, then the update
+    # in the backward hook, models.py:168-185); it reads no code or codeword
+    # the update writes.  --update-first: the multi-GPU order at N = 1.
+    p.add_argument("--update-first", action="store_true")
     return p.parse_args()
 
 
@@ -164,7 +173,12 @@ def main():
     # in the data loader): the SpMM task plan, built once per batch before the
     # timed region; its cost is reported as plan_ms
     spmm_plan = adj.plan(F, B=B)
-    plan_ms = time_plan(adj, n, nnz)
+    use_cb = (gat is None and not args.gather_rows and
+              kernels.codebook_source_ok(Xd, F, M, D) and
+              hasattr(kernels.lib(), "vqgnn_spmm_task_cb"))   # (older A/B builds lack it)
+    if use_cb:   # per batch as well: the records with out-of-batch columns -> nodes
+        spmm_plan = adj.plan_codebook(B, subset, N_graph)
+    plan_ms = time_plan(adj, n, nnz, cb=(B, subset, N_graph) if use_cb else None)
     # codebook state = one feature_update warm pass
     bank.feature_update(Xd, 0, nb, True, codes=codes, batch_idx=bidx)
     torch.cuda.synchronize()
@@ -177,14 +191,30 @@ def main():
         else:
             bank.feature_update(Xd, 0, nb, True, codes=codes, batch_idx=bidx)
 
+    # the codebook-source aggregation reads the pre-update codebook and the
+    # out-of-batch nodes' codes only (the update writes the batch nodes'), so
+    # on one rank it may run first; multi-GPU keeps update -> aggregation ->
+    # finalize, which overlaps the EMA all-reduce and the code exchange and
+    # keeps the staleness contract of DESIGN.md §6
+    # (feature_update, W = D, is the layer's init path: models.py:162-168 runs
+    # it before the gather, so its aggregation reads the updated codebook and
+    # keeps the update-first order)
+    agg_first = use_cb and world == 1 and W == 2 * D and not args.update_first
+
     def step(record):
         e = [torch.cuda.Event(enable_timing=True) for _ in range(5)] if record else None
         if record:
             e[0].record()
-        vq_update()
-        if record:
-            e[1].record()
-        aggregate(record, e)
+        if agg_first:
+            aggregate(record, e)
+            vq_update()
+            if record:
+                e[1].record()
+        else:
+            vq_update()
+            if record:
+                e[1].record()
+            aggregate(record, e)
         bank.finish_update()  # EMA finalize (multi-GPU: after the overlapped all-reduce)
         if args.graph:
             bank.sync_codes()     # a captured step joins its code exchange
@@ -195,6 +225,14 @@ def main():
             ev.append(e)
 
     def aggregate(record, e):
+        if use_cb:          # no x_first_order: the SpMM reads the codebook
+            if record:
+                e[2].record()
+            kernels.spmm_codebook(adj.rowptr, n, nnz, Xd, F, B, codes, bank.emb_out, D,
+                                  spmm_plan)
+            if record:
+                e[3].record()
+            return
         x_first, _ = kernels.gather_codewords(subset, B, codes, bank.emb_out, D)
         if record:
             e[2].record()
@@ -287,8 +325,12 @@ def main():
     value = total_edges * args.steps / dt
 
     # VQ update = BN + assign (e0 -> e1) + the deferred finalize (e3 -> e4)
-    vq_ms = float(np.mean([e[0].elapsed_time(e[1]) + e[3].elapsed_time(e[4]) for e in ev]))
-    gather_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in ev]))
+    if agg_first:     # e0 -> e2 -> e3 aggregation, e3 -> e1 update, e1 -> e4 finalize
+        vq_ms = float(np.mean([e[3].elapsed_time(e[4]) for e in ev]))
+        gather_ms = 0.0
+    else:
+        vq_ms = float(np.mean([e[0].elapsed_time(e[1]) + e[3].elapsed_time(e[4]) for e in ev]))
+        gather_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in ev]))
     spmm_ms = float(np.mean([e[2].elapsed_time(e[3]) for e in ev]))
     assign_ms = float(np.mean(assign_ms_list))
 
@@ -298,12 +340,19 @@ def main():
     #  and recomputes only the candidates);
     #  SpMM (spmm_task_kernel + spmm_task_fixup_kernel): rowptr + (col, val) + every
     #  input row once (x and x_first_order) + the output rows.
+    #  Codebook source (spmm_task_cb_kernel): the records, the B batch rows, the
+    #  out-of-batch nodes' codes (nb int16 each), the codebook's feature
+    #  halves once, the output rows; the codeword gather kernel is gone.
     spmm_bytes = 4 * (n + 1) + 8 * nnz + 4 * n * F + 4 * n * F
+    if use_cb:
+        spmm_bytes = 8 * nnz + 4 * B * F + 2 * (n - B) * nb + 4 * nb * M * D + 4 * n * F
     vq_flops = 2.0 * B * M * W * nb
     pmc, pmc_ctr, pmc_note = load_pmc(args)
     agg_name = ("gat aggregation (alpha + fused coefficient/SpMM/normalise walker)"
-                if gat is not None else "spmm_task_kernel+spmm_task_fixup_kernel")
-    agg_pmc = "spmm_task_kernel"
+                if gat is not None else
+                "spmm_task_cb_kernel+spmm_task_fixup_kernel (codebook source)" if use_cb else
+                "spmm_task_kernel+spmm_task_fixup_kernel")
+    agg_pmc = "spmm_task_cb_kernel" if use_cb else "spmm_task_kernel"
     rl_spmm = dict(kernel=agg_name, bound="hbm",
                    achieved=spmm_bytes / (spmm_ms * 1e-3) / 1e9, peak=8000.0, unit="GB/s",
                    bytes_per_launch=spmm_bytes, ms_per_launch=spmm_ms,
@@ -364,8 +413,13 @@ def main():
             dtype="f32", data="synthetic (seeded arxiv-shaped graph, random features)",
             config=dict(workload=f"{args.config}: one layer step (VQ {args.semantics} + EMA for "
                                  f"{nb} branches, "
-                                 f"codeword gather, "
-                                 f"{'GAT attention aggregation' if gat is not None else 'SpMM'})",
+                                 + ("SpMM with the out-of-batch rows read from the codebook)"
+                                    if use_cb else
+                                    "codeword gather, " +
+                                    ("GAT attention aggregation)" if gat is not None else "SpMM)")),
+                        aggregation=("codebook_source" if use_cb else "gathered_rows"),
+                        order=("aggregation, update, finalize" if agg_first else
+                               "update, aggregation, finalize"),
                         B=B, B_prime=n - B, nnz=nnz, F=F, M=M, D=D, W=W,
                         parallelism=f"dp{world}", world=world,
                         backend=(args.backend if comm is not None else None),
@@ -473,15 +527,18 @@ def assign_roofline(name, assign_ms, B, M, W, nb, f32_flops, ctr):
     return out
 
 
-def time_plan(adj, n, nnz, reps=5):
+def time_plan(adj, n, nnz, reps=5, cb=None):
     """Device time of one task-plan build (records, task starts, fix-up jobs and
-    the job-count readback), the per-batch preparation outside the timed step."""
+    the job-count readback; cb = (B, subset, nodes): plus the codebook-source
+    records), the per-batch preparation outside the timed step."""
     from vq_gnn_amd import kernels
     ts = []
     for _ in range(reps + 1):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        kernels.spmm_task_plan(adj.rowptr, adj.col, adj.value, n, nnz)
+        p = kernels.spmm_task_plan(adj.rowptr, adj.col, adj.value, n, nnz)
+        if cb is not None:
+            p.with_codebook_source(*cb)
         torch.cuda.synchronize()
         ts.append(time.perf_counter() - t0)
     return float(np.median(ts[1:])) * 1e3

@@ -272,6 +272,32 @@ int vqgnn_spmm_task(const int32_t* rowptr, int32_t n_rows, int32_t n_cols, int64
                     const int64_t* records, int32_t K, int32_t n_jobs, int32_t n_empty,
                     void* workspace, vqgnn_stream_t stream);
 
+/* 6b. Codebook-source SpMM: the layer's aggregation A @ [X ; x_first_order]
+ *    (models.py:168-174 + convs.py:95) with the out-of-batch rows read from
+ *    the codebook instead of a materialised x_first_order — row j >= B of
+ *    x_in is, for every branch b and feature d < D, emb_out[b][codes[subset[j]][b]][d]
+ *    (gather_codewords' values, include §4), served from an LDS image of the
+ *    codebook's feature halves.  Same records, fma chain and fix-up as
+ *    vqgnn_spmm_task over [X ; gather_codewords(...)]: the same output.
+ *    vqgnn_spmm_task_records_cb: copy of a plan's records (vqgnn_spmm_task_plan)
+ *      rewritten in place: a column j >= B becomes B + subset[j] (the node
+ *      whose codes give the row); requires B + n_nodes <= 2^26.
+ *    vqgnn_spmm_task_cb: out = A @ x_in for the rewritten records; codes
+ *      [n_nodes][ldc] int16 (c_indices), codewords = emb_out (branch stride
+ *      bstride, row stride ldw floats, 16-byte aligned); F a multiple of 128,
+ *      D a multiple of 4, M <= 300 (the LDS image: M x 512 bytes per 128-column
+ *      tile, vqgnn_spmm_task_cb_lds); X and out on the 32-bit near
+ *      path (else VQGNN_ERR_INVALID: use vqgnn_spmm_task).                  */
+int vqgnn_spmm_task_records_cb(int64_t* records, int64_t nnz, int32_t B, const int64_t* subset,
+                               int32_t n_cols, int64_t n_nodes, vqgnn_stream_t stream);
+size_t vqgnn_spmm_task_cb_lds(int32_t M);
+int vqgnn_spmm_task_cb(const int32_t* rowptr, int32_t n_rows, int64_t nnz, int32_t B,
+                       const float* X, int64_t ldx, int32_t F, const int16_t* codes, int64_t ldc,
+                       int64_t n_nodes, const float* codewords, int64_t ldw, int64_t bstride,
+                       int32_t M, int32_t D, float* out, int64_t ldo, const int32_t* plan,
+                       const int64_t* records_cb, int32_t K, int32_t n_jobs, int32_t n_empty,
+                       void* workspace, vqgnn_stream_t stream);
+
 /* 7. CSR transpose (structure + values) for the backward product
  *    dX = A^T dOut (torch_sparse matmul autograd, convs.py:95).  Output CSR of
  *    A^T with rows sorted by column of A; within a row, entries ordered by

@@ -1,6 +1,8 @@
 """Run one hot-path kernel a few times on a bench config's batch (PMC target).
 CONFIG=<bench config> (reddit configs build graph and batch on the device);
-argv[1]: step | vq | spmm | gat (the fused GAT aggregation of the bench)."""
+argv[1]: step | vq | spmm | gat (the fused GAT aggregation of the bench);
+GATHER_ROWS=1: the two-source SpMM over gathered rows instead of the
+codebook-source SpMM the bench runs for GCN configs."""
 import os
 import sys
 
@@ -42,6 +44,10 @@ bank = bank.to(dev)
 bank.feature_update(X, 0, nb, True, codes=codes, batch_idx=bidx)
 xt, _ = kernels.gather_codewords(subset, b.B, codes, bank.emb_out, D)
 plan = adj.plan(F, B=b.B)
+# the bench's aggregation: out-of-batch rows from the codebook where it applies
+use_cb = (what != "gat" and os.environ.get("GATHER_ROWS", "0") == "0" and
+          kernels.codebook_source_ok(X, F, M, D))
+plan_cb = adj.plan_codebook(b.B, subset, g.N) if use_cb else None
 gat = None
 if what == "gat":
     from vq_gnn_amd.convs_gat import OurGATConv
@@ -54,7 +60,9 @@ for _ in range(reps):
             gat.fused_forward(X, adj, xt, b.B)
     if what in ("vq", "step"):
         bank.update(X, G, 0, nb, True, codes=codes, batch_idx=bidx)
-    if what in ("spmm", "step"):
+    if what in ("spmm", "step") and use_cb:
+        kernels.spmm_codebook(adj.rowptr, b.n, b.nnz, X, F, b.B, codes, bank.emb_out, D, plan_cb)
+    elif what in ("spmm", "step"):
         xt, _ = kernels.gather_codewords(subset, b.B, codes, bank.emb_out, D)
         kernels.spmm(adj.rowptr, adj.col, adj.value, b.n, b.nnz, X, F, X2=xt, B=b.B, plan=plan)
 torch.cuda.synchronize()

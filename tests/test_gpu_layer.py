@@ -25,11 +25,13 @@ def _layer(F_in, F_out, M, N, conv="GCN", **kw):
                            False, **kw)
 
 
-@pytest.mark.parametrize("conv", ["GCN", "SAGE"])
-def test_layer_forward_backward_vs_oracle(conv):
+@pytest.mark.parametrize("conv,F_in", [("GCN", 32), ("SAGE", 32), ("GCN", 128), ("SAGE", 128)])
+def test_layer_forward_backward_vs_oracle(conv, F_in):
+    """F_in = 128: the aggregation reads the out-of-batch rows from the
+    codebook (CodebookInput -> kernels.spmm_codebook); 32: gathered rows."""
     torch.manual_seed(0)
     g, b = _small_batch(conv)
-    F_in, F_out, M, D = 32, 16, 64, 4
+    F_out, M, D = 16, 64, 4
     nb = F_in // D
     layer = _layer(F_in, F_out, M, g.N, conv)
     # oracle pre-state = the layer's initial state (CPU, before .to())

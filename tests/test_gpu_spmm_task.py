@@ -150,3 +150,82 @@ def test_task_plan_rejects_other_values():
     with pytest.raises(ValueError, match="other values"):
         kernels.spmm(a.rowptr, a.col, a.value * 2, 2, 3, torch.randn(2, 4, device=DEV), 4,
                      plan=plan)
+
+
+def _cb_case(rng, B, n, N, F, M, D, deg_hi=40, K=None):
+    """A layer-shaped case for the codebook-source SpMM: CSR over n = B + B'
+    rows, subset (batch nodes first), c_indices [N, nb], emb_out [nb, M, 2D]."""
+    nb = F // D
+    deg = rng.integers(0, deg_hi, size=n)
+    deg[rng.random(n) < 0.05] = 0
+    rowptr, col, val = _csr_from_deg(deg, n, rng)
+    a = _dev_csr(rowptr, col, val, n, n)
+    subset = torch.from_numpy(rng.permutation(N)[:n].astype(np.int64)).to(DEV)
+    codes = torch.from_numpy(rng.integers(0, M, size=(N, nb)).astype(np.int16)).to(DEV)
+    emb_out = torch.randn(nb, M, 2 * D, device=DEV)
+    X = torch.randn(B, F, device=DEV)
+    plan = kernels.spmm_task_plan(a.rowptr, a.col, a.value, n, a.nnz(), K)
+    return a, rowptr, col, val, subset, codes, emb_out, X, plan
+
+
+@pytest.mark.parametrize("B,n,K", [(700, 1200, 64), (0, 900, 8), (900, 900, 64), (1, 1000, 256)])
+def test_codebook_source_equals_gather_and_two_source(B, n, K):
+    """vqgnn_spmm_task_cb (include/vqgnn.h §6b) against gather_codewords +
+    the two-source task SpMM: the same records and fma chain, so the same
+    floats; and within 1e-5 of the fp64 sum.  B = 0 (every column from the
+    codebook) and B = n (none) included."""
+    rng = np.random.default_rng(B * 7 + n)
+    F, M, D, N = 128, 256, 4, 5000
+    a, rowptr, col, val, subset, codes, emb_out, X, plan = _cb_case(rng, B, n, N, F, M, D, K=K)
+    xf, _ = kernels.gather_codewords(subset, B, codes, emb_out, D)
+    if B == 0:
+        ref = kernels.spmm(a.rowptr, a.col, a.value, n, a.nnz(), xf, F, plan=plan)
+    elif B == n:
+        ref = kernels.spmm(a.rowptr, a.col, a.value, n, a.nnz(), X, F, plan=plan)
+    else:
+        ref = kernels.spmm(a.rowptr, a.col, a.value, n, a.nnz(), X, F, X2=xf, B=B, plan=plan)
+    pcb = plan.with_codebook_source(B, subset, N)
+    Xs = X if B > 0 else torch.zeros(1, F, device=DEV)
+    out = kernels.spmm_codebook(a.rowptr, n, a.nnz(), Xs, F, B, codes, emb_out, D, pcb)
+    assert torch.equal(out, ref)
+    xin = torch.cat([X, xf]).cpu().numpy()
+    _check(out, rowptr, col, val, xin)
+
+
+def test_codebook_source_arxiv_batch_and_strides():
+    """The bench batch (arxiv_gcn, M = 256, nb = 32): equal to gather +
+    two-source on a strided X and output, deterministic."""
+    cfg = dict(graph.CONFIGS["arxiv_gcn"])
+    g, _, b = graph.make_batch(cfg)
+    F, M, D = 128, cfg["M"], 4
+    nb = F // D
+    bidx, subset, adj = graph.batch_to_device(b, DEV)
+    gen = torch.Generator(device="cpu").manual_seed(11)
+    codes = torch.randint(0, M, (cfg["N"], nb + 3), dtype=torch.int16, generator=gen).to(DEV)
+    emb_out = torch.randn(nb, M, 2 * D, generator=gen).to(DEV)
+    X = torch.randn(b.B, F + 8, generator=gen).to(DEV)[:, 4:4 + F]
+    xf, _ = kernels.gather_codewords(subset, b.B, codes, emb_out, D)
+    ref = kernels.spmm(adj.rowptr, adj.col, adj.value, b.n, b.nnz, X, F, X2=xf, B=b.B,
+                       plan=adj.plan(F, B=b.B))
+    out = torch.full((b.n, F + 4), 3.0, device=DEV)[:, :F]
+    pcb = adj.plan_codebook(b.B, subset, cfg["N"])
+    kernels.spmm_codebook(adj.rowptr, b.n, b.nnz, X, F, b.B, codes, emb_out, D, pcb, out=out)
+    assert torch.equal(out, ref)
+    again = kernels.spmm_codebook(adj.rowptr, b.n, b.nnz, X, F, b.B, codes, emb_out, D, pcb)
+    assert torch.equal(again, ref)
+
+
+def test_codebook_source_rejects_unsupported():
+    rng = np.random.default_rng(3)
+    a, rowptr, col, val, subset, codes, emb_out, X, plan = _cb_case(rng, 50, 100, 300, 128, 256,
+                                                                    4)
+    pcb = plan.with_codebook_source(50, subset, 300)
+    with pytest.raises(RuntimeError, match="M=400"):
+        big = torch.randn(32, 400, 8, device=DEV)
+        kernels.spmm_codebook(a.rowptr, 100, a.nnz(), X, 128, 50, codes, big, 4, pcb)
+    with pytest.raises(ValueError, match="with_codebook_source"):
+        kernels.spmm_codebook(a.rowptr, 100, a.nnz(), X, 128, 50, codes, emb_out, 4, plan)
+    X64 = torch.randn(50, 64, device=DEV)
+    with pytest.raises(RuntimeError, match="multiple of 128"):
+        kernels.spmm_codebook(a.rowptr, 100, a.nnz(), X64, 64, 50, codes[:, :16],
+                              emb_out[:16], 4, pcb)

@@ -7,7 +7,9 @@ reduce='add')); no weight, bias or normalisation inside (convs.py:69-99 are
 commented out).  Here the product is the HIP edge-balanced SpMM, and the
 layer's input ``x_input = [x ; x_first_order]`` (models.py:168-174) may be
 passed as a ``GatheredInput`` pair so the concatenation is never copied: the
-kernel reads rows < B from x and rows >= B from x_first_order.
+kernel reads rows < B from x and rows >= B from x_first_order -- or as a
+``CodebookInput``, where x_first_order is never formed and the kernel reads
+each out-of-batch row's codewords from an LDS image of the codebook.
 """
 from __future__ import annotations
 
@@ -35,6 +37,29 @@ class GatheredInput(NamedTuple):
 
     def materialize(self):
         return torch.cat([self.x, self.x_first])
+
+
+class CodebookInput(NamedTuple):
+    """x_input = cat([x, x_first_order]) with x_first_order never formed:
+    row j >= B is the codeword feature halves of node subset[j]'s codes
+    (models.py:168-173), read by the SpMM from an LDS image of emb_out
+    (kernels.spmm_codebook, include/vqgnn.h §6b)."""
+    x: torch.Tensor
+    subset: torch.Tensor
+    codes: torch.Tensor
+    emb_out: torch.Tensor
+    D: int
+
+    def supported(self):
+        F = self.x.shape[1]
+        return (kernels.codebook_source_ok(self.x, F, self.emb_out.shape[1], self.D) and
+                hasattr(kernels.lib(), "vqgnn_spmm_task_cb"))
+
+    def gathered(self):
+        """The GatheredInput form (x_first_order materialised by the gather)."""
+        xf, _ = kernels.gather_codewords(self.subset, self.x.shape[0], self.codes,
+                                         self.emb_out, self.D)
+        return GatheredInput(self.x, xf)
 
 
 class _VQHook:
@@ -78,6 +103,23 @@ class GatherSpMMFunction(torch.autograd.Function):
             dx = kernels.spmm(at.rowptr, at.col, at.value, B, at.nnz(), dout, F,
                               plan=at.plan(F, n_rows=B))
         return dx, None, None, None, None
+
+
+class CodebookSpMMFunction(GatherSpMMFunction):
+    """GatherSpMMFunction with the out-of-batch rows read from the codebook
+    (kernels.spmm_codebook); same backward (A^T dout)[:B]."""
+
+    @staticmethod
+    def forward(ctx, x, adj, src, hook, anchor):
+        B, F = x.shape
+        n = adj.size(0)
+        xc = x if (x.stride(1) == 1 and x.stride(0) % 4 == 0 and
+                   x.data_ptr() % 16 == 0) else x.contiguous()
+        plan = adj.plan_codebook(B, src.subset, src.codes.shape[0])
+        out = kernels.spmm_codebook(adj.rowptr, n, adj.nnz(), xc, F, B, src.codes, src.emb_out,
+                                    src.D, plan)
+        ctx.adj, ctx.B, ctx.hook = adj, B, hook
+        return out
 
 
 class SpMMFunction(torch.autograd.Function):
@@ -136,6 +178,13 @@ class OurGCNConv(nn.Module):
 
     def forward(self, x, edge_index, edge_weight=None, _hook=None):
         adj = as_csr(edge_index)
+        if isinstance(x, CodebookInput):
+            if x.supported():
+                anchor = None
+                if _hook is not None and not x.x.requires_grad:
+                    anchor = torch.zeros((), device=x.x.device, requires_grad=True)
+                return CodebookSpMMFunction.apply(x.x, adj, x, _hook, anchor)
+            x = x.gathered()
         if isinstance(x, GatheredInput):
             anchor = None
             if _hook is not None and not x.x.requires_grad:
@@ -149,4 +198,4 @@ class OurGCNConv(nn.Module):
         return f"{self.__class__.__name__}({self.in_channels}, {self.out_channels})"
 
 
-__all__ = ["OurGCNConv", "GatheredInput", "CSR"]
+__all__ = ["OurGCNConv", "GatheredInput", "CodebookInput", "CSR"]

@@ -75,6 +75,16 @@ struct TaskArgs {
   int norm_B;
   float* den;               // [n_rows] optional: coefficient sums
   float* coef;              // [nnz] optional: the coefficients (for the backward)
+  // codebook source (CB): the records of columns >= B hold B + the node id,
+  // whose source row is its codewords -- column c of the row is feature
+  // c % D of codeword codes[node][c / D] of branch c / D -- read from an LDS
+  // image of the codebook's feature halves instead of a gathered row
+  const int16_t* codes;     // [nodes][ldc]
+  uint32_t codes_bytes;     // buffer range of codes (< 2^31)
+  uint32_t ldcb;            // ldc in bytes
+  const float* cbe;         // codewords: branch b, codeword m, feature d at
+  int64_t cb_ldw, cb_bstride;   //   cbe[b * cb_bstride + m * cb_ldw + d]
+  int cb_M, cb_D;
 };
 
 __device__ __forceinline__ int upper_bound_i32(const int32_t* __restrict__ a, int n, int key) {
@@ -93,6 +103,17 @@ __global__ void task_records_kernel(const int32_t* __restrict__ col, const float
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= nnz) return;
   rec[e] = make_int2(col[e] & (int)kColMask, val ? __float_as_int(val[e]) : __float_as_int(1.f));
+}
+
+// codebook-source records: a column j >= B becomes B + nodes[j] (the node
+// whose codes give the row); flags and weight kept
+__global__ void task_remap_cb_kernel(int2* __restrict__ rec, int nnz, int B,
+                                     const int64_t* __restrict__ nodes) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= nnz) return;
+  const uint32_t x = (uint32_t)rec[e].x;
+  const uint32_t j = x & kColMask;
+  if ((int)j >= B) rec[e].x = (int)((x & ~kColMask) | ((uint32_t)B + (uint32_t)nodes[j]));
 }
 
 __global__ void task_row_ends_kernel(const int32_t* __restrict__ rowptr, int n_rows,
@@ -193,8 +214,9 @@ __device__ __forceinline__ float gat_edge_coef(const TaskArgs& a, int e, uint32_
 // PART (near path): the last column tile is partial (F/4 not a multiple of
 // G*NC): its lanes past F load nothing (an offset past the buffer range
 // returns 0 without a memory access) instead of reading the next row
-template <int G, int NC, int U, bool FAR, bool GAT, bool PART>
+template <int G, int NC, int U, bool FAR, bool GAT, bool PART, bool CB = false>
 __device__ __forceinline__ void task_walk(const TaskArgs& a, int wv, int nwaves) {
+  static_assert(!CB || (G == 32 && NC == 1 && !FAR && !GAT && !PART), "CB: the default near shape");
   constexpr int TPW = 64 / G;
   const int lane = threadIdx.x & 63;
   const int g = lane / G, k = lane % G;
@@ -232,6 +254,17 @@ __device__ __forceinline__ void task_walk(const TaskArgs& a, int wv, int nwaves)
   const __amdgpu_buffer_rsrc_t rsr = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(a.rec + wbase), 0,
       (int)(uint32_t)min((int64_t)(a.nnz - wbase) * 8, (int64_t)0x7FFFFFFF), 0x00020000);
+  // CB: the codes' buffer, this lane's branch code offset, its LDS column
+  const __amdgpu_buffer_rsrc_t rsc = __builtin_amdgcn_make_buffer_rsrc(
+      CB ? (void*)a.codes : (void*)a.rec, 0, CB ? (int)a.codes_bytes : 0, 0x00020000);
+  uint32_t lane_boff = 0, lane16 = 0;
+  const char* cb_img = nullptr;
+  if constexpr (CB) {
+    extern __shared__ __attribute__((aligned(16))) char cb_smem[];
+    lane_boff = (uint32_t)((4 * c4base) / a.cb_D) * 2u;
+    lane16 = (uint32_t)k * 16u;
+    cb_img = cb_smem;
+  }
 
   float4 acc[NC];
 #pragma unroll
@@ -283,7 +316,16 @@ __device__ __forceinline__ void task_walk(const TaskArgs& a, int wv, int nwaves)
   };
   auto issue = [&](int2 rcur, int e, Blk& bk, float4 (&v)[U][NC]) {
     group_bcast<kAnd>(rcur.x, bk.cx, std::make_integer_sequence<int, U>{});
-    if constexpr (!FAR) {
+    if constexpr (CB) {
+      // X rows: the row's byte offset; codebook rows: 2^31 | the node's code
+      // row offset (bit 31 pushes either offset out of the other's range)
+      const uint32_t x = (uint32_t)rcur.x;
+      const uint32_t j = x & kColMask;
+      const bool s1 = (int)j < a.B;
+      const uint32_t roff = s1 ? __umul24(x, a.ldxb) + a.offx
+                               : 0x80000000u | __umul24(j - (uint32_t)a.B, a.ldcb);
+      group_bcast<kAnd>((int)roff, bk.co, std::make_integer_sequence<int, U>{});
+    } else if constexpr (!FAR) {
       const uint32_t x = (uint32_t)rcur.x;
       const bool s1 = (int)(x & kColMask) < a.B;
       const uint32_t roff = __umul24(x, s1 ? a.ldxb : a.ldx2b) +
@@ -291,6 +333,26 @@ __device__ __forceinline__ void task_walk(const TaskArgs& a, int wv, int nwaves)
       group_bcast<kAnd>((int)roff, bk.co, std::make_integer_sequence<int, U>{});
     }
     group_bcast<kAnd>(rcur.y, bk.cw, std::make_integer_sequence<int, U>{});
+    if constexpr (CB) {
+      // codes first (an X edge's offset is out of range: no access), then
+      // the X rows, then -- once the codes are in -- the codewords from LDS;
+      // lane k's float4 is column 4 (32 tile + k): branch (4 (32 tile + k)) / D
+      uint32_t cd[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        cd[u] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(
+            rsc, ((uint32_t)bk.co[u] ^ 0x80000000u) + lane_boff, 0, 0);
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (bk.co[u] >= 0)
+          v[u][0] = __builtin_bit_cast(
+              float4, __builtin_amdgcn_raw_buffer_load_b128(rsx, (uint32_t)bk.co[u] + lane_off, 0, 0));
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (bk.co[u] < 0)
+          v[u][0] = *reinterpret_cast<const float4*>(cb_img + (cd[u] & 0xffffu) * 512u + lane16);
+      return;
+    }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
 #pragma unroll
@@ -468,6 +530,38 @@ spmm_task_kernel(TaskArgs a) {
   const int wv = __builtin_amdgcn_readfirstlane(
       xcd_remap(blockIdx.x, gridDim.x) * (kTaskThreads / 64) + (threadIdx.x >> 6));
   task_walk<G, NC, U, FAR, GAT, PART>(a, wv, nwaves);
+}
+
+// Codebook-source task kernel: persistent 16-wave workgroups (the LDS
+// image leaves one per CU), one per CU and column tile; the workgroup stages
+// its tile's codeword features -- image row m = the 128 columns of codeword
+// m's branches, 512 B, so lane k always reads banks 4k..4k+3: conflict-free
+// whatever the codes -- and its waves walk task pairs round-robin.
+constexpr int kCbThreads = 1024;
+
+template <int U>
+__global__ void __launch_bounds__(kCbThreads) __attribute__((amdgpu_waves_per_eu(4)))
+spmm_task_cb_kernel(TaskArgs a, int nunits) {
+  extern __shared__ __attribute__((aligned(16))) char cb_smem[];
+  const int tile = blockIdx.y;
+  const int F4 = a.F >> 2;
+  for (int i = threadIdx.x; i < a.cb_M * 32; i += kCbThreads) {
+    const int m = i >> 5, c4 = tile * 32 + (i & 31);
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (c4 < F4) {
+      const int col = 4 * c4, b = col / a.cb_D, d = col % a.cb_D;
+      v = *reinterpret_cast<const float4*>(a.cbe + b * a.cb_bstride + (int64_t)m * a.cb_ldw + d);
+    }
+    *reinterpret_cast<float4*>(cb_smem + (size_t)i * 16) = v;
+  }
+  __syncthreads();
+  const int wave = threadIdx.x >> 6;
+  const int g = xcd_remap(blockIdx.x, gridDim.x);
+  const int stride = (int)gridDim.x * (kCbThreads / 64);
+  for (int u0 = g * (kCbThreads / 64); u0 < nunits; u0 += stride) {
+    const int wv = __builtin_amdgcn_readfirstlane(u0 + wave);
+    task_walk<32, 1, U, false, false, false, true>(a, wv, nunits);
+  }
 }
 
 // One wave per fix-up job.  A cut row: out[row] = tail[ts] + ... + tail[t-1]
@@ -776,6 +870,84 @@ extern "C" int vqgnn_spmm_task(const int32_t* rowptr, int32_t n_rows, int32_t n_
   if (rc != VQGNN_OK) return rc;
   task_launch<false>(a, near, as_stream(stream));
   return check_launch("spmm_task");
+}
+
+extern "C" int vqgnn_spmm_task_records_cb(int64_t* records, int64_t nnz, int32_t B,
+                                          const int64_t* nodes, int32_t n_cols, int64_t n_nodes,
+                                          vqgnn_stream_t stream) {
+  clear_error();
+  VQGNN_REQUIRE(nnz >= 0 && nnz < (int64_t)1 << 31 && B >= 0 && n_cols >= B && n_nodes >= 0,
+                "spmm_task_records_cb: bad arguments");
+  VQGNN_REQUIRE(nnz == 0 || (records && (n_cols == B || nodes)),
+                "spmm_task_records_cb: null pointer");
+  VQGNN_REQUIRE((int64_t)B + n_nodes <= (int64_t)kColMask,
+                "spmm_task_records_cb: B + %lld nodes exceed 2^26", (long long)n_nodes);
+  if (nnz > 0 && n_cols > B)
+    hipLaunchKernelGGL(task_remap_cb_kernel, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0,
+                       as_stream(stream), reinterpret_cast<int2*>(records), (int)nnz, B, nodes);
+  return check_launch("spmm_task_records_cb");
+}
+
+extern "C" size_t vqgnn_spmm_task_cb_lds(int32_t M) {
+  return M > 0 ? (size_t)M * 512 : 0;
+}
+
+extern "C" int vqgnn_spmm_task_cb(const int32_t* rowptr, int32_t n_rows, int64_t nnz, int32_t B,
+                                  const float* X, int64_t ldx, int32_t F, const int16_t* codes,
+                                  int64_t ldc, int64_t n_nodes, const float* codewords,
+                                  int64_t ldw, int64_t bstride, int32_t M, int32_t D, float* out,
+                                  int64_t ldo, const int32_t* plan, const int64_t* records_cb,
+                                  int32_t K, int32_t n_jobs, int32_t n_empty, void* workspace,
+                                  vqgnn_stream_t stream) {
+  clear_error();
+  TaskArgs a{};
+  bool near = false;
+  const int rc = task_setup(a, rowptr, n_rows, B, nnz, B, X, ldx, X, ldx, F, out, ldo, plan,
+                            records_cb, K, n_jobs, n_empty, workspace, &near);
+  if (rc != VQGNN_OK) return rc;
+  VQGNN_REQUIRE(near, "spmm_task_cb: X and out must fit the 32-bit near path");
+  VQGNN_REQUIRE(F % 128 == 0, "spmm_task_cb: F=%d must be a multiple of 128", F);
+  VQGNN_REQUIRE(D > 0 && D % 4 == 0 && F % D == 0, "spmm_task_cb: D=%d", D);
+  VQGNN_REQUIRE(M > 0 && M <= 300, "spmm_task_cb: M=%d above the LDS image (300)", M);
+  VQGNN_REQUIRE(nnz == 0 || (codes && codewords), "spmm_task_cb: null pointer");
+  VQGNN_REQUIRE(ldc >= F / D && n_nodes >= 0 && n_nodes < (1 << 24) &&
+                    n_nodes * ldc * 2 < ((int64_t)1 << 31) &&
+                    ldc * 2 < (1 << 24) && (int64_t)B + n_nodes <= (int64_t)kColMask,
+                "spmm_task_cb: codes [%lld x %lld] out of range", (long long)n_nodes,
+                (long long)ldc);
+  VQGNN_REQUIRE(ldw >= D && ldw % 4 == 0 && bstride % 4 == 0 && ((uintptr_t)codewords & 15) == 0,
+                "spmm_task_cb: codeword rows must be 16-byte aligned");
+  a.codes = codes;
+  a.codes_bytes = (uint32_t)(n_nodes * ldc * 2);
+  a.ldcb = (uint32_t)(ldc * 2);
+  a.cbe = codewords;
+  a.cb_ldw = ldw;
+  a.cb_bstride = bstride;
+  a.cb_M = M;
+  a.cb_D = D;
+  hipStream_t s = as_stream(stream);
+  if (nnz > 0) {
+    const size_t lds = vqgnn_spmm_task_cb_lds(M);
+    // U = 8 edges per block (96 VGPRs); U = 12 measured the same (77.6 against
+    // 77.7 us on the arxiv batch), U = 16 spills
+    static const bool attr_set = [] {
+      (void)hipFuncSetAttribute((const void*)spmm_task_cb_kernel<8>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      return true;
+    }();
+    (void)attr_set;
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess)
+      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipGetLastError();
+    const int nunits = (a.ntasks + 1) / 2;
+    int wgs = (nunits + kCbThreads / 64 - 1) / (kCbThreads / 64);
+    wgs = wgs < cus ? wgs : cus;
+    hipLaunchKernelGGL(spmm_task_cb_kernel<8>, dim3(wgs, F / 128), dim3(kCbThreads), lds, s, a,
+                       nunits);
+  }
+  task_fixup<false>(a, s);
+  return check_launch("spmm_task_cb");
 }
 
 extern "C" int vqgnn_gat_spmm_task(const int32_t* rowptr, int32_t n_rows, int32_t n_cols,

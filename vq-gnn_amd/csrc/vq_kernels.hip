@@ -388,8 +388,8 @@ bn_reduce_finalize_kernel(const double* __restrict__ part, int chunks, int F, in
 // blocks (a superblock), level 2 `step` superblocks (a group), level 3 the
 // groups; the tail rows and the unfinished levels are added last as
 // ((tail + acc1) + acc2) + acc3.  lp = max(4, ceil_log2(B) / 4).
-// bn_cascade_partial_kernel: one wave per (superblock, 64-column tile) — the
-// lane of column c sums its superblock's blocks in the reference's order and
+// bn_cascade_partial_kernel: four waves per (superblock, 64-column tile) — the
+// lanes of column c sum its superblock's blocks in the reference's order and
 // also accumulates P = sum (x - x0), Q = sum (x - x0)^2 in double about the
 // column's first value x0 (the variance terms, cancellation-free).
 // bn_contig_chunk_kernel: the channels-last per-thread row chunks (CONTIG
@@ -397,7 +397,8 @@ bn_reduce_finalize_kernel(const double* __restrict__ part, int chunks, int F, in
 // bn_aten_finalize_kernel: one wave per column folds the partials and runs
 // the BatchNorm update of its arithmetic.
 // ---------------------------------------------------------------------------
-constexpr int kCasWaves = 4;
+constexpr int kCasWaves = 4;       // waves per (superblock, 64-column tile)
+constexpr int kCasMaxStep = 64;    // block sums a workgroup holds (lp <= 6)
 
 __device__ __forceinline__ const float* bn_col_base(const float* X, int64_t ldx, const float* G,
                                                     int64_t ldg, int F, int c, int64_t* ld) {
@@ -405,42 +406,67 @@ __device__ __forceinline__ const float* bn_col_base(const float* X, int64_t ldx,
   return c < F ? X + c : G + (c - F);
 }
 
+// One workgroup per (superblock, tile): wave w sums blocks w, w + 4, ... of
+// the superblock (16 rows in flight per lane) into an LDS table, then wave 0
+// adds the block sums in block order -- the reference's level-1 chain, bit
+// for bit -- and the waves' fp64 (P, Q) in wave order.  Superblocks of more
+// than kCasMaxStep blocks (B > 2^27 rows) are summed by wave 0 alone.
 __global__ void __launch_bounds__(kCasWaves * 64)
 bn_cascade_partial_kernel(const float* __restrict__ X, int64_t ldx,
                           const float* __restrict__ G, int64_t ldg, int B, int F, int C,
                           int lp, int nsb, int ntiles, float* __restrict__ sb_sum,
                           double* __restrict__ sb_p, double* __restrict__ sb_q,
                           float* __restrict__ tail) {
-  const int w = blockIdx.x * kCasWaves + (threadIdx.x >> 6);
-  if (w >= nsb * ntiles) return;
-  const int sb = w / ntiles, tile = w % ntiles;
-  const int c = tile * 64 + (threadIdx.x & 63);
-  if (c >= C) return;
+  __shared__ float s_bs[kCasMaxStep][64];
+  __shared__ double s_pq[2][kCasWaves][64];
+  const int sb = blockIdx.x / ntiles, tile = blockIdx.x % ntiles;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int c = tile * 64 + lane;
+  const bool live = c < C;
   int64_t ld;
-  const float* base = bn_col_base(X, ldx, G, ldg, F, c, &ld);
+  const float* base = bn_col_base(X, ldx, G, ldg, F, live ? c : 0, &ld);
   const double x0 = (double)base[0];
   const int step = 1 << lp;
   const int nblk_all = B >> lp;
   const int nblk = min(step, nblk_all - (sb << lp));     // complete blocks in this superblock
   const int64_t r0 = (int64_t)sb << (2 * lp);
-  float acc1 = 0.f;
+  const bool split = step <= kCasMaxStep;
+  const int kstride = split ? kCasWaves : 1;
   double p = 0.0, q = 0.0;
-  for (int k = 0; k < nblk; ++k) {
-    const float* rp = base + (r0 + ((int64_t)k << lp)) * ld;
-    float bs = 0.f;
-    for (int i0 = 0; i0 < step; i0 += 16) {
-      float v[16];
+  float acc1 = 0.f;
+  if (live && (split || wave == 0)) {
+    for (int k = split ? wave : 0; k < nblk; k += kstride) {
+      const float* rp = base + (r0 + ((int64_t)k << lp)) * ld;
+      float bs = 0.f;
+      for (int i0 = 0; i0 < step; i0 += 16) {
+        float v[16];
 #pragma unroll
-      for (int u = 0; u < 16; ++u) v[u] = rp[(int64_t)(i0 + u) * ld];
+        for (int u = 0; u < 16; ++u) v[u] = rp[(int64_t)(i0 + u) * ld];
 #pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        bs = __fadd_rn(bs, v[u]);
-        const double d = (double)v[u] - x0;
-        p += d;
-        q = fma(d, d, q);
+        for (int u = 0; u < 16; ++u) {
+          bs = __fadd_rn(bs, v[u]);
+          const double d = (double)v[u] - x0;
+          p += d;
+          q = fma(d, d, q);
+        }
       }
+      if (split) s_bs[k][lane] = bs;
+      else acc1 = __fadd_rn(acc1, bs);
     }
-    acc1 = __fadd_rn(acc1, bs);
+  }
+  s_pq[0][wave][lane] = p;
+  s_pq[1][wave][lane] = q;
+  __syncthreads();
+  if (wave != 0 || !live) return;
+  if (split) {
+    for (int k = 0; k < nblk; ++k) acc1 = __fadd_rn(acc1, s_bs[k][lane]);
+    p = s_pq[0][0][lane];
+    q = s_pq[1][0][lane];
+#pragma unroll
+    for (int w = 1; w < kCasWaves; ++w) {
+      p += s_pq[0][w][lane];
+      q += s_pq[1][w][lane];
+    }
   }
   if (sb == nsb - 1) {        // the tail rows (B mod step) follow the last complete block
     float ts = 0.f;
@@ -1580,9 +1606,8 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
       const int npair = (mlim + 31) >> 5;
       const uint32_t pmask = npair > 1 ? (2u << (31 - __builtin_clz((uint32_t)npair - 1))) - 1 : 0u;
       const floatx4 zero = {0.f, 0.f, 0.f, 0.f};
-      for (int p = 0; p * 32 < mlim; ++p, ap += 512) {
-        const half8 a0 = *reinterpret_cast<const half8*>(ap);
-        const half8 a1 = *reinterpret_cast<const half8*>(ap + 256);
+      auto ld_a = [&](int off) { return *reinterpret_cast<const half8*>(ap + off); };
+      auto sweep_pair = [&](const half8 a0, const half8 a1, int p) {
         uint32_t m4[4];
         {
           floatx4 d[4];
@@ -1611,6 +1636,26 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
             cb[g] = min(mt, cb[g]);                     // equal scores: the earliest pair
           }
         }
+      };
+      // each wave loads the next pair's A fragments under this pair's MFMAs,
+      // two register sets in turn (the kFltSlack codewords past the chunk
+      // absorb the read one pair past the last).  It fits 4 waves per SIMD
+      // (<= 128 VGPRs), which is what both workgroup shapes reach anyway (2
+      // 8-wave or 1 16-wave workgroups per CU); WM 0 instances would not fit.
+      constexpr bool kPrefetchA = WM != 0;
+      if constexpr (kPrefetchA) {
+        half8 x0 = ld_a(0), x1 = ld_a(256);
+        for (int p = 0; mlim > 0; p += 2, ap += 1024) {
+          const half8 y0 = ld_a(512), y1 = ld_a(768);
+          sweep_pair(x0, x1, p);
+          if ((p + 1) * 32 >= mlim) break;
+          x0 = ld_a(1024);
+          x1 = ld_a(1280);
+          sweep_pair(y0, y1, p + 1);
+          if ((p + 2) * 32 >= mlim) break;
+        }
+      } else {
+        for (int p = 0; p * 32 < mlim; ++p, ap += 512) sweep_pair(ld_a(0), ld_a(256), p);
       }
       // ---- hand the owner lane the four quads' statistics of its row: a
       // 4 x 4 transpose over (quad, group); keys carry their quad (index order
@@ -2336,9 +2381,7 @@ extern "C" int vqgnn_bn_stats_finalize(const float* X, int64_t ldx, const float*
   w += align_up((size_t)kMaxRefThreads * C * sizeof(float), 256);
   float* cb1 = reinterpret_cast<float*>(w);
   const int ntiles = (C + 63) / 64;
-  const int waves = g.nsb * ntiles;
-  hipLaunchKernelGGL(bn_cascade_partial_kernel, dim3((waves + kCasWaves - 1) / kCasWaves),
-                     dim3(kCasWaves * 64), 0, s, X, ldx, G, ldg, B, F, C, g.lp, g.nsb, ntiles,
+  hipLaunchKernelGGL(bn_cascade_partial_kernel, dim3(g.nsb * ntiles), dim3(kCasWaves * 64), 0, s, X, ldx, G, ldg, B, F, C, g.lp, g.nsb, ntiles,
                      sb_sum, sb_p, sb_q, tail);
   int T = 1;
   if (contig) {

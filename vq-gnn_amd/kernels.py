@@ -274,6 +274,20 @@ class TaskPlan:
         return TaskPlan(self.plan, records, self.K, self.nnz, self.n_rows, val, self.n_jobs,
                         self.n_empty, self.rowptr)
 
+    def with_codebook_source(self, B, subset, n_nodes):
+        """The plan of spmm_codebook (include/vqgnn.h §6b): a copy of the
+        records whose columns j >= B name the node subset[j] (B + node id),
+        so the kernel reads that node's codes instead of an x_first row."""
+        records = self.records.clone()
+        check(lib().vqgnn_spmm_task_records_cb(ptr(records), self.nnz, int(B), ptr(subset),
+                                               int(subset.numel()), int(n_nodes), stream_ptr()),
+              "spmm_task_records_cb")
+        p = TaskPlan(self.plan, records, self.K, self.nnz, self.n_rows, None, self.n_jobs,
+                     self.n_empty, self.rowptr)
+        p.val_ptr = self.val_ptr
+        p.cb_B = int(B)
+        return p
+
 
 TASK_K = 64
 
@@ -323,6 +337,45 @@ def spmm(rowptr, col, val, n_rows, nnz, X, F, X2=None, B=None, out=None, plan=No
                                 plan.n_jobs, plan.n_empty, ptr(ws), stream_ptr()), "spmm_task")
         return out
     raise TypeError(f"spmm: plan must be a TaskPlan (CSR.plan), got {type(plan)}")
+
+
+CB_MAX_M = 300      # the codebook-source SpMM's LDS image: (M + 1) x 512 B
+
+
+def codebook_source_ok(X, F, M, D, out=None):
+    """Whether spmm_codebook serves this layer shape (include/vqgnn.h §6b)."""
+    return (F % 128 == 0 and D > 0 and D % 4 == 0 and F % D == 0 and 0 < M <= CB_MAX_M and
+            X.stride(1) == 1 and X.stride(0) % 4 == 0 and X.data_ptr() % 16 == 0)
+
+
+def spmm_codebook(rowptr, n_rows, nnz, X, F, B, codes, emb_out, D, plan_cb, out=None):
+    """out = A @ [X[:B] ; x_first_order] with x_first_order's rows (the
+    codeword feature halves of each out-of-batch node's codes, models.py:
+    168-173) read from an LDS image of emb_out (vqgnn_spmm_task_cb); plan_cb
+    from TaskPlan.with_codebook_source.  Equals spmm(..., X2=gather_codewords
+    (subset, B, codes, emb_out, D)[0], B=B)."""
+    require_gpu(X, "spmm_codebook")
+    if getattr(plan_cb, "cb_B", None) != int(B):
+        raise ValueError("spmm_codebook: plan_cb must come from TaskPlan.with_codebook_source "
+                         f"for B={B}")
+    if plan_cb.nnz != int(nnz) or int(n_rows) > plan_cb.n_rows:
+        raise ValueError(f"spmm_codebook: task plan for nnz={plan_cb.nnz}, rows={plan_cb.n_rows}; "
+                         f"called with nnz={nnz}, n_rows={n_rows}")
+    if codes.dtype != torch.int16 or emb_out.dtype != torch.float32:
+        raise TypeError("spmm_codebook: codes must be int16 and emb_out float32")
+    dev = X.device
+    if out is None:
+        out = torch.empty(n_rows, F, dtype=torch.float32, device=dev)
+    L = lib()
+    ws = workspace(L.vqgnn_spmm_task_workspace(int(nnz), plan_cb.K, F), dev)
+    M = emb_out.shape[1]
+    check(L.vqgnn_spmm_task_cb(ptr(rowptr), int(n_rows), int(nnz), int(B), ptr(X), _ld(X), F,
+                               ptr(codes), codes.stride(0), codes.shape[0], ptr(emb_out),
+                               emb_out.stride(1), emb_out.stride(0), M, int(D), ptr(out),
+                               _ld(out), ptr(plan_cb.plan), ptr(plan_cb.records), plan_cb.K,
+                               plan_cb.n_jobs, plan_cb.n_empty, ptr(ws), stream_ptr()),
+          "spmm_task_cb")
+    return out
 
 
 def csr_transpose(rowptr, col, val, n_rows, n_cols, nnz, want_perm=False):

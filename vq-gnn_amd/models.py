@@ -24,7 +24,7 @@ import torch
 import torch.nn.functional as F
 
 from . import kernels
-from .convs import GatheredInput, OurGCNConv, _VQHook
+from .convs import CodebookInput, OurGCNConv, _VQHook
 from .sparse import as_csr
 from .vq import VectorQuantizerEMA, VQBank
 
@@ -210,8 +210,12 @@ class LowRankGNNLayer(torch.nn.Module):
             for i in need:
                 self.gnn_block[i].init(x_det[:, D * i:D * (i + 1)], batch_idx)
 
-        # x_first_order (models.py:168-173): codeword feature halves of B'
-        x_first, _ = kernels.gather_codewords(subset, B, self._codes, self._bank.emb_out, D)
+        # x_first_order (models.py:168-173): codeword feature halves of B' --
+        # materialised for GAT; GCN / SAGE read them from the codebook inside
+        # the SpMM where the shape allows (CodebookInput)
+        x_first = None
+        if self.conv_type == 'GAT':
+            x_first, _ = kernels.gather_codewords(subset, B, self._codes, self._bank.emb_out, D)
 
         hook = None
         if self.vq_update_in_backward and self.training and not unlabeled and \
@@ -221,7 +225,8 @@ class LowRankGNNLayer(torch.nn.Module):
         if self.conv_type == 'GAT':
             x_output = self.conv.fused_forward(x, adj, x_first, B, hook)
         else:
-            x_output = self.conv(GatheredInput(x, x_first), adj, _hook=hook)
+            x_output = self.conv(CodebookInput(x, subset, self._codes, self._bank.emb_out, D),
+                                 adj, _hook=hook)
         # multi-GPU: the other ranks' new codes were exchanged behind the
         # gather + aggregation; land them before anything reads c_indices again
         self._bank.sync_codes()

@@ -138,6 +138,16 @@ class CSR:
             self._plans["task"] = p
         return p
 
+    def plan_codebook(self, B, subset, n_nodes):
+        """The codebook-source plan of kernels.spmm_codebook (columns >= B
+        name the node subset[j]), cached per (B, subset) like plan()."""
+        key = ("cb", int(B), subset.data_ptr(), int(n_nodes))
+        p = self._plans.get(key)
+        if p is None:
+            p = self.plan().with_codebook_source(B, subset, n_nodes)
+            self._plans[key] = p
+        return p
+
     def rows(self):
         """COO row index of every entry (int32, on the device); cached."""
         if self._rows is None:
