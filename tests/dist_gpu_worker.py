@@ -137,6 +137,10 @@ def main(out_dir):
     # collectives (no hang), the EMA statistics stay inside the fixed-point
     # row bound (finite, identical replicas), and both ranks raise together
     # at the check after the update.
+    # (the flags are read by the explicit check below, as with
+    # VQGNN_DEFER_BAD_INIT=1, not inside finish_update)
+    import vq_gnn_amd.vq as vqmod
+    strict, vqmod.STRICT_BAD_INIT = vqmod.STRICT_BAD_INIT, False
     for tag, b_over in (("over500", 500), ("over700", 700)):
         ob = fresh_bank()
         ob.comm = CodebookSync(count_group=sync.count_group, capacity=300)
@@ -157,6 +161,7 @@ def main(out_dir):
         for k in ("emb", "emb_out", "ema_w", "cs"):
             res[f"{tag}_{k}"] = getattr(ob, k).cpu().numpy()
         res[f"{tag}_codes"] = oc.cpu().numpy()
+    vqmod.STRICT_BAD_INIT = strict
     np.savez(os.path.join(out_dir, f"r{rank}.npz"), **res)
     dist.barrier()
     dist.destroy_process_group()
