@@ -57,11 +57,6 @@ def parse():
     # codebook (kernels.spmm_codebook) where the shape allows
     # it; --gather-rows: materialise x_first_order and run the two-source SpMM
     p.add_argument("--gather-rows", action="store_true")
-    # one rank, codebook source: the aggregation runs before the VQ update, the
-    # reference layer's own order (the forward's aggregation, then the update
-    # in the backward hook, models.py:168-185); it reads no code or codeword
-    # the update writes.  --update-first: the multi-GPU order at N = 1.
-    p.add_argument("--update-first", action="store_true")
     return p.parse_args()
 
 
@@ -191,30 +186,14 @@ def main():
         else:
             bank.feature_update(Xd, 0, nb, True, codes=codes, batch_idx=bidx)
 
-    # the codebook-source aggregation reads the pre-update codebook and the
-    # out-of-batch nodes' codes only (the update writes the batch nodes'), so
-    # on one rank it may run first; multi-GPU keeps update -> aggregation ->
-    # finalize, which overlaps the EMA all-reduce and the code exchange and
-    # keeps the staleness contract of DESIGN.md §6
-    # (feature_update, W = D, is the layer's init path: models.py:162-168 runs
-    # it before the gather, so its aggregation reads the updated codebook and
-    # keeps the update-first order)
-    agg_first = use_cb and world == 1 and W == 2 * D and not args.update_first
-
     def step(record):
         e = [torch.cuda.Event(enable_timing=True) for _ in range(5)] if record else None
         if record:
             e[0].record()
-        if agg_first:
-            aggregate(record, e)
-            vq_update()
-            if record:
-                e[1].record()
-        else:
-            vq_update()
-            if record:
-                e[1].record()
-            aggregate(record, e)
+        vq_update()
+        if record:
+            e[1].record()
+        aggregate(record, e)
         bank.finish_update()  # EMA finalize (multi-GPU: after the overlapped all-reduce)
         if args.graph:
             bank.sync_codes()     # a captured step joins its code exchange
@@ -325,12 +304,8 @@ def main():
     value = total_edges * args.steps / dt
 
     # VQ update = BN + assign (e0 -> e1) + the deferred finalize (e3 -> e4)
-    if agg_first:     # e0 -> e2 -> e3 aggregation, e3 -> e1 update, e1 -> e4 finalize
-        vq_ms = float(np.mean([e[3].elapsed_time(e[4]) for e in ev]))
-        gather_ms = 0.0
-    else:
-        vq_ms = float(np.mean([e[0].elapsed_time(e[1]) + e[3].elapsed_time(e[4]) for e in ev]))
-        gather_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in ev]))
+    vq_ms = float(np.mean([e[0].elapsed_time(e[1]) + e[3].elapsed_time(e[4]) for e in ev]))
+    gather_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in ev]))
     spmm_ms = float(np.mean([e[2].elapsed_time(e[3]) for e in ev]))
     assign_ms = float(np.mean(assign_ms_list))
 
@@ -418,8 +393,6 @@ def main():
                                     "codeword gather, " +
                                     ("GAT attention aggregation)" if gat is not None else "SpMM)")),
                         aggregation=("codebook_source" if use_cb else "gathered_rows"),
-                        order=("aggregation, update, finalize" if agg_first else
-                               "update, aggregation, finalize"),
                         B=B, B_prime=n - B, nnz=nnz, F=F, M=M, D=D, W=W,
                         parallelism=f"dp{world}", world=world,
                         backend=(args.backend if comm is not None else None),
