@@ -3,7 +3,8 @@ selected by VQGNN_LIB): on the arxiv bench batch, the out-of-batch rows read
 their codewords from an LDS image of the codebook instead of a gathered
 x_first row.  Checks the output against gather_codewords + the two-source
 task SpMM (same fma chain: bit-identical expected) and times both.
-Usage: VQGNN_LIB=... python scripts/spmm_cb_probe.py [reps]"""
+Usage: VQGNN_LIB=... python scripts/spmm_cb_probe.py [reps] [config] [entry]
+(entry: vqgnn_spmm_task_cb, or a variant's entry with the same arguments)"""
 import ctypes
 import os
 import sys
@@ -20,13 +21,22 @@ from vq_gnn_amd.graph import CONFIGS, batch_to_device, make_batch  # noqa: E402
 
 dev = torch.device("cuda:0")
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 30
-cfg = dict(CONFIGS["arxiv_gcn"])
+name = sys.argv[2] if len(sys.argv) > 2 else "arxiv_gcn"
+entry = sys.argv[3] if len(sys.argv) > 3 else "vqgnn_spmm_task_cb"
+cfg = dict(CONFIGS[name])
 F, M, D = cfg["F"], cfg["M"], 4
 nb = F // D
-g, _, b = make_batch(cfg)
-bidx, subset, adj = batch_to_device(b, dev)
-B, n, nnz = b.B, b.n, b.nnz
-N = cfg["N"]
+if cfg.get("device_build"):
+    from vq_gnn_amd.graph import make_batch_device
+    dg, (bidx, subset, adj) = make_batch_device(cfg, device=dev)
+    N = dg.N
+    del dg
+    B, n, nnz = int(bidx.numel()), int(subset.numel()), adj.nnz()
+else:
+    g, _, b = make_batch(cfg)
+    bidx, subset, adj = batch_to_device(b, dev)
+    B, n, nnz = b.B, b.n, b.nnz
+    N = cfg["N"]
 gen = torch.Generator(device="cpu").manual_seed(3)
 X = torch.randn(B, F, generator=gen).to(dev)
 codes = torch.randint(0, M, (N, nb), dtype=torch.int16, generator=gen).to(dev)
@@ -41,8 +51,9 @@ L.vqgnn_spmm_task_records_cb.restype = ctypes.c_int
 L.vqgnn_spmm_task_records_cb.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
                                          ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64,
                                          ctypes.c_void_p]
-L.vqgnn_spmm_task_cb.restype = ctypes.c_int
-L.vqgnn_spmm_task_cb.argtypes = ([ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_int32,
+fcb = getattr(L, entry)
+fcb.restype = ctypes.c_int
+fcb.argtypes = ([ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_int32,
                                   ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
                                   ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
                                   ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int32,
@@ -64,7 +75,7 @@ def ref():
 
 
 def cb():
-    rc = L.vqgnn_spmm_task_cb(p(adj.rowptr), n, nnz, B, p(X), F, F, p(codes), nb, N,
+    rc = fcb(p(adj.rowptr), n, nnz, B, p(X), F, F, p(codes), nb, N,
                               p(emb_out), emb_out.stride(1), emb_out.stride(0), M, D,
                               p(out_cb), F, p(plan.plan), p(rec_cb), plan.K, plan.n_jobs,
                               plan.n_empty, p(ws), stream)
@@ -96,6 +107,7 @@ def timeit(fn):
 
 
 u = os.environ.get("VQGNN_TASK_CB_U", "8")
-for name, fn in (("gather+task", ref), (f"cb U={u}", cb), ("gather+task", ref), (f"cb U={u}", cb)):
+tag = entry.replace("vqgnn_spmm_task_", "")
+for nm, fn in (("gather+task", ref), (f"{tag} U={u}", cb), ("gather+task", ref), (f"{tag} U={u}", cb)):
     t, ts = timeit(fn)
-    print(f"{name:12s} {t:7.1f} us ({', '.join(f'{x:.1f}' for x in ts)})", flush=True)
+    print(f"{name} {nm:12s} {t:8.1f} us ({', '.join(f'{x:.1f}' for x in ts)})", flush=True)
