@@ -1,6 +1,7 @@
 """Time vq_assign_kernel pieces on the arxiv batch shapes (B = 84,670,
 nb = 32, M = 256, W = 8): with / without the code scatter and the fused EMA
-statistics.  VQGNN_ASSIGN_MSWEEP (set before start) shortens the sweep."""
+statistics.  VQGNN_ASSIGN_MSWEEP (set before start) shortens the sweep;
+M=<codewords> (default 256; arxiv_gat: 1024)."""
 import os
 import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -10,7 +11,8 @@ vqgnn_pkg.load()
 from vq_gnn_amd import kernels
 
 DEV = torch.device("cuda:0")
-B, nb, M, D = 84670, 32, 256, 4
+B, nb, D = 84670, 32, 4
+M = int(os.environ.get("M", "256"))
 F = nb * D
 W = int(os.environ.get("W", "8"))
 torch.manual_seed(0)
@@ -44,5 +46,5 @@ for wc, ws in ((True, True), (False, True), (True, False), (False, False)):
         run(wc, ws)
     e1.record()
     torch.cuda.synchronize()
-    print(f"W={W} msweep={os.environ.get('VQGNN_ASSIGN_MSWEEP', 'all')} codes={wc} stats={ws}: "
+    print(f"M={M} W={W} msweep={os.environ.get('VQGNN_ASSIGN_MSWEEP', 'all')} codes={wc} stats={ws}: "
           f"{e0.elapsed_time(e1) / 10 * 1e3:.1f} us (stats: + a slab memset)", flush=True)
