@@ -229,3 +229,26 @@ def test_codebook_source_rejects_unsupported():
     with pytest.raises(RuntimeError, match="multiple of 128"):
         kernels.spmm_codebook(a.rowptr, 100, a.nnz(), X64, 64, 50, codes[:, :16],
                               emb_out[:16], 4, pcb)
+
+
+def test_codebook_plan_cache_follows_the_subset():
+    """CSR.plan_codebook caches the rewritten records per subset tensor: an
+    in-place change of the subset (or another tensor) rebuilds them."""
+    rng = np.random.default_rng(21)
+    F, M, D, N, B, n = 128, 256, 4, 3000, 300, 800
+    a, rowptr, col, val, subset, codes, emb_out, X, plan = _cb_case(rng, B, n, N, F, M, D)
+
+    def both():
+        xf, _ = kernels.gather_codewords(subset, B, codes, emb_out, D)
+        ref = kernels.spmm(a.rowptr, a.col, a.value, n, a.nnz(), X, F, X2=xf, B=B, plan=a.plan())
+        got = kernels.spmm_codebook(a.rowptr, n, a.nnz(), X, F, B, codes, emb_out, D,
+                                    a.plan_codebook(B, subset, N))
+        return ref, got
+
+    ref, got = both()
+    assert torch.equal(ref, got)
+    assert a.plan_codebook(B, subset, N) is a.plan_codebook(B, subset, N)
+    subset[B:] = torch.from_numpy(rng.permutation(N)[:n - B].astype(np.int64)).to(DEV)
+    ref2, got2 = both()
+    assert not torch.equal(ref, ref2)
+    assert torch.equal(ref2, got2)

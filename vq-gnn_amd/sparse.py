@@ -141,11 +141,15 @@ class CSR:
     def plan_codebook(self, B, subset, n_nodes):
         """The codebook-source plan of kernels.spmm_codebook (columns >= B
         name the node subset[j]), cached per (B, subset) like plan()."""
-        key = ("cb", int(B), subset.data_ptr(), int(n_nodes))
-        p = self._plans.get(key)
-        if p is None:
-            p = self.plan().with_codebook_source(B, subset, n_nodes)
-            self._plans[key] = p
+        # the entry keeps the subset tensor: a cached plan is reused only for
+        # that same tensor, unmodified (its version counter), never for new
+        # node ids that happen to sit at the same address
+        key = ("cb", int(B), int(n_nodes))
+        ent = self._plans.get(key)
+        if ent is not None and ent[0] is subset and ent[1] == subset._version:
+            return ent[2]
+        p = self.plan().with_codebook_source(B, subset, n_nodes)
+        self._plans[key] = (subset, subset._version, p)
         return p
 
     def rows(self):
