@@ -1608,32 +1608,58 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
       const floatx4 zero = {0.f, 0.f, 0.f, 0.f};
       auto ld_a = [&](int off) { return *reinterpret_cast<const half8*>(ap + off); };
       auto sweep_pair = [&](const half8 a0, const half8 a1, int p) {
-        uint32_t m4[4];
-        {
-          floatx4 d[4];
+        if constexpr (WM != 0) {
+          // both tiles' eight MFMAs issue back to back into their own
+          // accumulators, then the VALU folds them (sched_group_barrier:
+          // without it the compiler reads each MFMA's result right after it,
+          // in two accumulator sets, and waits out every MFMA's latency in
+          // s_nop).  arxiv assign -2.5 %, arxiv_gat -1..3 %, ppi -3 %
+          // (profiles/r04s_sweep_schedule_ab.txt); 121 VGPRs at 8 waves, 128
+          // at 16.
+          floatx4 d0[4], d1[4];
 #pragma unroll
-          for (int g = 0; g < 4; ++g) d[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, bop[g], zero, 0, 0, 0);
+          for (int g = 0; g < 4; ++g) d0[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, bop[g], zero, 0, 0, 0);
 #pragma unroll
-          for (int g = 0; g < 4; ++g)   // by value: clang's __builtin_bit_cast of a vector-element
-                                        // subscript reads element 0 (ROCm 7.2's clang)
-            m4[g] = min(min(__float_as_uint(d[g][0]), __float_as_uint(d[g][1])),
-                        min(__float_as_uint(d[g][2]), __float_as_uint(d[g][3])));
-        }
-        // one tile's four accumulators in flight at a time (register budget)
-        __builtin_amdgcn_sched_barrier(0);
-        {
-          floatx4 d[4];
-#pragma unroll
-          for (int g = 0; g < 4; ++g) d[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, bop[g], zero, 0, 0, 0);
+          for (int g = 0; g < 4; ++g) d1[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, bop[g], zero, 0, 0, 0);
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
-            // a chain, not a tree: two v_min3_u32 (the MFMA results are read by
-            // compiler-visible instructions, so its MFMA read hazards hold)
-            uint32_t mm = min(min(m4[g], __float_as_uint(d[g][0])), __float_as_uint(d[g][1]));
-            mm = min(min(mm, __float_as_uint(d[g][2])), __float_as_uint(d[g][3]));
+            // by value: clang's __builtin_bit_cast of a vector-element
+            // subscript reads element 0 (ROCm 7.2's clang)
+            uint32_t mm = min(min(__float_as_uint(d0[g][0]), __float_as_uint(d0[g][1])),
+                              min(__float_as_uint(d0[g][2]), __float_as_uint(d0[g][3])));
+            mm = min(min(mm, __float_as_uint(d1[g][0])), __float_as_uint(d1[g][1]));
+            mm = min(min(mm, __float_as_uint(d1[g][2])), __float_as_uint(d1[g][3]));
             const uint32_t mt = and_or_u32(mm, ~pmask, (uint32_t)p);
             s2[g] = umed3(mt, cb[g], s2[g]);            // min(s2, max(mt, cb)): cb <= s2
             cb[g] = min(mt, cb[g]);                     // equal scores: the earliest pair
+          }
+          __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);    // the 8 MFMAs first
+          __builtin_amdgcn_sched_group_barrier(0x002, 40, 0);   // then the VALU
+        } else {   // WM 0 (any W): one tile's accumulators at a time (> 128 VGPRs otherwise)
+          uint32_t m4[4];
+          {
+            floatx4 d[4];
+#pragma unroll
+            for (int g = 0; g < 4; ++g) d[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, bop[g], zero, 0, 0, 0);
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+              m4[g] = min(min(__float_as_uint(d[g][0]), __float_as_uint(d[g][1])),
+                          min(__float_as_uint(d[g][2]), __float_as_uint(d[g][3])));
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          {
+            floatx4 d[4];
+#pragma unroll
+            for (int g = 0; g < 4; ++g) d[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, bop[g], zero, 0, 0, 0);
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+              // a chain, not a tree: two v_min3_u32
+              uint32_t mm = min(min(m4[g], __float_as_uint(d[g][0])), __float_as_uint(d[g][1]));
+              mm = min(min(mm, __float_as_uint(d[g][2])), __float_as_uint(d[g][3]));
+              const uint32_t mt = and_or_u32(mm, ~pmask, (uint32_t)p);
+              s2[g] = umed3(mt, cb[g], s2[g]);
+              cb[g] = min(mt, cb[g]);
+            }
           }
         }
       };
