@@ -175,6 +175,38 @@ int vqgnn_vq_assign(const float* X, int64_t ldx, const float* G, int64_t ldg,
                     const int64_t* batch_idx, int64_t* ema_parts, int32_t ema_zeroed,
                     int64_t stat_count, void* workspace, vqgnn_stream_t stream);
 
+/* 3a. The assign with the BatchNorm finalize folded into its prologue
+ *     (single process, FP64 / STRIDED arithmetic): vqgnn_bn_stats_partial is
+ *     vqgnn_bn_stats_finalize's statistics pass alone (its workspace:
+ *     vqgnn_bn_stats_workspace(B, F)); vqgnn_vq_assign_bn takes that
+ *     workspace and the finalize's parameters (as vqgnn_bn_stats_finalize;
+ *     with_grad = (W == 2D), F = nb * D) in place of coef.  Every workgroup
+ *     of branch b folds b's columns itself -- the finalize kernel's arithmetic,
+ *     bit for bit -- and the first row part's workgroups update the running
+ *     statistics and num_batches_tracked and write coef / batch_out, so the
+ *     results equal vqgnn_bn_stats_finalize + vqgnn_vq_assign with one launch
+ *     fewer.  The columns' arithmetic is that call's cascade form: at least
+ *     one half STRIDED (all-FP64 statistics take the fp64-sum path there, and
+ *     are rejected here); CONTIG has no fold.
+ *     vqgnn_vq_assign_bn_supported says whether a shape has the fold
+ *     (the filter path, W <= 8, B <= 2^23, and the fold's scratch within the
+ *     codebook planes' LDS).                                                   */
+int32_t vqgnn_vq_assign_bn_supported(int32_t B, int32_t nb, int32_t D, int32_t M, int32_t W);
+int vqgnn_bn_stats_partial(const float* X, int64_t ldx, const float* G, int64_t ldg,
+                           int32_t B, int32_t F, int32_t with_grad, void* workspace,
+                           vqgnn_stream_t stream);
+int vqgnn_vq_assign_bn(const float* X, int64_t ldx, const float* G, int64_t ldg,
+                       int32_t B, int32_t nb, int32_t D, int32_t M, int32_t W,
+                       float grad_scale, const float* embedding, int32_t ldw,
+                       int64_t emb_bstride, int64_t* idx_out, int16_t* codes, int64_t ldc,
+                       const int64_t* batch_idx, int64_t* ema_parts, int32_t ema_zeroed,
+                       int64_t stat_count, void* workspace, const void* bn_workspace,
+                       int32_t mode, int32_t arith_x, int32_t arith_g, double momentum_f,
+                       double eps_f, double momentum_g, double eps_g, double eps_std,
+                       float* rm_f, float* rv_f, float* rm_g, float* rv_g, float* coef,
+                       float* batch_out, int64_t* nbt_f, int64_t* nbt_g, int32_t nbt_d,
+                       vqgnn_stream_t stream);
+
 /* 3b. Fold P partial slabs into one: out[i] = sum_p parts[p][i] (exact).
  *     Multi-GPU callers fold, then all-reduce (sum) the single int64 slab.    */
 int vqgnn_vq_ema_reduce(const int64_t* parts, int32_t nparts, int64_t part_elems,

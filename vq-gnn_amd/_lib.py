@@ -46,6 +46,16 @@ SIGNATURES = {
                                        _i32, _i32, _c_void_p, _f32, _c_void_p, _i32, _i64,
                                        _c_void_p, _c_void_p, _i64, _c_void_p, _c_void_p,
                                        _i32, _i64, _c_void_p, _c_void_p]),
+    "vqgnn_vq_assign_bn_supported": (_i32, [_i32, _i32, _i32, _i32, _i32]),
+    "vqgnn_bn_stats_partial": (ctypes.c_int, [_c_void_p, _i64, _c_void_p, _i64, _i32, _i32, _i32,
+                                              _c_void_p, _c_void_p]),
+    "vqgnn_vq_assign_bn": (ctypes.c_int, [_c_void_p, _i64, _c_void_p, _i64, _i32, _i32, _i32,
+                                          _i32, _i32, _f32, _c_void_p, _i32, _i64, _c_void_p,
+                                          _c_void_p, _i64, _c_void_p, _c_void_p, _i32, _i64,
+                                          _c_void_p, _c_void_p, _i32, _i32, _i32, _f64, _f64,
+                                          _f64, _f64, _f64, _c_void_p, _c_void_p, _c_void_p,
+                                          _c_void_p, _c_void_p, _c_void_p, _c_void_p,
+                                          _c_void_p, _i32, _c_void_p]),
     "vqgnn_vq_ema_finalize": (ctypes.c_int, [_c_void_p, _i32, _i32, _i64, _i32, _i32, _i32, _i32,
                                              _i32, _f32,
                                              _i32, _f32, _f32, _c_void_p, _i64, _c_void_p,

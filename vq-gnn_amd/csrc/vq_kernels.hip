@@ -513,16 +513,16 @@ bn_contig_chunk_kernel(const float* __restrict__ X, int64_t ldx, const float* __
   buf[(int64_t)t * C + c] = s;
 }
 
-__global__ void __launch_bounds__(64)
-bn_aten_finalize_kernel(const float* __restrict__ X, int64_t ldx, const float* __restrict__ G,
-                        int64_t ldg, int B, int F, int C, int lp, int nsb,
-                        const float* __restrict__ sb_sum, const double* __restrict__ sb_p,
-                        const double* __restrict__ sb_q, const float* __restrict__ tail,
-                        int T, const float* __restrict__ cbuf0, const float* __restrict__ cbuf1,
-                        BnArgs a) {
-  extern __shared__ float sbs[];          // [nsb] superblock sums of this column, then
-                                          // [nsb >> lp] level-2 group sums
-  const int c = blockIdx.x, lane = threadIdx.x;
+// The finalize's fold of one column c, in three phases separated by the
+// caller's barriers (bn_aten_finalize_kernel: a one-wave block; the fused
+// assign prologue of vq_filter_kernel: one wave per k slot).  sbs is the
+// column's LDS scratch: [nsb] superblock sums, then [nsb >> lp] group sums.
+// Phase 1 (every lane): the superblock sums into sbs, the fp64 (P, Q) summed
+// over the lanes by a fixed butterfly (every lane ends with the totals).
+__device__ __forceinline__ void bn_fold_load(int c, int nsb, const float* __restrict__ sb_sum,
+                                             const double* __restrict__ sb_p,
+                                             const double* __restrict__ sb_q, float* sbs,
+                                             int lane, double* pp, double* qq) {
   const int64_t o = (int64_t)c * nsb;
   double p = 0.0, q = 0.0;
   for (int i = lane; i < nsb; i += 64) {
@@ -535,26 +535,39 @@ bn_aten_finalize_kernel(const float* __restrict__ X, int64_t ldx, const float* _
     p += __shfl_xor(p, off);
     q += __shfl_xor(q, off);
   }
-  __syncthreads();
+  *pp = p;
+  *qq = q;
+}
+
+// Phase 2 (every lane): the level-2 group sums, one lane per group
+__device__ __forceinline__ void bn_fold_groups(int B, int lp, int nsb, float* sbs, int lane) {
   const int step = 1 << lp;
   const int nblk = B >> lp, nsb_full = nblk >> lp, ngr = nsb_full >> lp;
-  float* grp = sbs + nsb;                 // [ngr] level-2 group sums, one lane each
+  float* grp = sbs + nsb;
   for (int gi = lane; gi < ngr; gi += 64) {
     float acc2 = 0.f;
     for (int k = 0; k < step; ++k) acc2 = __fadd_rn(acc2, sbs[gi * step + k]);
     grp[gi] = acc2;
   }
-  __syncthreads();
-  if (lane != 0) return;
+}
+
+// Phase 3 (one lane): the cascade total ((tail + acc1) + acc2) + acc3 and the
+// column's statistics in its arithmetic
+__device__ __forceinline__ BnCol bn_fold_stats(const float* X, int64_t ldx, const float* G,
+                                               int64_t ldg, int B, int F, int C, int lp, int nsb,
+                                               const float* sbs, const float* __restrict__ tail,
+                                               int T, const float* __restrict__ cbuf0,
+                                               const float* __restrict__ cbuf1, int c, int arith,
+                                               double p, double q) {
+  const int step = 1 << lp;
+  const int nblk = B >> lp, nsb_full = nblk >> lp, ngr = nsb_full >> lp;
+  const float* grp = sbs + nsb;
   float acc3 = 0.f;
   for (int gi = 0; gi < ngr; ++gi) acc3 = __fadd_rn(acc3, grp[gi]);
   float acc2 = 0.f;
   for (int k = ngr * step; k < nsb_full; ++k) acc2 = __fadd_rn(acc2, sbs[k]);
   const float acc1 = nsb_full < nsb ? sbs[nsb_full] : 0.f;
   const float total = __fadd_rn(__fadd_rn(__fadd_rn(tail[c], acc1), acc2), acc3);
-  const bool g = c >= F;
-  const int k = g ? c - F : c;
-  const int arith = g ? a.arith_g : a.arith_x;
   int64_t ld;
   const double x0 = (double)bn_col_base(X, ldx, G, ldg, F, c, &ld)[0];
   const double nd = (double)B;
@@ -581,7 +594,50 @@ bn_aten_finalize_kernel(const float* __restrict__ X, int64_t ldx, const float* _
     st.mean = (float)md;
     st.var_sum = vs_exact;
   }
+  return st;
+}
+
+__global__ void __launch_bounds__(64)
+bn_aten_finalize_kernel(const float* __restrict__ X, int64_t ldx, const float* __restrict__ G,
+                        int64_t ldg, int B, int F, int C, int lp, int nsb,
+                        const float* __restrict__ sb_sum, const double* __restrict__ sb_p,
+                        const double* __restrict__ sb_q, const float* __restrict__ tail,
+                        int T, const float* __restrict__ cbuf0, const float* __restrict__ cbuf1,
+                        BnArgs a) {
+  extern __shared__ float sbs[];
+  const int c = blockIdx.x, lane = threadIdx.x;
+  double p, q;
+  bn_fold_load(c, nsb, sb_sum, sb_p, sb_q, sbs, lane, &p, &q);
+  __syncthreads();
+  bn_fold_groups(B, lp, nsb, sbs, lane);
+  __syncthreads();
+  if (lane != 0) return;
+  const bool g = c >= F;
+  const int k = g ? c - F : c;
+  const int arith = g ? a.arith_g : a.arith_x;
+  const BnCol st = bn_fold_stats(X, ldx, G, ldg, B, F, C, lp, nsb, sbs, tail, T, cbuf0, cbuf1, c,
+                                 arith, p, q);
   bn_emit(a, F, g, k, st, true, (int64_t)B);
+}
+
+// The finalize folded into vq_filter_kernel's prologue (single-process
+// BatchNorm of the cascade arithmetic): the partials of
+// bn_cascade_partial_kernel and the finalize's parameters.  Every workgroup
+// of branch b folds b's k-slot columns itself; part 0's workgroups are the
+// owners that update the running statistics, num_batches_tracked, the
+// coefficient table and the batch stash, exactly as bn_aten_finalize_kernel.
+struct BnFold {
+  const float* sb_sum;
+  const double* sb_p;
+  const double* sb_q;
+  const float* tail;
+  int lp, nsb, C;
+  BnArgs a;
+};
+
+// LDS scratch of the fold: W columns of nsb + ngr floats (+1 for alignment)
+static inline size_t bn_fold_scratch(int nsb, int lp, int W) {
+  return (size_t)W * (size_t)(nsb + (nsb >> lp) + 1) * sizeof(float);
 }
 
 // ---------------------------------------------------------------------------
@@ -715,7 +771,8 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
                  int64_t* __restrict__ idx_out, int16_t* __restrict__ codes, int64_t ldc,
                  const int64_t* __restrict__ batch_idx, int* __restrict__ idx32,
                  unsigned long long* __restrict__ partial, int* __restrict__ flags,
-                 int rows_per_part, int chunk, int shift_f, int shift_g, int m_sweep, int elds);
+                 int rows_per_part, int chunk, int shift_f, int shift_g, int m_sweep, int elds,
+                 BnFold fold);
 
 // the filter's row-load mode: 2 -> W = 8 = 2D, D = 4; 1 -> W = D = 4 (float4
 // rows, aligned); 0 -> general
@@ -1409,7 +1466,8 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
                  int64_t* __restrict__ idx_out, int16_t* __restrict__ codes, int64_t ldc,
                  const int64_t* __restrict__ batch_idx, int* __restrict__ idx32,
                  unsigned long long* __restrict__ partial, int* __restrict__ flags,
-                 int rows_per_part, int chunk, int shift_f, int shift_g, int m_sweep, int elds) {
+                 int rows_per_part, int chunk, int shift_f, int shift_g, int m_sweep, int elds,
+                 BnFold fold) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int NT = WV * 64;
   const int W = WM == 2 ? 8 : (WM == 1 ? 4 : W_);          // compile-time in the row modes
@@ -1444,7 +1502,55 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
     s_nflag = 0;
     s_bigmin = 0x7f800000u;                           // +inf: no out-of-range codeword
   }
-  if (tid < 8) {
+  if (fold.sb_sum) {
+    // the BatchNorm finalize of this branch's W columns, one wave per k slot
+    // (the finalize kernel's phases, bit for bit), in the planes' LDS before
+    // they are staged; part 0's workgroup is the owner of the state updates
+    const int percol = fold.nsb + (fold.nsb >> fold.lp) + 1;
+    const bool fw = wave < W;
+    const int k = fw ? wave : 0;
+    const bool gk = W != D && k >= D;
+    const int col = b * D + (gk ? k - D : k);
+    const int c = gk ? F + col : col;
+    float* sbs = reinterpret_cast<float*>(lds) + (size_t)k * percol;
+    double p = 0.0, qq = 0.0;
+    if (fw) bn_fold_load(c, fold.nsb, fold.sb_sum, fold.sb_p, fold.sb_q, sbs, lane, &p, &qq);
+    __syncthreads();
+    if (fw) bn_fold_groups(B, fold.lp, fold.nsb, sbs, lane);
+    __syncthreads();
+    if (fw && lane == 0) {
+      const BnArgs& ba = fold.a;
+      const int arith = gk ? ba.arith_g : ba.arith_x;
+      const BnCol st = bn_fold_stats(X, ldx, Gr, ldg, B, F, fold.C, fold.lp, fold.nsb, sbs,
+                                     fold.tail, 1, nullptr, nullptr, c, arith, p, qq);
+      float al, be, sh;
+      if (part == 0) {
+        bn_emit(ba, F, gk ? 1 : 0, col, st, true, (int64_t)B);
+        const int o = gk ? 2 * F : 0;            // this thread's own stores, read back
+        al = ba.coef[o + col];
+        be = ba.coef[o + F + col];
+        sh = ba.coef[(gk ? 5 * F : 4 * F) + col];
+      } else {
+        // the same column arithmetic into registers; the running statistics
+        // are read only by the eval form (mode 0), which nothing writes
+        float rm = 0.f, rv = 0.f;
+        if (ba.mode == 0) {
+          rm = (gk ? ba.rm_g : ba.rm_f)[col];
+          rv = (gk ? ba.rv_g : ba.rv_f)[col];
+        }
+        bn_column(st, true, (int64_t)B, ba.mode, arith, gk ? ba.mom_g : ba.mom_f,
+                  gk ? ba.eps_g : ba.eps_f, ba.eps_std, &rm, &rv, &al, &be, &sh, nullptr,
+                  nullptr);
+      }
+      s_kt[0][k] = al;
+      s_kt[1][k] = be;
+      s_kt[2][k] = sh;
+    }
+    if (tid < 8) {
+      if (tid >= W) s_kt[0][tid] = s_kt[1][tid] = s_kt[2][tid] = 0.f;
+      s_kt[3][tid] = (W != D && tid >= D) ? grad_scale : 1.f;
+    }
+  } else if (tid < 8) {
     const int k = tid;
     const bool kvv = k < W;
     const bool gk = W != D && k >= D;
@@ -1832,9 +1938,9 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
         const bool gk = W != D && k >= D;
         const int c = b * D + (gk ? k - D : k);
         const float raw = gk ? Gr[(int64_t)row * ldg + c] : X[(int64_t)row * ldx + c];
-        v = __fmul_rn(fmaf(__fsub_rn(raw, coef[(gk ? 5 * F : 4 * F) + c]),
-                           coef[(gk ? 2 * F : 0) + c], coef[(gk ? 3 * F : F) + c]),
-                      gk ? grad_scale : 1.f);
+        // the k-slot table (with the BatchNorm fold, coef is written by part
+        // 0's workgroups of this same launch: only s_kt is this one's)
+        v = __fmul_rn(fmaf(__fsub_rn(raw, s_kt[2][k]), s_kt[0][k], s_kt[1][k]), s_kt[3][k]);
         sxr = (k == 0) ? __fmul_rn(v, v) : __fadd_rn(sxr, __fmul_rn(v, v));
       }
       xv[k] = v;
@@ -2251,6 +2357,43 @@ static size_t aten_ws_bytes(int B, int F) {
   return s;
 }
 
+// the cascade arithmetic's workspace: superblock sums, fp64 (P, Q), tails,
+// the CONTIG chunk buffers
+struct CascadeWs {
+  float* sb_sum;
+  double* sb_p;
+  double* sb_q;
+  float* tail;
+  float* cb0;
+  float* cb1;
+};
+
+static CascadeWs cascade_ws(void* workspace, int C, const CascadeGeom& g) {
+  CascadeWs ws;
+  char* w = reinterpret_cast<char*>(workspace);
+  ws.sb_sum = reinterpret_cast<float*>(w);
+  w += align_up((size_t)C * g.nsb * sizeof(float), 256);
+  ws.sb_p = reinterpret_cast<double*>(w);
+  w += align_up((size_t)C * g.nsb * sizeof(double), 256);
+  ws.sb_q = reinterpret_cast<double*>(w);
+  w += align_up((size_t)C * g.nsb * sizeof(double), 256);
+  ws.tail = reinterpret_cast<float*>(w);
+  w += align_up((size_t)C * sizeof(float), 256);
+  ws.cb0 = reinterpret_cast<float*>(w);
+  w += align_up((size_t)kMaxRefThreads * C * sizeof(float), 256);
+  ws.cb1 = reinterpret_cast<float*>(w);
+  return ws;
+}
+
+static void launch_cascade_partial(const float* X, int64_t ldx, const float* G, int64_t ldg,
+                                   int B, int F, int C, const CascadeGeom& g, const CascadeWs& ws,
+                                   hipStream_t s) {
+  const int ntiles = (C + 63) / 64;
+  hipLaunchKernelGGL(bn_cascade_partial_kernel, dim3(g.nsb * ntiles), dim3(kCasWaves * 64), 0, s,
+                     X, ldx, G, ldg, B, F, C, g.lp, g.nsb, ntiles, ws.sb_sum, ws.sb_p, ws.sb_q,
+                     ws.tail);
+}
+
 extern "C" size_t vqgnn_bn_stats_workspace(int32_t B, int32_t F) {
   return std::max(fp64_ws_bytes(B, F), aten_ws_bytes(B, F));
 }
@@ -2394,21 +2537,14 @@ extern "C" int vqgnn_bn_stats_finalize(const float* X, int64_t ldx, const float*
   }
   VQGNN_REQUIRE(sums == nullptr, "bn_stats_finalize: fp64 sums exist only for the FP64 arithmetic");
   const CascadeGeom g = cascade_geom(B);
-  char* w = reinterpret_cast<char*>(workspace);
-  float* sb_sum = reinterpret_cast<float*>(w);
-  w += align_up((size_t)C * g.nsb * sizeof(float), 256);
-  double* sb_p = reinterpret_cast<double*>(w);
-  w += align_up((size_t)C * g.nsb * sizeof(double), 256);
-  double* sb_q = reinterpret_cast<double*>(w);
-  w += align_up((size_t)C * g.nsb * sizeof(double), 256);
-  float* tail = reinterpret_cast<float*>(w);
-  w += align_up((size_t)C * sizeof(float), 256);
-  float* cb0 = reinterpret_cast<float*>(w);
-  w += align_up((size_t)kMaxRefThreads * C * sizeof(float), 256);
-  float* cb1 = reinterpret_cast<float*>(w);
-  const int ntiles = (C + 63) / 64;
-  hipLaunchKernelGGL(bn_cascade_partial_kernel, dim3(g.nsb * ntiles), dim3(kCasWaves * 64), 0, s, X, ldx, G, ldg, B, F, C, g.lp, g.nsb, ntiles,
-                     sb_sum, sb_p, sb_q, tail);
+  const CascadeWs ws = cascade_ws(workspace, C, g);
+  float* sb_sum = ws.sb_sum;
+  double* sb_p = ws.sb_p;
+  double* sb_q = ws.sb_q;
+  float* tail = ws.tail;
+  float* cb0 = ws.cb0;
+  float* cb1 = ws.cb1;
+  launch_cascade_partial(X, ldx, G, ldg, B, F, C, g, ws, s);
   int T = 1;
   if (contig) {
     // at::parallel_for(0, B, 1): min(T, B) threads of ceil(B / threads) rows
@@ -2583,11 +2719,12 @@ static int launch_filter(const float* X, int64_t ldx, const float* G, int64_t ld
                          const float* emb, int ldw, int64_t emb_bstride, int64_t* idx_out,
                          int16_t* codes, int64_t ldc, const int64_t* batch_idx,
                          unsigned long long* parts, int ema_zeroed, int64_t stat_count,
-                         void* workspace, hipStream_t s) {
+                         void* workspace, hipStream_t s, const BnFold* bn_fold = nullptr) {
   const AssignGeom g = assign_geom(B, nb, M, W);
   const StatShift sh = stat_shift(stat_count, grad_scale);
   const bool want_ema = parts != nullptr;
   const bool fused = want_ema && g.fused;
+  const BnFold fold = bn_fold ? *bn_fold : BnFold{};
   int* idx32 = (want_ema && !g.fused) ? reinterpret_cast<int*>(workspace) : nullptr;
   int* flags = reinterpret_cast<int*>(reinterpret_cast<char*>(workspace) + idx32_bytes(g, B, nb));
   // the geometry sized the slab in when the EMA statistics fuse; without
@@ -2615,7 +2752,7 @@ static int launch_filter(const float* X, int64_t ldx, const float* G, int64_t ld
                           (uint32_t)lds, s, ev0, ev1, 0, X, ldx, G, ldg, B, nb, D, M, W,       \
                           coef, grad_scale, emb, ldw, emb_bstride, idx_out, codes, ldc,        \
                           batch_idx, idx32, parts, flags, g.rows_per_part, g.chunk, sh.f,      \
-                          sh.g, m_sweep, g.elds);                                              \
+                          sh.g, m_sweep, g.elds, fold);                                        \
   } while (0)
 #define FLT_LAUNCH_WV(FU, WMV)                                                                \
   do {                                                                                        \
@@ -2637,6 +2774,12 @@ static int launch_filter(const float* X, int64_t ldx, const float* G, int64_t ld
   return launch_ema_tail(X, ldx, G, ldg, B, nb, D, M, W, coef, grad_scale, idx32, parts, g, sh, s);
 }
 
+static int assign_check(const float* X, int64_t ldx, const float* G, int64_t ldg, int32_t B,
+                        int32_t nb, int32_t D, int32_t M, int32_t W, const float* embedding,
+                        int32_t ldw, int64_t emb_bstride, int16_t* codes, int64_t ldc,
+                        const int64_t* batch_idx, int64_t* ema_parts, int64_t stat_count,
+                        void* workspace);
+
 extern "C" int vqgnn_vq_assign(const float* X, int64_t ldx, const float* G, int64_t ldg,
                                int32_t B, int32_t nb, int32_t D, int32_t M, int32_t W,
                                const float* coef, float grad_scale, const float* embedding,
@@ -2645,21 +2788,10 @@ extern "C" int vqgnn_vq_assign(const float* X, int64_t ldx, const float* G, int6
                                int64_t* ema_parts, int32_t ema_zeroed, int64_t stat_count,
                                void* workspace, vqgnn_stream_t stream) {
   clear_error();
-  VQGNN_REQUIRE(X && coef && embedding, "vq_assign: null pointer");
-  VQGNN_REQUIRE(B > 0 && nb > 0 && D > 0 && M > 0, "vq_assign: bad shape");
-  VQGNN_REQUIRE(W == D || W == 2 * D, "vq_assign: W must be D or 2D (W=%d D=%d)", W, D);
-  VQGNN_REQUIRE(W <= 16, "vq_assign: W=%d > 16 not implemented", W);
-  VQGNN_REQUIRE(ldx >= (int64_t)nb * D, "vq_assign: ldx too small");
-  VQGNN_REQUIRE(W == D || (G && ldg >= (int64_t)nb * D), "vq_assign: grads required for W=2D");
-  VQGNN_REQUIRE(ldw >= W && emb_bstride >= (int64_t)M * ldw, "vq_assign: bad codebook layout");
-  VQGNN_REQUIRE(!codes || (batch_idx && ldc >= nb), "vq_assign: codes needs batch_idx, ldc>=nb");
-  VQGNN_REQUIRE(workspace || (!ema_parts && !use_filter(W)),
-                "vq_assign: workspace required (vqgnn_vq_assign_workspace)");
-  VQGNN_REQUIRE(M <= 32767 || !codes, "vq_assign: int16 codes need M <= 32767");
-  VQGNN_REQUIRE(!ema_parts || stat_count >= B, "vq_assign: stat_count < B");
-  VQGNN_REQUIRE((int64_t)B * ldx * 4 < ((int64_t)1 << 32) &&
-                    (!G || (int64_t)B * ldg * 4 < ((int64_t)1 << 32)),
-                "vq_assign: B*ldx (and B*ldg) must span < 4 GiB");
+  VQGNN_REQUIRE(coef, "vq_assign: null pointer");
+  const int rc = assign_check(X, ldx, G, ldg, B, nb, D, M, W, embedding, ldw, emb_bstride, codes,
+                              ldc, batch_idx, ema_parts, stat_count, workspace);
+  if (rc != VQGNN_OK) return rc;
   hipStream_t s = as_stream(stream);
   unsigned long long* parts = reinterpret_cast<unsigned long long*>(ema_parts);
   if (use_filter(W))
@@ -2678,6 +2810,106 @@ extern "C" int vqgnn_vq_assign(const float* X, int64_t ldx, const float* G, int6
   return launch_assign<4>(X, ldx, G, ldg, B, nb, D, M, W, coef, grad_scale, embedding, ldw,
                           emb_bstride, idx_out, codes, ldc, batch_idx, parts, ema_zeroed, stat_count,
                           workspace, s);
+}
+
+extern "C" int32_t vqgnn_vq_assign_bn_supported(int32_t B, int32_t nb, int32_t D, int32_t M,
+                                                int32_t W) {
+  if (B <= 1 || B > (1 << 23) || nb <= 0 || D <= 0 || M <= 0 || !(W == D || W == 2 * D) ||
+      !use_filter(W))
+    return 0;
+  const AssignGeom g = assign_geom(B, nb, M, W);
+  const CascadeGeom cg = cascade_geom(B);
+  // the fold's scratch lives in the codebook planes' LDS before they are staged
+  return bn_fold_scratch(cg.nsb, cg.lp, W) <= (size_t)kFltBytesPerCode * (g.chunk + kFltSlack)
+             ? 1 : 0;
+}
+
+extern "C" int vqgnn_bn_stats_partial(const float* X, int64_t ldx, const float* G, int64_t ldg,
+                                      int32_t B, int32_t F, int32_t with_grad, void* workspace,
+                                      vqgnn_stream_t stream) {
+  clear_error();
+  VQGNN_REQUIRE(X && workspace, "bn_stats_partial: null pointer");
+  VQGNN_REQUIRE(B > 0 && F > 0 && ldx >= F, "bn_stats_partial: bad shape B=%d F=%d", B, F);
+  VQGNN_REQUIRE(B <= (1 << 23), "bn_stats_partial: B=%d rows exceed 2^23", B);
+  VQGNN_REQUIRE(!with_grad || (G && ldg >= F), "bn_stats_partial: grads required");
+  const int C = with_grad ? 2 * F : F;
+  const CascadeGeom g = cascade_geom(B);
+  launch_cascade_partial(X, ldx, G, ldg, B, F, C, g, cascade_ws(workspace, C, g),
+                         as_stream(stream));
+  return check_launch("bn_stats_partial");
+}
+
+extern "C" int vqgnn_vq_assign_bn(const float* X, int64_t ldx, const float* G, int64_t ldg,
+                                  int32_t B, int32_t nb, int32_t D, int32_t M, int32_t W,
+                                  float grad_scale, const float* embedding, int32_t ldw,
+                                  int64_t emb_bstride, int64_t* idx_out, int16_t* codes,
+                                  int64_t ldc, const int64_t* batch_idx, int64_t* ema_parts,
+                                  int32_t ema_zeroed, int64_t stat_count, void* workspace,
+                                  const void* bn_workspace, int32_t mode, int32_t arith_x,
+                                  int32_t arith_g, double momentum_f, double eps_f,
+                                  double momentum_g, double eps_g, double eps_std, float* rm_f,
+                                  float* rv_f, float* rm_g, float* rv_g, float* coef,
+                                  float* batch_out, int64_t* nbt_f, int64_t* nbt_g,
+                                  int32_t nbt_d, vqgnn_stream_t stream) {
+  clear_error();
+  const int rc = assign_check(X, ldx, G, ldg, B, nb, D, M, W, embedding, ldw, emb_bstride, codes,
+                              ldc, batch_idx, ema_parts, stat_count, workspace);
+  if (rc != VQGNN_OK) return rc;
+  const bool with_grad = W == 2 * D;
+  VQGNN_REQUIRE(vqgnn_vq_assign_bn_supported(B, nb, D, M, W),
+                "vq_assign_bn: no fused BatchNorm fold for B=%d nb=%d M=%d W=%d "
+                "(vqgnn_vq_assign_bn_supported)", B, nb, M, W);
+  VQGNN_REQUIRE(bn_workspace && coef && rm_f && rv_f && (!with_grad || (rm_g && rv_g)),
+                "vq_assign_bn: null pointer");
+  VQGNN_REQUIRE(mode >= 0 && mode <= 3, "vq_assign_bn: mode must be 0..3");
+  VQGNN_REQUIRE(arith_ok(arith_x) && arith_x != kBnContig &&
+                    (!with_grad || (arith_ok(arith_g) && arith_g != kBnContig)),
+                "vq_assign_bn: the cascade arithmetic (FP64 / STRIDED) only");
+  // all-FP64 single-process statistics take vqgnn_bn_stats_finalize's fp64
+  // sums, not the cascade: no fold of them here (same bits as that call only)
+  VQGNN_REQUIRE(!(arith_x == kBnFp64 && (!with_grad || arith_g == kBnFp64)),
+                "vq_assign_bn: all-FP64 statistics use vqgnn_bn_stats_finalize");
+  const int F = nb * D;
+  const int C = with_grad ? 2 * F : F;
+  const CascadeGeom cg = cascade_geom(B);
+  const CascadeWs ws = cascade_ws(const_cast<void*>(bn_workspace), C, cg);
+  BnFold fold;
+  fold.sb_sum = ws.sb_sum;
+  fold.sb_p = ws.sb_p;
+  fold.sb_q = ws.sb_q;
+  fold.tail = ws.tail;
+  fold.lp = cg.lp;
+  fold.nsb = cg.nsb;
+  fold.C = C;
+  fold.a = bn_args(mode, arith_x, with_grad ? arith_g : kBnFp64, momentum_f, eps_f, momentum_g,
+                   eps_g, eps_std, rm_f, rv_f, rm_g, rv_g, coef, batch_out, nbt_f, nbt_g, nbt_d);
+  return launch_filter(X, ldx, G, ldg, B, nb, D, M, W, coef, grad_scale, embedding, ldw,
+                       emb_bstride, idx_out, codes, ldc, batch_idx,
+                       reinterpret_cast<unsigned long long*>(ema_parts), ema_zeroed, stat_count,
+                       workspace, as_stream(stream), &fold);
+}
+
+static int assign_check(const float* X, int64_t ldx, const float* G, int64_t ldg, int32_t B,
+                        int32_t nb, int32_t D, int32_t M, int32_t W, const float* embedding,
+                        int32_t ldw, int64_t emb_bstride, int16_t* codes, int64_t ldc,
+                        const int64_t* batch_idx, int64_t* ema_parts, int64_t stat_count,
+                        void* workspace) {
+  VQGNN_REQUIRE(X && embedding, "vq_assign: null pointer");
+  VQGNN_REQUIRE(B > 0 && nb > 0 && D > 0 && M > 0, "vq_assign: bad shape");
+  VQGNN_REQUIRE(W == D || W == 2 * D, "vq_assign: W must be D or 2D (W=%d D=%d)", W, D);
+  VQGNN_REQUIRE(W <= 16, "vq_assign: W=%d > 16 not implemented", W);
+  VQGNN_REQUIRE(ldx >= (int64_t)nb * D, "vq_assign: ldx too small");
+  VQGNN_REQUIRE(W == D || (G && ldg >= (int64_t)nb * D), "vq_assign: grads required for W=2D");
+  VQGNN_REQUIRE(ldw >= W && emb_bstride >= (int64_t)M * ldw, "vq_assign: bad codebook layout");
+  VQGNN_REQUIRE(!codes || (batch_idx && ldc >= nb), "vq_assign: codes needs batch_idx, ldc>=nb");
+  VQGNN_REQUIRE(workspace || (!ema_parts && !use_filter(W)),
+                "vq_assign: workspace required (vqgnn_vq_assign_workspace)");
+  VQGNN_REQUIRE(M <= 32767 || !codes, "vq_assign: int16 codes need M <= 32767");
+  VQGNN_REQUIRE(!ema_parts || stat_count >= B, "vq_assign: stat_count < B");
+  VQGNN_REQUIRE((int64_t)B * ldx * 4 < ((int64_t)1 << 32) &&
+                    (!G || (int64_t)B * ldg * 4 < ((int64_t)1 << 32)),
+                "vq_assign: B*ldx (and B*ldg) must span < 4 GiB");
+  return VQGNN_OK;
 }
 
 extern "C" void vqgnn_vq_stat_shifts(int64_t stat_count, float grad_scale, int32_t* shift_f,

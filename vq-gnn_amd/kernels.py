@@ -107,6 +107,49 @@ def bn_stats_finalize(X, G, F, mode, mom_f, eps_f, mom_g, eps_g, eps_std, rm_f, 
     return coef, batch, sums
 
 
+class BnFold:
+    """BatchNorm statistics whose finalize runs in the prologue of the next
+    vq_assign (include/vqgnn.h §5b): the cascade partials are on the device,
+    coef / batch are filled (and the running statistics, num_batches_tracked
+    updated) by the assign's launch, in stream order.  Pass it as vq_assign's
+    ``coef``; it serves one assign call over the same X / G."""
+    __slots__ = ("ws", "X", "G", "F", "mode", "arith_x", "arith_g", "moms", "rm_f", "rv_f",
+                 "rm_g", "rv_g", "coef", "batch", "nbt_f", "nbt_g", "D", "used")
+
+
+def bn_fold_supported(B, nb, D, M, W) -> bool:
+    """Whether vq_assign can fold the BatchNorm finalize for this shape."""
+    return bool(lib().vqgnn_vq_assign_bn_supported(int(B), int(nb), int(D), int(M), int(W)))
+
+
+def bn_stats_partial(X, G, F, mode, mom_f, eps_f, mom_g, eps_g, eps_std, rm_f, rv_f,
+                     rm_g=None, rv_g=None, want_batch=False, nbt_f=None, nbt_g=None, D=0,
+                     arith_x=BN_STRIDED, arith_g=BN_STRIDED) -> BnFold:
+    """bn_stats_finalize's statistics pass alone (FP64 / STRIDED arithmetic);
+    its finalize is folded into the vq_assign that receives the returned
+    BnFold.  Same arguments and results as bn_stats_finalize."""
+    require_gpu(X, "bn_stats_partial")
+    if BN_CONTIG in (arith_x, arith_g if G is not None else arith_x):
+        raise ValueError("bn_stats_partial: the CONTIG arithmetic has no folded finalize")
+    B = X.shape[0]
+    dev = X.device
+    with_grad = G is not None
+    L = lib()
+    f = BnFold()
+    f.ws = workspace(L.vqgnn_bn_stats_workspace(B, F), dev)
+    check(L.vqgnn_bn_stats_partial(ptr(X), _ld(X), ptr(G), _ld(G) if with_grad else 0, B, F,
+                                   int(with_grad), ptr(f.ws), stream_ptr()), "bn_stats_partial")
+    f.X, f.G, f.F, f.mode, f.D = X, G, F, int(mode), int(D)
+    f.arith_x, f.arith_g = int(arith_x), int(arith_g)
+    f.moms = (float(mom_f), float(eps_f), float(mom_g), float(eps_g), float(eps_std))
+    f.rm_f, f.rv_f, f.rm_g, f.rv_g = rm_f, rv_f, rm_g, rv_g
+    f.nbt_f, f.nbt_g = nbt_f, nbt_g
+    f.coef = _coef(F, with_grad, dev)
+    f.batch = torch.empty(4, F, dtype=torch.float32, device=dev) if want_batch else None
+    f.used = False
+    return f
+
+
 def stat_shifts(stat_count: int, grad_scale: float) -> tuple[int, int]:
     """Fixed-point scale of the EMA statistic slabs (include/vqgnn.h §3)."""
     import ctypes
@@ -162,11 +205,26 @@ def vq_assign(X, G, coef, grad_scale, emb, D, W, idx_out=None, codes=None, batch
             parts, zeroed = stats_out, 1
         else:
             parts = torch.empty(P, nb, M, W + 1, dtype=torch.int64, device=X.device)
+    count = int(stat_count if stat_count is not None else B)
+    if isinstance(coef, BnFold):
+        f = coef
+        if f.used or f.X is not X or f.G is not G or f.F != nb * D:
+            raise ValueError("vq_assign: a BnFold serves one assign over the X / G of its "
+                             "bn_stats_partial")
+        f.used = True
+        mf, ef, mg, eg, es = f.moms
+        check(L.vqgnn_vq_assign_bn(ptr(X), _ld(X), ptr(G), _ld(G) if G is not None else 0, B,
+                                   nb, D, M, W, float(grad_scale), ptr(emb), ldw, emb.stride(0),
+                                   ptr(idx_out), ptr(codes), ldc, ptr(batch_idx), ptr(parts),
+                                   zeroed, count, ptr(ws), ptr(f.ws), f.mode, f.arith_x,
+                                   f.arith_g, mf, ef, mg, eg, es, ptr(f.rm_f), ptr(f.rv_f),
+                                   ptr(f.rm_g), ptr(f.rv_g), ptr(f.coef), ptr(f.batch),
+                                   ptr(f.nbt_f), ptr(f.nbt_g), f.D, stream_ptr()), "vq_assign_bn")
+        return parts
     check(L.vqgnn_vq_assign(ptr(X), _ld(X), ptr(G), _ld(G) if G is not None else 0, B, nb, D,
                             M, W, ptr(coef), float(grad_scale), ptr(emb), ldw, emb.stride(0),
                             ptr(idx_out), ptr(codes), ldc, ptr(batch_idx), ptr(parts), zeroed,
-                            int(stat_count if stat_count is not None else B), ptr(ws),
-                            stream_ptr()), "vq_assign")
+                            count, ptr(ws), stream_ptr()), "vq_assign")
     return parts
 
 

@@ -31,7 +31,7 @@ import torch
 from torch import nn
 
 from . import kernels
-from .kernels import (BN_EVAL, BN_EVAL_INIT, BN_FP64, BN_TRAIN, BN_TRAIN_INIT,
+from .kernels import (BN_CONTIG, BN_EVAL, BN_EVAL_INIT, BN_FP64, BN_TRAIN, BN_TRAIN_INIT,
                       bn_arith_of)
 
 # 'Bad Init!' (vq.py:188) is a device flag.  The reference checks it with a
@@ -234,6 +234,17 @@ class VQBank(nn.Module):
             return BN_FP64, layout
         return layout, layout
 
+    def _bn_fold(self, B, nbr, W, ax, ag):
+        """Single process: whether the BatchNorm finalize folds into the
+        assign's prologue (kernels.bn_stats_partial + vq_assign(BnFold): one
+        launch fewer, the same bits as bn_stats_finalize + vq_assign;
+        include/vqgnn.h §3a).  VQGNN_BN_FOLD=0 keeps the separate finalize."""
+        if os.environ.get("VQGNN_BN_FOLD", "0") == "0":
+            return False
+        if BN_CONTIG in (ax, ag) or (ax == BN_FP64 and ag == BN_FP64):
+            return False
+        return kernels.bn_fold_supported(B, nbr, self.D, self.M, W)
+
     def feature_update(self, X, b0, nbr, training, idx_out=None, codes=None, batch_idx=None):
         """vq.py:160-202 for branches [b0, b0+nbr): X is [B, nbr*D] (a row-major view)."""
         self.finish_update()
@@ -249,10 +260,15 @@ class VQBank(nn.Module):
         ax, ax_eval = self._arith(X, comm)
         if training and comm is None:      # one process: statistics + finalize
             count = B
-            coef, _, _ = kernels.bn_stats_finalize(X, None, F, BN_TRAIN, 0.1, 1e-5, 0.0, 0.0,
-                                                   0.0, self.rm_f[sl], self.rv_f[sl],
-                                                   nbt_f=self.nbt_f[sl], D=D, arith_x=ax,
-                                                   ref_threads=self._threads())
+            if self._bn_fold(B, nbr, D, ax, ax):
+                coef = kernels.bn_stats_partial(X, None, F, BN_TRAIN, 0.1, 1e-5, 0.0, 0.0, 0.0,
+                                                self.rm_f[sl], self.rv_f[sl],
+                                                nbt_f=self.nbt_f[sl], D=D, arith_x=ax)
+            else:
+                coef, _, _ = kernels.bn_stats_finalize(X, None, F, BN_TRAIN, 0.1, 1e-5, 0.0,
+                                                       0.0, 0.0, self.rm_f[sl], self.rv_f[sl],
+                                                       nbt_f=self.nbt_f[sl], D=D, arith_x=ax,
+                                                       ref_threads=self._threads())
         elif training:         # multi-GPU: the global count rides in the sums
             sums = kernels.bn_stats(X, None, F, with_count=True)
             max_B = comm.allreduce_stats_(sums, B)
@@ -340,7 +356,11 @@ class VQBank(nn.Module):
                      nbt_g=self.nbt_g[sl] if training else None, D=D)
         ax, ax_eval = self._arith(X, comm)
         ag, ag_eval = self._arith(G, comm)
-        if comm is None:   # one process: statistics + finalize (the stash in every mode)
+        if comm is None and self._bn_fold(B, nbr, 2 * D, ax, ag):
+            # one process, the finalize folded into the assign (the stash too)
+            coef = kernels.bn_stats_partial(X, G, F, *bn_args, **bn_kw, arith_x=ax, arith_g=ag)
+            batch = coef.batch
+        elif comm is None:   # one process: statistics + finalize (the stash in every mode)
             coef, batch, _ = kernels.bn_stats_finalize(X, G, F, *bn_args, **bn_kw, arith_x=ax,
                                                        arith_g=ag,
                                                        ref_threads=self._threads())
