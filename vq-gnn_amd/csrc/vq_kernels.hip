@@ -525,10 +525,28 @@ __device__ __forceinline__ void bn_fold_load(int c, int nsb, const float* __rest
                                              int lane, double* pp, double* qq) {
   const int64_t o = (int64_t)c * nsb;
   double p = 0.0, q = 0.0;
-  for (int i = lane; i < nsb; i += 64) {
-    sbs[i] = sb_sum[o + i];
-    p += sb_p[o + i];
-    q += sb_q[o + i];
+  // eight rounds of loads in flight before the in-order adds (one memory
+  // round trip up to nsb = 512 instead of one per 64 superblocks)
+  constexpr int U = 8;
+  for (int i0 = lane; i0 < nsb; i0 += 64 * U) {
+    float sv[U];
+    double pv[U], qv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + 64 * u;
+      sv[u] = i < nsb ? sb_sum[o + i] : 0.f;
+      pv[u] = i < nsb ? sb_p[o + i] : 0.0;
+      qv[u] = i < nsb ? sb_q[o + i] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + 64 * u;
+      if (i < nsb) {
+        sbs[i] = sv[u];
+        p += pv[u];
+        q += qv[u];
+      }
+    }
   }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {   // fixed butterfly: deterministic
@@ -546,7 +564,13 @@ __device__ __forceinline__ void bn_fold_groups(int B, int lp, int nsb, float* sb
   float* grp = sbs + nsb;
   for (int gi = lane; gi < ngr; gi += 64) {
     float acc2 = 0.f;
-    for (int k = 0; k < step; ++k) acc2 = __fadd_rn(acc2, sbs[gi * step + k]);
+    for (int k0 = 0; k0 < step; k0 += 16) {     // step = 2^lp, lp >= 4: whole runs of 16
+      float v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v[u] = sbs[gi * step + k0 + u];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) acc2 = __fadd_rn(acc2, v[u]);
+    }
     grp[gi] = acc2;
   }
 }
@@ -562,14 +586,24 @@ __device__ __forceinline__ BnCol bn_fold_stats(const float* X, int64_t ldx, cons
   const int step = 1 << lp;
   const int nblk = B >> lp, nsb_full = nblk >> lp, ngr = nsb_full >> lp;
   const float* grp = sbs + nsb;
+  // the two global loads first: their round trip overlaps the LDS chains
+  int64_t ld;
+  const float x0f = bn_col_base(X, ldx, G, ldg, F, c, &ld)[0];
+  const float tc = tail[c];
   float acc3 = 0.f;
-  for (int gi = 0; gi < ngr; ++gi) acc3 = __fadd_rn(acc3, grp[gi]);
+  for (int g0 = 0; g0 < ngr; g0 += 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = g0 + u < ngr ? grp[g0 + u] : 0.f;
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (g0 + u < ngr) acc3 = __fadd_rn(acc3, v[u]);
+  }
   float acc2 = 0.f;
   for (int k = ngr * step; k < nsb_full; ++k) acc2 = __fadd_rn(acc2, sbs[k]);
   const float acc1 = nsb_full < nsb ? sbs[nsb_full] : 0.f;
-  const float total = __fadd_rn(__fadd_rn(__fadd_rn(tail[c], acc1), acc2), acc3);
-  int64_t ld;
-  const double x0 = (double)bn_col_base(X, ldx, G, ldg, F, c, &ld)[0];
+  const float total = __fadd_rn(__fadd_rn(__fadd_rn(tc, acc1), acc2), acc3);
+  const double x0 = (double)x0f;
   const double nd = (double)B;
   BnCol st;
   st.tmean = __fdiv_rn(total, (float)B);

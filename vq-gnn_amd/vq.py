@@ -239,7 +239,7 @@ class VQBank(nn.Module):
         assign's prologue (kernels.bn_stats_partial + vq_assign(BnFold): one
         launch fewer, the same bits as bn_stats_finalize + vq_assign;
         include/vqgnn.h §3a).  VQGNN_BN_FOLD=0 keeps the separate finalize."""
-        if os.environ.get("VQGNN_BN_FOLD", "0") == "0":
+        if os.environ.get("VQGNN_BN_FOLD", "1") == "0":
             return False
         if BN_CONTIG in (ax, ag) or (ax == BN_FP64 and ag == BN_FP64):
             return False
