@@ -185,7 +185,8 @@ int vqgnn_vq_assign(const float* X, int64_t ldx, const float* G, int64_t ldg,
  *     bit for bit -- and the first row part's workgroups update the running
  *     statistics and num_batches_tracked and write coef / batch_out, so the
  *     results equal vqgnn_bn_stats_finalize + vqgnn_vq_assign with one launch
- *     fewer.  The columns' arithmetic is that call's cascade form: at least
+ *     fewer (the host layer's default stays the two calls: every row part
+ *     re-reads the partials).  The columns' arithmetic is that call's cascade form: at least
  *     one half STRIDED (all-FP64 statistics take the fp64-sum path there, and
  *     are rejected here); CONTIG has no fold.
  *     vqgnn_vq_assign_bn_supported says whether a shape has the fold
