@@ -194,3 +194,27 @@ def test_synthetic_graph_device_structure():
     cl = torch.searchsorted(cptr, torch.arange(5000), right=True) - 1
     intra = float((cl[row] == cl[col]).double().mean())
     assert 0.7 < intra < 0.85          # dedup drops more intra-cluster repeats
+
+
+def test_bn_fold_gating(monkeypatch):
+    """VQBank's choice between the separate BatchNorm finalize and the fold
+    into the assign (include/vqgnn.h §3a): opt-in by VQGNN_BN_FOLD=1, only
+    for the cascade arithmetic (a STRIDED half; never CONTIG, never all-FP64)
+    and the shapes the library supports."""
+    from vq_gnn_amd import kernels
+    from vq_gnn_amd.vq import VQBank
+    bank = VQBank(4, 64, 4)
+    asked = []
+    monkeypatch.setattr(kernels, "bn_fold_supported",
+                        lambda B, nb, D, M, W: asked.append((B, nb, D, M, W)) or True)
+    S, C, F64 = kernels.BN_STRIDED, kernels.BN_CONTIG, kernels.BN_FP64
+    monkeypatch.delenv("VQGNN_BN_FOLD", raising=False)
+    assert not bank._bn_fold(1000, 4, 8, S, S)            # default: the separate finalize
+    monkeypatch.setenv("VQGNN_BN_FOLD", "1")
+    assert bank._bn_fold(1000, 4, 8, S, S)
+    assert asked[-1] == (1000, 4, 4, 64, 8)
+    assert bank._bn_fold(1000, 4, 8, S, F64)              # mixed: the cascade path
+    assert not bank._bn_fold(1000, 4, 8, C, S)            # CONTIG has no fold
+    assert not bank._bn_fold(1000, 4, 8, F64, F64)        # all-FP64: the fp64-sum path
+    monkeypatch.setattr(kernels, "bn_fold_supported", lambda *a: False)
+    assert not bank._bn_fold(1000, 4, 8, S, S)
