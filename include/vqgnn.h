@@ -238,16 +238,23 @@ int vqgnn_vq_ema_finalize(int64_t* ema_parts, int32_t nparts, int32_t zero_after
 
 /* ------------------------------------------------------------------------ *
  * 5. Out-of-batch codeword gather (models.py:158, :168-173): for j in [0, n-B)
- *    and b < nb, with code = codes[subset[B+j]][b]:
+ *    and b < nb, with node = subset[B+j] and code = codes[node][b]:
  *      xt[j][b*D + k] = emb_out[b][code][col_offset + k],  k < D
  *      lcodes[j][b]   = code                               (optional)
  *    col_offset = 0 gives x_first_order (feature halves), col_offset = D the
- *    grad halves (grad_first_order).  emb_out [nb][M][ldw], branch stride
- *    emb_bstride; xt [n-B][ldt].  xt may be NULL (codes only).
+ *    grad halves (grad_first_order).  codes [n_nodes][ldc] (c_indices);
+ *    emb_out [n_branches][M][ldw], branch stride emb_bstride; xt [n-B][ldt].
+ *    xt may be NULL (codes only).  nb (the code columns read) must not exceed
+ *    n_branches (VQGNN_ERR_INVALID): the gather never reads past the codebook.
+ *    A node outside [0, n_nodes) or a code outside [0, M) reads nothing: its
+ *    D values are zeros (lcodes: -1 for a bad node).  (The reference raises
+ *    IndexError there; c_indices written by vqgnn_vq_assign are always in
+ *    range.)
  * ------------------------------------------------------------------------ */
 int vqgnn_gather_codewords(const int64_t* subset, int32_t B, int32_t n,
-                           const int16_t* codes, int64_t ldc, int32_t nb, int32_t D,
-                           const float* emb_out, int32_t ldw, int64_t emb_bstride,
+                           const int16_t* codes, int64_t ldc, int64_t n_nodes,
+                           int32_t nb, int32_t D, const float* emb_out,
+                           int32_t n_branches, int32_t M, int32_t ldw, int64_t emb_bstride,
                            int32_t col_offset, float* xt, int64_t ldt,
                            int16_t* lcodes, vqgnn_stream_t stream);
 
@@ -316,20 +323,28 @@ int vqgnn_spmm_task(const int32_t* rowptr, int32_t n_rows, int32_t n_cols, int64
  *      rewritten in place: a column j >= B becomes B + subset[j] (the node
  *      whose codes give the row); requires B + n_nodes <= 2^26.
  *    vqgnn_spmm_task_cb: out = A @ x_in for the rewritten records; codes
- *      [n_nodes][ldc] int16 (c_indices), codewords = emb_out (branch stride
- *      bstride, row stride ldw floats, 16-byte aligned); F a multiple of 128,
- *      D a multiple of 4, M <= 300 (the LDS image: M x 512 bytes per 128-column
- *      tile, vqgnn_spmm_task_cb_lds); X and out on the 32-bit near
- *      path (else VQGNN_ERR_INVALID: use vqgnn_spmm_task).                  */
+ *      [n_nodes][ldc] int16 (c_indices, every code in [0, M)), codewords =
+ *      emb_out [n_branches][M][ldw] (branch stride bstride, 16-byte aligned
+ *      rows); the F / D code columns read must not exceed n_branches; F a
+ *      multiple of 128, D a multiple of 4, M <= 300 (the LDS image: M x 512
+ *      bytes per 128-column tile, vqgnn_spmm_task_cb_lds); X and out on the
+ *      32-bit near path.  Any other shape: VQGNN_ERR_INVALID (use
+ *      vqgnn_gather_codewords + vqgnn_spmm_task, which has a 64-bit path).
+ *    vqgnn_spmm_task_cb_supported: 1 iff vqgnn_spmm_task_cb accepts this
+ *      shape (the same checks, no launch), so a host falls back before the
+ *      call instead of catching its error.                                   */
 int vqgnn_spmm_task_records_cb(int64_t* records, int64_t nnz, int32_t B, const int64_t* subset,
                                int32_t n_cols, int64_t n_nodes, vqgnn_stream_t stream);
 size_t vqgnn_spmm_task_cb_lds(int32_t M);
+int32_t vqgnn_spmm_task_cb_supported(int32_t n_rows, int32_t B, int64_t ldx, int32_t F,
+                                     int64_t ldo, int64_t n_nodes, int64_t ldc,
+                                     int32_t n_branches, int32_t M, int32_t D);
 int vqgnn_spmm_task_cb(const int32_t* rowptr, int32_t n_rows, int64_t nnz, int32_t B,
                        const float* X, int64_t ldx, int32_t F, const int16_t* codes, int64_t ldc,
                        int64_t n_nodes, const float* codewords, int64_t ldw, int64_t bstride,
-                       int32_t M, int32_t D, float* out, int64_t ldo, const int32_t* plan,
-                       const int64_t* records_cb, int32_t K, int32_t n_jobs, int32_t n_empty,
-                       void* workspace, vqgnn_stream_t stream);
+                       int32_t n_branches, int32_t M, int32_t D, float* out, int64_t ldo,
+                       const int32_t* plan, const int64_t* records_cb, int32_t K, int32_t n_jobs,
+                       int32_t n_empty, void* workspace, vqgnn_stream_t stream);
 
 /* 7. CSR transpose (structure + values) for the backward product
  *    dX = A^T dOut (torch_sparse matmul autograd, convs.py:95).  Output CSR of
@@ -392,8 +407,12 @@ int vqgnn_gat_edge_grad(const int32_t* rows, const int32_t* col, const float* co
  *     6e with each edge's coefficient exp(leaky(alpha_l_s[j] + alpha_r_s[i]))
  *     * w computed in the kernel (the op order of vqgnn_gat_coef; the scaled
  *     scalars of vqgnn_gat_alpha), the ones column as a per-row
- *     coefficient sum, and rows < norm_B divided by that sum + 1e-16 before
- *     the store (models.py:188; norm_B = 0: no normalisation).  Replaces
+ *     coefficient sum, and rows < norm_B normalised by that sum + 1e-16
+ *     before the store (models.py:188; norm_B = 0: no normalisation) -- as
+ *     ONE v_rcp_f32 of (sum + 1e-16) times each column, not the reference's
+ *     IEEE division: within 3 ulp of vqgnn_gat_normalize's true quotient
+ *     (pinned in tests/test_gpu_gat.py), and the same bits for a row whether
+ *     the plan cuts it across tasks (fix-up) or not (walker).  Replaces
  *     vqgnn_gat_coef + vqgnn_spmm_task + vqgnn_gat_normalize; the coefficients are
  *     never materialised unless coef (optional, [nnz], CSR order) is given for
  *     the backward; den (optional, [n_rows]) receives the sums.  erow: the

@@ -67,3 +67,30 @@ def test_invalid_arguments_rejected_without_device():
     # the code exchange's stamp epochs start at 1
     rc = h.vqgnn_scatter_wire(16, 4, 8, 256, 16, 0, 10, 16, 8, None)
     assert rc == 1 and b"epoch" in h.vqgnn_last_error()
+
+
+def test_codebook_reads_bounded_by_its_branch_count():
+    """VERDICT r04 (GPU fault): the gather and the codebook-source SpMM take
+    the codebook's branch count and reject a call that would read past it --
+    before any launch, so dummy device addresses never get dereferenced."""
+    h = L.lib()
+    # gather: 35 code columns against a 32-branch [32, 256, 8] codebook
+    rc = h.vqgnn_gather_codewords(16, 100, 200, 16, 35, 1000, 35, 4, 16, 32, 256, 8, 256 * 8, 0,
+                                  16, 35 * 4, None, None)
+    assert rc == 1 and b"branches" in h.vqgnn_last_error()
+    # the same call with nb = 32 passes validation (not launched: n == B)
+    rc = h.vqgnn_gather_codewords(16, 100, 100, 16, 35, 1000, 32, 4, 16, 32, 256, 8, 256 * 8, 0,
+                                  16, 32 * 4, None, None)
+    assert rc == 0
+    # codebook-source SpMM: F / D = 32 code columns against 16 branches
+    rc = h.vqgnn_spmm_task_cb(16, 100, 1000, 50, 16, 128, 128, 16, 32, 1000, 16, 8, 256 * 8, 16,
+                              256, 4, 16, 128, 16, 16, 64, 0, 0, 16, None)
+    assert rc == 1 and b"branches" in h.vqgnn_last_error()
+    assert h.vqgnn_spmm_task_cb_supported(100, 50, 128, 128, 128, 1000, 32, 16, 256, 4) == 0
+    assert h.vqgnn_spmm_task_cb_supported(100, 50, 128, 128, 128, 1000, 32, 32, 256, 4) == 1
+    # the kernel's other limits, mirrored by the query (ADVICE r04)
+    assert h.vqgnn_spmm_task_cb_supported(100, 50, 128, 128, 128, 1000, 32, 32, 301, 4) == 0
+    assert h.vqgnn_spmm_task_cb_supported(1 << 24, 50, 128, 128, 128, 1000, 32, 32, 256, 4) == 0
+    assert h.vqgnn_spmm_task_cb_supported(100, 5_000_000, 128, 128, 128, 1000, 32, 32, 256,
+                                          4) == 0          # X past the 2 GiB near range
+    assert h.vqgnn_spmm_task_cb_supported(100, 50, 128, 64, 128, 1000, 16, 16, 256, 4) == 0

@@ -161,3 +161,27 @@ def test_codebook_sync_direct_rccl_only_on_nccl(tmp_path):
     (the CPU tests, the one-GPU rehearsals) keep torch.distributed."""
     mp.spawn(_gloo_direct_flag, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
     assert [open(tmp_path / f"direct{r}.txt").read() for r in range(2)] == ["0", "0"]
+
+
+def test_release_comms_aborts_unless_closed():
+    """CodebookSync's finalizer destroys its communicators only
+    after close() ran; any other release (an exception exit, sys.exit from a
+    handler, a failing thread, collection) aborts them."""
+    from vq_gnn_amd.dist import _release_comms
+
+    class Fake:
+        def __init__(self):
+            self.calls = []
+
+        def abort(self):
+            self.calls.append("abort")
+
+        def destroy(self):
+            self.calls.append("destroy")
+
+    a, b = Fake(), Fake()
+    _release_comms(a, b, [False])
+    assert a.calls == b.calls == ["abort"]
+    a, b = Fake(), Fake()
+    _release_comms(a, None, [True])
+    assert a.calls == ["destroy"] and b.calls == []

@@ -216,6 +216,14 @@ def test_gat_fused_kernel_matches_coefficient_path(F, empty_runs):
     for got in (out, ref):
         err = np.abs(got.cpu().numpy() - ref64)
         assert (err <= 1e-5 * sc + 1e-30).all(), f"rel err {(err / (sc + 1e-30)).max():.2e}"
+    # the fused rows are the raw sum times v_rcp_f32(den + 1e-16); gat_normalize
+    # divides (the reference's /=, models.py:188): pinned at 3 ulp apart
+    # (include/vqgnn.h §8b), rows >= B (never normalised) bit-identical
+    o, rr = out.cpu().numpy(), ref.cpu().numpy()
+    ulp = np.spacing(np.abs(rr[:B]).astype(np.float32))
+    assert (np.abs(o[:B] - rr[:B]) <= 3 * ulp).all(), \
+        f"fused vs divided: {(np.abs(o[:B] - rr[:B]) / np.maximum(ulp, 1e-45)).max():.1f} ulp"
+    assert np.array_equal(o[B:], rr[B:])
     assert torch.equal(out[torch.as_tensor(np.diff(rowptr) == 0, device=DEV)],
                        torch.zeros_like(out[torch.as_tensor(np.diff(rowptr) == 0, device=DEV)]))
     again, _, _ = kernels.gat_spmm(adj.rowptr, adj.col, adj.value, n, nnz, x, F, als, ars,

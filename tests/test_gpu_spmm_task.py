@@ -194,17 +194,26 @@ def test_codebook_source_equals_gather_and_two_source(B, n, K):
 
 def test_codebook_source_arxiv_batch_and_strides():
     """The bench batch (arxiv_gcn, M = 256, nb = 32): equal to gather +
-    two-source on a strided X and output, deterministic."""
+    two-source on a strided X, codes (c_indices view with ld 35 > nb, as a
+    column slice of a wider code table) and output, deterministic, and within
+    1e-5 of the fp64 sum (the gather once took nb from the
+    codes' 35 columns and read past the 32-branch codebook)."""
     cfg = dict(graph.CONFIGS["arxiv_gcn"])
     g, _, b = graph.make_batch(cfg)
     F, M, D = 128, cfg["M"], 4
     nb = F // D
     bidx, subset, adj = graph.batch_to_device(b, DEV)
     gen = torch.Generator(device="cpu").manual_seed(11)
-    codes = torch.randint(0, M, (cfg["N"], nb + 3), dtype=torch.int16, generator=gen).to(DEV)
+    wide = torch.randint(0, M, (cfg["N"], nb + 3), dtype=torch.int16, generator=gen).to(DEV)
+    codes = wide[:, :nb]                                     # ld = nb + 3
     emb_out = torch.randn(nb, M, 2 * D, generator=gen).to(DEV)
     X = torch.randn(b.B, F + 8, generator=gen).to(DEV)[:, 4:4 + F]
     xf, _ = kernels.gather_codewords(subset, b.B, codes, emb_out, D)
+    assert xf.shape == (b.n - b.B, F)
+    # the wide table through the gather: nb comes from the codebook (32), not
+    # from the table's 35 columns, so the same rows
+    xf_wide, _ = kernels.gather_codewords(subset, b.B, wide, emb_out, D)
+    assert torch.equal(xf, xf_wide)
     ref = kernels.spmm(adj.rowptr, adj.col, adj.value, b.n, b.nnz, X, F, X2=xf, B=b.B,
                        plan=adj.plan(F, B=b.B))
     out = torch.full((b.n, F + 4), 3.0, device=DEV)[:, :F]
@@ -213,6 +222,15 @@ def test_codebook_source_arxiv_batch_and_strides():
     assert torch.equal(out, ref)
     again = kernels.spmm_codebook(adj.rowptr, b.n, b.nnz, X, F, b.B, codes, emb_out, D, pcb)
     assert torch.equal(again, ref)
+    # the codewords of every out-of-batch row, restated on the host from the
+    # codes (models.py:168-173), then the fp64 sum (convs.py:95)
+    sub = subset.cpu().numpy()
+    cod = codes.cpu().numpy().astype(np.int64)
+    emb = emb_out.cpu().numpy()
+    xf_host = emb[np.arange(nb)[None, :], cod[sub[b.B:]], :D].reshape(b.n - b.B, F)
+    assert np.array_equal(xf.cpu().numpy(), xf_host)
+    xin = np.concatenate([X.cpu().numpy(), xf_host])
+    _check(out, b.rowptr, b.col, b.val, xin)
 
 
 def test_codebook_source_rejects_unsupported():
@@ -229,6 +247,48 @@ def test_codebook_source_rejects_unsupported():
     with pytest.raises(RuntimeError, match="multiple of 128"):
         kernels.spmm_codebook(a.rowptr, 100, a.nnz(), X64, 64, 50, codes[:, :16],
                               emb_out[:16], 4, pcb)
+    # F / D = 32 code columns against a 16-branch codebook: rejected, no read
+    with pytest.raises(RuntimeError, match="branches"):
+        kernels.spmm_codebook(a.rowptr, 100, a.nnz(), X, 128, 50, codes, emb_out[:16], 4, pcb)
+    with pytest.raises(ValueError, match="branches"):
+        kernels.gather_codewords(subset, 50, codes, emb_out[:16], 4, nb=32)
+    with pytest.raises(ValueError, match="columns"):
+        kernels.gather_codewords(subset, 50, codes[:, :8], emb_out, 4)
+    with pytest.raises(ValueError, match="int64"):
+        plan.with_codebook_source(50, subset.to(torch.int32), 300)
+    with pytest.raises(ValueError, match="columns"):
+        a.plan().with_codebook_source(50, subset[:99], 300)
+    # CodebookInput falls back to the gathered rows where the kernel cannot
+    from vq_gnn_amd.convs import CodebookInput
+    assert CodebookInput(X, subset, codes, emb_out, 4).supported(100)
+    assert not CodebookInput(X, subset, codes, big, 4).supported(100)
+    assert not CodebookInput(X, subset, codes, emb_out[:16], 4).supported(100)
+
+
+def test_gather_bad_nodes_and_codes_read_nothing():
+    """A node outside [0, N) or a code outside [0, M) gives a zero row (and
+    lcodes -1 for the node), never a read past codes / emb_out."""
+    M, D, nb, N = 16, 4, 4, 10
+    codes = torch.randint(0, M, (N, nb), dtype=torch.int16, device=DEV)
+    codes[3, 2] = M + 5
+    codes[4, 1] = -1
+    emb_out = torch.randn(nb, M, 2 * D, device=DEV)
+    subset = torch.tensor([0, 1, 3, 4, 10, -2, 7], dtype=torch.int64, device=DEV)
+    xt, lc = kernels.gather_codewords(subset, 2, codes, emb_out, D, want_codes=True)
+    xt, lc = xt.cpu(), lc.cpu()
+    e = emb_out.cpu()
+    for j, node in enumerate([3, 4, 10, -2, 7]):
+        for br in range(nb):
+            seg = xt[j, br * D:(br + 1) * D]
+            if not 0 <= node < N:
+                assert lc[j, br] == -1 and torch.count_nonzero(seg) == 0
+                continue
+            c = int(codes[node, br])
+            assert lc[j, br] == c
+            if 0 <= c < M:
+                assert torch.equal(seg, e[br, c, :D])
+            else:
+                assert torch.count_nonzero(seg) == 0
 
 
 def test_codebook_plan_cache_follows_the_subset():

@@ -61,9 +61,9 @@ SIGNATURES = {
                                              _i32, _f32, _f32, _c_void_p, _i64, _c_void_p,
                                              _c_void_p, _c_void_p, _i64, _c_void_p, _c_void_p,
                                              _c_void_p, _c_void_p, _c_void_p, _c_void_p]),
-    "vqgnn_gather_codewords": (ctypes.c_int, [_c_void_p, _i32, _i32, _c_void_p, _i64, _i32,
-                                              _i32, _c_void_p, _i32, _i64, _i32, _c_void_p,
-                                              _i64, _c_void_p, _c_void_p]),
+    "vqgnn_gather_codewords": (ctypes.c_int, [_c_void_p, _i32, _i32, _c_void_p, _i64, _i64,
+                                              _i32, _i32, _c_void_p, _i32, _i32, _i32, _i64,
+                                              _i32, _c_void_p, _i64, _c_void_p, _c_void_p]),
     "vqgnn_scatter_codes": (ctypes.c_int, [_c_void_p, _i32, _c_void_p, _i32, _c_void_p, _i64,
                                            _c_void_p]),
     "vqgnn_spmm_task_size": (_i64, [_i64, _i32, _i32]),
@@ -78,10 +78,12 @@ SIGNATURES = {
     "vqgnn_spmm_task_records_cb": (ctypes.c_int, [_c_void_p, _i64, _i32, _c_void_p, _i32, _i64,
                                                   _c_void_p]),
     "vqgnn_spmm_task_cb_lds": (_size, [_i32]),
+    "vqgnn_spmm_task_cb_supported": (_i32, [_i32, _i32, _i64, _i32, _i64, _i64, _i64, _i32,
+                                            _i32, _i32]),
     "vqgnn_spmm_task_cb": (ctypes.c_int, [_c_void_p, _i32, _i64, _i32, _c_void_p, _i64, _i32,
                                           _c_void_p, _i64, _i64, _c_void_p, _i64, _i64, _i32,
-                                          _i32, _c_void_p, _i64, _c_void_p, _c_void_p, _i32,
-                                          _i32, _i32, _c_void_p, _c_void_p]),
+                                          _i32, _i32, _c_void_p, _i64, _c_void_p, _c_void_p,
+                                          _i32, _i32, _i32, _c_void_p, _c_void_p]),
     "vqgnn_gat_att_grad_workspace": (_size, [_i32, _i32, _i32]),
     "vqgnn_gat_att_grad": (ctypes.c_int, [_c_void_p, _i64, _c_void_p, _i64, _i32, _i32, _i32,
                                           _i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p,

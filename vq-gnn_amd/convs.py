@@ -50,15 +50,21 @@ class CodebookInput(NamedTuple):
     emb_out: torch.Tensor
     D: int
 
-    def supported(self):
+    def supported(self, n_rows=None):
+        """Whether the codebook-source kernel serves this input (its own
+        shape limits, include/vqgnn.h §6b); else ``gathered()`` is used."""
         F = self.x.shape[1]
-        return (kernels.codebook_source_ok(self.x, F, self.emb_out.shape[1], self.D) and
-                hasattr(kernels.lib(), "vqgnn_spmm_task_cb"))
+        return (hasattr(kernels.lib(), "vqgnn_spmm_task_cb") and
+                kernels.codebook_source_ok(self.x, F, self.emb_out.shape[1], self.D,
+                                           codes=self.codes,
+                                           n_rows=n_rows if n_rows is not None
+                                           else self.subset.numel(),
+                                           n_branches=self.emb_out.shape[0]))
 
     def gathered(self):
         """The GatheredInput form (x_first_order materialised by the gather)."""
         xf, _ = kernels.gather_codewords(self.subset, self.x.shape[0], self.codes,
-                                         self.emb_out, self.D)
+                                         self.emb_out, self.D, nb=self.x.shape[1] // self.D)
         return GatheredInput(self.x, xf)
 
 
@@ -179,7 +185,7 @@ class OurGCNConv(nn.Module):
     def forward(self, x, edge_index, edge_weight=None, _hook=None):
         adj = as_csr(edge_index)
         if isinstance(x, CodebookInput):
-            if x.supported():
+            if x.supported(adj.size(0)):
                 anchor = None
                 if _hook is not None and not x.x.requires_grad:
                     anchor = torch.zeros((), device=x.x.device, requires_grad=True)

@@ -28,4 +28,4 @@ int check_launch(const char* what) {
 }  // namespace vqgnn
 
 extern "C" const char* vqgnn_last_error(void) { return vqgnn::g_err; }
-extern "C" int vqgnn_version(void) { return 200; }
+extern "C" int vqgnn_version(void) { return 500; }

@@ -23,20 +23,30 @@ namespace vqgnn {
 // x_first_order[j][b*D + k] = emb_out[b][codes[subset[B + j]][b]][off + k]
 // (models.py:168-173; off = 0 feature half, off = D grad half), and optionally
 // lcodes[j][b] = the code.  Thread per (node, branch); D == 4 stores float4.
+// Bounds: a node outside [0, n_nodes) or a code outside [0, M) reads nothing
+// (its D values are written as zeros; lcodes gets -1 for a bad node, the code
+// as read for a bad code).  The host checks nb <= the codebook's branches.
 __global__ void gather_codewords_kernel(const int64_t* __restrict__ subset, int B, int nprime,
-                                        const int16_t* __restrict__ codes, int64_t ldc, int nb,
-                                        int D, const float* __restrict__ emb, int ldw,
+                                        const int16_t* __restrict__ codes, int64_t ldc,
+                                        int64_t n_nodes, int nb, int D,
+                                        const float* __restrict__ emb, int M, int ldw,
                                         int64_t bstride, int off, float* __restrict__ xt,
                                         int64_t ldt, int16_t* __restrict__ lcodes) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= (int64_t)nprime * nb) return;
   const int64_t j = t / nb;
   const int b = (int)(t % nb);
-  const int code = codes[subset[B + j] * ldc + b];
+  const int64_t node = subset[B + j];
+  const bool nok = node >= 0 && node < n_nodes;
+  const int code = nok ? (int)codes[node * ldc + b] : -1;
   if (lcodes) lcodes[t] = (int16_t)code;
   if (!xt) return;
-  const float* src = emb + b * bstride + (int64_t)code * ldw + off;
   float* dst = xt + j * ldt + (int64_t)b * D;
+  if (code < 0 || code >= M) {
+    for (int k = 0; k < D; ++k) dst[k] = 0.f;
+    return;
+  }
+  const float* src = emb + b * bstride + (int64_t)code * ldw + off;
   if (D == 4 && ((((uintptr_t)src) | ((uintptr_t)dst)) & 15) == 0) {
     *reinterpret_cast<float4*>(dst) = *reinterpret_cast<const float4*>(src);
   } else {
@@ -101,21 +111,27 @@ __global__ void transpose_finish_kernel(const int32_t* __restrict__ sorted_cols,
 using namespace vqgnn;
 
 extern "C" int vqgnn_gather_codewords(const int64_t* subset, int32_t B, int32_t n,
-                                      const int16_t* codes, int64_t ldc, int32_t nb, int32_t D,
-                                      const float* emb_out, int32_t ldw, int64_t emb_bstride,
-                                      int32_t col_offset, float* xt, int64_t ldt,
-                                      int16_t* lcodes, vqgnn_stream_t stream) {
+                                      const int16_t* codes, int64_t ldc, int64_t n_nodes,
+                                      int32_t nb, int32_t D, const float* emb_out,
+                                      int32_t n_branches, int32_t M, int32_t ldw,
+                                      int64_t emb_bstride, int32_t col_offset, float* xt,
+                                      int64_t ldt, int16_t* lcodes, vqgnn_stream_t stream) {
   clear_error();
-  VQGNN_REQUIRE(n >= B && B >= 0 && nb > 0 && ldc >= nb && D > 0, "gather_codewords: bad shape");
+  VQGNN_REQUIRE(n >= B && B >= 0 && nb > 0 && ldc >= nb && D > 0 && n_nodes >= 0,
+                "gather_codewords: bad shape");
   const int64_t tot = (int64_t)(n - B) * nb;
   if (tot == 0) return VQGNN_OK;
   VQGNN_REQUIRE(subset && codes && (xt || lcodes), "gather_codewords: null pointer");
-  VQGNN_REQUIRE(!xt || (emb_out && ldt >= (int64_t)nb * D && col_offset >= 0 &&
-                        col_offset + D <= ldw),
+  // every branch read must exist in the codebook (emb_out [n_branches][M][ldw])
+  VQGNN_REQUIRE(!xt || (emb_out && nb <= n_branches && M > 0),
+                "gather_codewords: %d code columns read past the codebook's %d branches "
+                "(M=%d)", nb, n_branches, M);
+  VQGNN_REQUIRE(!xt || (ldt >= (int64_t)nb * D && col_offset >= 0 && col_offset + D <= ldw &&
+                        (n_branches == 1 || emb_bstride >= (int64_t)M * ldw)),
                 "gather_codewords: bad codebook / output layout");
   hipLaunchKernelGGL(gather_codewords_kernel, dim3((tot + 255) / 256), dim3(256), 0,
-                     as_stream(stream), subset, B, n - B, codes, ldc, nb, D, emb_out, ldw,
-                     emb_bstride, col_offset, xt, ldt, lcodes);
+                     as_stream(stream), subset, B, n - B, codes, ldc, n_nodes, nb, D, emb_out, M,
+                     ldw, emb_bstride, col_offset, xt, ldt, lcodes);
   return check_launch("gather_codewords");
 }
 

@@ -106,14 +106,20 @@ __global__ void task_records_kernel(const int32_t* __restrict__ col, const float
 }
 
 // codebook-source records: a column j >= B becomes B + nodes[j] (the node
-// whose codes give the row); flags and weight kept
-__global__ void task_remap_cb_kernel(int2* __restrict__ rec, int nnz, int B,
-                                     const int64_t* __restrict__ nodes) {
+// whose codes give the row); flags and weight kept.  A column past the subset
+// or a node outside [0, n_nodes) becomes B + n_nodes, past the codes' buffer
+// range: its code reads as 0 with no memory access (invalid input, bounded)
+__global__ void task_remap_cb_kernel(int2* __restrict__ rec, int nnz, int B, int n_cols,
+                                     const int64_t* __restrict__ nodes, int64_t n_nodes) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= nnz) return;
   const uint32_t x = (uint32_t)rec[e].x;
   const uint32_t j = x & kColMask;
-  if ((int)j >= B) rec[e].x = (int)((x & ~kColMask) | ((uint32_t)B + (uint32_t)nodes[j]));
+  if ((int)j >= B) {
+    int64_t node = (int)j < n_cols ? nodes[j] : n_nodes;
+    if (node < 0 || node > n_nodes) node = n_nodes;
+    rec[e].x = (int)((x & ~kColMask) | ((uint32_t)B + (uint32_t)node));
+  }
 }
 
 __global__ void task_row_ends_kernel(const int32_t* __restrict__ rowptr, int n_rows,
@@ -884,7 +890,8 @@ extern "C" int vqgnn_spmm_task_records_cb(int64_t* records, int64_t nnz, int32_t
                 "spmm_task_records_cb: B + %lld nodes exceed 2^26", (long long)n_nodes);
   if (nnz > 0 && n_cols > B)
     hipLaunchKernelGGL(task_remap_cb_kernel, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0,
-                       as_stream(stream), reinterpret_cast<int2*>(records), (int)nnz, B, nodes);
+                       as_stream(stream), reinterpret_cast<int2*>(records), (int)nnz, B, n_cols, nodes,
+                       n_nodes);
   return check_launch("spmm_task_records_cb");
 }
 
@@ -892,29 +899,54 @@ extern "C" size_t vqgnn_spmm_task_cb_lds(int32_t M) {
   return M > 0 ? (size_t)M * 512 : 0;
 }
 
+// The shapes vqgnn_spmm_task_cb serves (its own checks below plus the near
+// path of task_setup for X [B][ldx] and out [n_rows][ldo]); 0 -> use
+// gather_codewords + vqgnn_spmm_task, which has a 64-bit far path.
+static const char* cb_unsupported(int32_t n_rows, int32_t B, int64_t ldx, int32_t F, int64_t ldo,
+                                  int64_t n_nodes, int64_t ldc, int32_t n_branches, int32_t M,
+                                  int32_t D) {
+  if (F <= 0 || F % 128 != 0) return "F must be a multiple of 128";
+  if (D <= 0 || D % 4 != 0 || F % D != 0) return "D must be a multiple of 4 dividing F";
+  if (F / D > n_branches) return "F / D code columns exceed the codebook's branches";
+  if (M <= 0 || M > 300) return "M above the LDS image (300)";
+  if (ldc < F / D || n_nodes < 0 || n_nodes >= (1 << 24) ||
+      n_nodes * ldc * 2 >= ((int64_t)1 << 31) || ldc * 2 >= (1 << 24) ||
+      (int64_t)B + n_nodes > (int64_t)kColMask)
+    return "codes out of range";
+  if (n_rows < 0 || n_rows >= (1 << 24) || B < 0 || B >= (1 << 24)) return "rows above 2^24";
+  if (ldx < F || ldo < F || ldx * 4 >= (1 << 24) || ldo * 4 >= (1 << 24))
+    return "leading dimension off the near path";
+  if ((int64_t)(B > 0 ? B - 1 : 0) * ldx * 4 + (int64_t)F * 4 >= 0x7FFFFFF0ll)
+    return "X above the 2 GiB near range";
+  if ((int64_t)n_rows * ldo * 4 >= ((int64_t)1 << 32)) return "out above 4 GiB";
+  return nullptr;
+}
+
+extern "C" int32_t vqgnn_spmm_task_cb_supported(int32_t n_rows, int32_t B, int64_t ldx, int32_t F,
+                                                int64_t ldo, int64_t n_nodes, int64_t ldc,
+                                                int32_t n_branches, int32_t M, int32_t D) {
+  return cb_unsupported(n_rows, B, ldx, F, ldo, n_nodes, ldc, n_branches, M, D) ? 0 : 1;
+}
+
 extern "C" int vqgnn_spmm_task_cb(const int32_t* rowptr, int32_t n_rows, int64_t nnz, int32_t B,
                                   const float* X, int64_t ldx, int32_t F, const int16_t* codes,
                                   int64_t ldc, int64_t n_nodes, const float* codewords,
-                                  int64_t ldw, int64_t bstride, int32_t M, int32_t D, float* out,
-                                  int64_t ldo, const int32_t* plan, const int64_t* records_cb,
-                                  int32_t K, int32_t n_jobs, int32_t n_empty, void* workspace,
-                                  vqgnn_stream_t stream) {
+                                  int64_t ldw, int64_t bstride, int32_t n_branches, int32_t M,
+                                  int32_t D, float* out, int64_t ldo, const int32_t* plan,
+                                  const int64_t* records_cb, int32_t K, int32_t n_jobs,
+                                  int32_t n_empty, void* workspace, vqgnn_stream_t stream) {
   clear_error();
+  const char* why = cb_unsupported(n_rows, B, ldx, F, ldo, n_nodes, ldc, n_branches, M, D);
+  VQGNN_REQUIRE(!why, "spmm_task_cb: %s (n_rows=%d B=%d F=%d D=%d M=%d branches=%d codes "
+                "[%lld x %lld])", why ? why : "", n_rows, B, F, D, M, n_branches,
+                (long long)n_nodes, (long long)ldc);
   TaskArgs a{};
   bool near = false;
   const int rc = task_setup(a, rowptr, n_rows, B, nnz, B, X, ldx, X, ldx, F, out, ldo, plan,
                             records_cb, K, n_jobs, n_empty, workspace, &near);
   if (rc != VQGNN_OK) return rc;
   VQGNN_REQUIRE(near, "spmm_task_cb: X and out must fit the 32-bit near path");
-  VQGNN_REQUIRE(F % 128 == 0, "spmm_task_cb: F=%d must be a multiple of 128", F);
-  VQGNN_REQUIRE(D > 0 && D % 4 == 0 && F % D == 0, "spmm_task_cb: D=%d", D);
-  VQGNN_REQUIRE(M > 0 && M <= 300, "spmm_task_cb: M=%d above the LDS image (300)", M);
   VQGNN_REQUIRE(nnz == 0 || (codes && codewords), "spmm_task_cb: null pointer");
-  VQGNN_REQUIRE(ldc >= F / D && n_nodes >= 0 && n_nodes < (1 << 24) &&
-                    n_nodes * ldc * 2 < ((int64_t)1 << 31) &&
-                    ldc * 2 < (1 << 24) && (int64_t)B + n_nodes <= (int64_t)kColMask,
-                "spmm_task_cb: codes [%lld x %lld] out of range", (long long)n_nodes,
-                (long long)ldc);
   VQGNN_REQUIRE(ldw >= D && ldw % 4 == 0 && bstride % 4 == 0 && ((uintptr_t)codewords & 15) == 0,
                 "spmm_task_cb: codeword rows must be 16-byte aligned");
   a.codes = codes;

@@ -90,16 +90,21 @@ class CodebookSync:
         self._ev_i = 0
         # no strong reference from an exit hook: a dropped CodebookSync frees
         # its communicators and side stream at once
-        self._finalizer = weakref.finalize(self, _release_comms, self._ca, self._cb)
+        # close() flips the flag: only a clean shutdown destroys (which flushes
+        # and can wait on a peer); any other release aborts
+        self._clean = [False]
+        self._finalizer = weakref.finalize(self, _release_comms, self._ca, self._cb, self._clean)
 
     def close(self):
         """Destroy the direct communicators after this rank's work drained
         (call on every rank at a clean shutdown).  Without it they are
-        released when the object is collected or at exit -- by ncclCommAbort
-        when the process exits on an uncaught exception, so a rank whose
-        peer died mid-collective exits instead of hanging in a destroy."""
+        released when the object is collected or at exit by ncclCommAbort
+        (whatever the exit path: an uncaught exception, sys.exit from a
+        handler, a failing thread), so a rank whose peer died mid-collective
+        exits instead of hanging in a destroy."""
         if getattr(self, "_finalizer", None) is not None and self._finalizer.alive:
             torch.cuda.synchronize()
+            self._clean[0] = True
             self._finalizer()
         self._ca = self._cb = None
 
@@ -295,16 +300,15 @@ class PendingWire:
                                  self.epoch)
 
 
-def _release_comms(ca, cb):
-    """Finalizer of CodebookSync's direct communicators.  An uncaught
-    exception (sys.last_type set by the interpreter's error print) may have
-    left a collective waiting for a peer that will never come: abort them.
-    Otherwise destroy them (the collectives have completed or will)."""
-    import sys
-    failing = getattr(sys, "last_type", None) is not None
+def _release_comms(ca, cb, clean):
+    """Finalizer of CodebookSync's direct communicators: destroy them only
+    after close() drained this rank's work (clean[0]); on any other release
+    -- collection or interpreter exit without close(), on any error path --
+    a collective may still wait for a peer that will never come, so abort
+    them (ncclCommAbort does not wait)."""
     for c in (ca, cb):
         if c is not None:
-            c.abort() if failing else c.destroy()
+            c.destroy() if clean[0] else c.abort()
 
 
 def _device_of(group):

@@ -257,20 +257,40 @@ def vq_ema_finalize(parts, D, W, decay, laplace, grad_scale, epsilon, cs, ema_w,
 
 
 def gather_codewords(subset, B, codes, emb_out, D, col_offset=0, want_x=True,
-                     want_codes=False):
+                     want_codes=False, nb=None):
     """models.py:168-173 for all branches: returns (xt [n-B, nb*D] or None,
     lcodes [n-B, nb] int16 or None).  col_offset 0 = feature halves
-    (x_first_order), D = grad halves (grad_first_order)."""
+    (x_first_order), D = grad halves (grad_first_order).  nb = the codebook's
+    branch count (emb_out.shape[0]); codes may hold more columns (a strided
+    c_indices view), never fewer."""
     n = subset.shape[0]
-    nb = codes.shape[1]
+    if subset.dtype != torch.int64 or subset.dim() != 1 or subset.stride(0) != 1:
+        raise ValueError("gather_codewords: subset must be a contiguous int64 [n] tensor")
+    if codes.dtype != torch.int16 or codes.dim() != 2 or codes.stride(1) != 1:
+        raise ValueError("gather_codewords: codes must be an int16 [N, ldc] row-major view")
+    if nb is None:
+        if emb_out is None:
+            raise ValueError("gather_codewords: nb is needed when emb_out is None")
+        nb = emb_out.shape[0]
+    nb = int(nb)
+    if codes.shape[1] < nb:
+        raise ValueError(f"gather_codewords: codes has {codes.shape[1]} columns < {nb} branches")
+    if emb_out is not None and emb_out.shape[0] < nb:
+        raise ValueError(f"gather_codewords: emb_out has {emb_out.shape[0]} branches < nb={nb}")
     dev = codes.device
     xt = torch.empty(n - B, nb * D, dtype=torch.float32, device=dev) if want_x else None
     lc = torch.empty(n - B, nb, dtype=torch.int16, device=dev) if want_codes else None
-    ldw = emb_out.shape[2] if emb_out is not None else 0
-    bstride = emb_out.stride(0) if emb_out is not None else 0
-    check(lib().vqgnn_gather_codewords(ptr(subset), B, n, ptr(codes), codes.stride(0), nb, D,
-                                       ptr(emb_out), ldw, bstride, int(col_offset), ptr(xt),
-                                       nb * D, ptr(lc), stream_ptr()), "gather_codewords")
+    if emb_out is not None:
+        n_br, M, ldw = (int(v) for v in emb_out.shape)
+        if emb_out.stride(2) != 1 or emb_out.stride(1) != ldw:
+            raise ValueError("gather_codewords: emb_out must be row-major per branch")
+        bstride = emb_out.stride(0)
+    else:
+        n_br, M, ldw, bstride = nb, 1, 0, 0
+    check(lib().vqgnn_gather_codewords(ptr(subset), B, n, ptr(codes), codes.stride(0),
+                                       codes.shape[0], nb, D, ptr(emb_out), n_br, M, ldw,
+                                       bstride, int(col_offset), ptr(xt), nb * D, ptr(lc),
+                                       stream_ptr()), "gather_codewords")
     return xt, lc
 
 
@@ -313,9 +333,11 @@ class TaskPlan:
     adjacency, valid for any F and any leading row count.  Building it reads
     the two job counts back to the host (one sync per plan)."""
 
-    def __init__(self, plan, records, K, nnz, n_rows, val, n_jobs, n_empty, rowptr=None):
+    def __init__(self, plan, records, K, nnz, n_rows, val, n_jobs, n_empty, rowptr=None,
+                 n_cols=None):
         self.plan, self.records, self.K = plan, records, K
         self.nnz, self.n_rows = nnz, n_rows
+        self.n_cols = n_cols          # columns of the planned CSR (None: not recorded)
         self.val_ptr = val.data_ptr() if val is not None else 0
         self.n_jobs, self.n_empty = n_jobs, n_empty
         self.rowptr = rowptr
@@ -330,18 +352,26 @@ class TaskPlan:
                                             self.nnz, ptr(records), stream_ptr()),
               "spmm_task_records")
         return TaskPlan(self.plan, records, self.K, self.nnz, self.n_rows, val, self.n_jobs,
-                        self.n_empty, self.rowptr)
+                        self.n_empty, self.rowptr, self.n_cols)
 
     def with_codebook_source(self, B, subset, n_nodes):
         """The plan of spmm_codebook (include/vqgnn.h §6b): a copy of the
         records whose columns j >= B name the node subset[j] (B + node id),
         so the kernel reads that node's codes instead of an x_first row."""
+        if subset.dtype != torch.int64 or subset.dim() != 1 or subset.stride(0) != 1:
+            raise ValueError("with_codebook_source: subset must be a contiguous int64 [n] "
+                             "tensor (the kernel reads it as int64 by record column)")
+        if self.n_cols is not None and subset.numel() != self.n_cols:
+            raise ValueError(f"with_codebook_source: subset has {subset.numel()} nodes, the "
+                             f"adjacency {self.n_cols} columns")
+        if not 0 <= int(B) <= subset.numel():
+            raise ValueError(f"with_codebook_source: B={B} outside [0, {subset.numel()}]")
         records = self.records.clone()
         check(lib().vqgnn_spmm_task_records_cb(ptr(records), self.nnz, int(B), ptr(subset),
                                                int(subset.numel()), int(n_nodes), stream_ptr()),
               "spmm_task_records_cb")
         p = TaskPlan(self.plan, records, self.K, self.nnz, self.n_rows, None, self.n_jobs,
-                     self.n_empty, self.rowptr)
+                     self.n_empty, self.rowptr, self.n_cols)
         p.val_ptr = self.val_ptr
         p.cb_B = int(B)
         return p
@@ -350,7 +380,7 @@ class TaskPlan:
 TASK_K = 64
 
 
-def spmm_task_plan(rowptr, col, val, n_rows, nnz, K=None):
+def spmm_task_plan(rowptr, col, val, n_rows, nnz, K=None, n_cols=None):
     L = lib()
     K = int(K or TASK_K)
     dev = rowptr.device
@@ -362,7 +392,8 @@ def spmm_task_plan(rowptr, col, val, n_rows, nnz, K=None):
                                  ptr(plan), ptr(records), ptr(counts), stream_ptr()),
           "spmm_task_plan")
     n_jobs, n_empty = (int(v) for v in counts.tolist())
-    return TaskPlan(plan, records, K, int(nnz), int(n_rows), val, n_jobs, n_empty, rowptr)
+    return TaskPlan(plan, records, K, int(nnz), int(n_rows), val, n_jobs, n_empty, rowptr,
+                    None if n_cols is None else int(n_cols))
 
 
 def spmm(rowptr, col, val, n_rows, nnz, X, F, X2=None, B=None, out=None, plan=None):
@@ -400,10 +431,25 @@ def spmm(rowptr, col, val, n_rows, nnz, X, F, X2=None, B=None, out=None, plan=No
 CB_MAX_M = 300      # the codebook-source SpMM's LDS image: (M + 1) x 512 B
 
 
-def codebook_source_ok(X, F, M, D, out=None):
-    """Whether spmm_codebook serves this layer shape (include/vqgnn.h §6b)."""
-    return (F % 128 == 0 and D > 0 and D % 4 == 0 and F % D == 0 and 0 < M <= CB_MAX_M and
-            X.stride(1) == 1 and X.stride(0) % 4 == 0 and X.data_ptr() % 16 == 0)
+def codebook_source_ok(X, F, M, D, out=None, codes=None, n_rows=None, n_branches=None):
+    """Whether spmm_codebook serves this layer shape (include/vqgnn.h §6b):
+    the kernel's own checks (vqgnn_spmm_task_cb_supported) plus the host-side
+    alignment of X.  codes / n_rows / n_branches default to shapes that pass
+    their checks; out defaults to a dense [n_rows, F]."""
+    if not (X.dim() == 2 and X.stride(1) == 1 and X.stride(0) % 4 == 0 and
+            X.data_ptr() % 16 == 0):
+        return False
+    if out is not None and not (out.stride(1) == 1 and out.stride(0) % 4 == 0 and
+                                out.data_ptr() % 16 == 0):
+        return False
+    B = X.shape[0]
+    nr = int(n_rows) if n_rows is not None else B
+    ldo = out.stride(0) if out is not None else F
+    nn, ldc = (codes.shape[0], codes.stride(0)) if codes is not None else (0, F // max(D, 1))
+    nbr = int(n_branches) if n_branches is not None else F // max(D, 1)
+    return bool(lib().vqgnn_spmm_task_cb_supported(int(nr), int(B), int(X.stride(0)), int(F),
+                                                   int(ldo), int(nn), int(ldc), nbr, int(M),
+                                                   int(D)))
 
 
 def spmm_codebook(rowptr, n_rows, nnz, X, F, B, codes, emb_out, D, plan_cb, out=None):
@@ -421,15 +467,19 @@ def spmm_codebook(rowptr, n_rows, nnz, X, F, B, codes, emb_out, D, plan_cb, out=
                          f"called with nnz={nnz}, n_rows={n_rows}")
     if codes.dtype != torch.int16 or emb_out.dtype != torch.float32:
         raise TypeError("spmm_codebook: codes must be int16 and emb_out float32")
+    if codes.dim() != 2 or codes.stride(1) != 1:
+        raise ValueError("spmm_codebook: codes must be an int16 [N, ldc] row-major view")
+    n_br, M, ldw = (int(v) for v in emb_out.shape)
+    if emb_out.stride(2) != 1 or emb_out.stride(1) != ldw:
+        raise ValueError("spmm_codebook: emb_out must be row-major per branch")
     dev = X.device
     if out is None:
         out = torch.empty(n_rows, F, dtype=torch.float32, device=dev)
     L = lib()
     ws = workspace(L.vqgnn_spmm_task_workspace(int(nnz), plan_cb.K, F), dev)
-    M = emb_out.shape[1]
     check(L.vqgnn_spmm_task_cb(ptr(rowptr), int(n_rows), int(nnz), int(B), ptr(X), _ld(X), F,
                                ptr(codes), codes.stride(0), codes.shape[0], ptr(emb_out),
-                               emb_out.stride(1), emb_out.stride(0), M, int(D), ptr(out),
+                               emb_out.stride(1), emb_out.stride(0), n_br, M, int(D), ptr(out),
                                _ld(out), ptr(plan_cb.plan), ptr(plan_cb.records), plan_cb.K,
                                plan_cb.n_jobs, plan_cb.n_empty, ptr(ws), stream_ptr()),
           "spmm_task_cb")

@@ -134,7 +134,7 @@ class CSR:
         p = self._plans.get("task")
         if p is None:
             p = kernels.spmm_task_plan(self.rowptr, self.col, self.value, self._sizes[0],
-                                       self._host_nnz)
+                                       self._host_nnz, n_cols=self._sizes[1])
             self._plans["task"] = p
         return p
 
