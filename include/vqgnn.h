@@ -321,7 +321,7 @@ int vqgnn_spmm_task(const int32_t* rowptr, int32_t n_rows, int32_t n_cols, int64
  *    vqgnn_spmm_task over [X ; gather_codewords(...)]: the same output.
  *    vqgnn_spmm_task_records_cb: copy of a plan's records (vqgnn_spmm_task_plan)
  *      rewritten in place: a column j >= B becomes B + subset[j] (the node
- *      whose codes give the row); requires B + n_nodes <= 2^26.
+ *      whose codes give the row); requires B + n_nodes < 2^26 - 1.
  *    vqgnn_spmm_task_cb: out = A @ x_in for the rewritten records; codes
  *      [n_nodes][ldc] int16 (c_indices, every code in [0, M)), codewords =
  *      emb_out [n_branches][M][ldw] (branch stride bstride, 16-byte aligned
@@ -410,7 +410,8 @@ int vqgnn_gat_edge_grad(const int32_t* rows, const int32_t* col, const float* co
  *     coefficient sum, and rows < norm_B normalised by that sum + 1e-16
  *     before the store (models.py:188; norm_B = 0: no normalisation) -- as
  *     ONE v_rcp_f32 of (sum + 1e-16) times each column, not the reference's
- *     IEEE division: within 3 ulp of vqgnn_gat_normalize's true quotient
+ *     IEEE division: within 2.5 * 2^-23 relative (<= 5 ulp) of
+ *     vqgnn_gat_normalize's true quotient
  *     (pinned in tests/test_gpu_gat.py), and the same bits for a row whether
  *     the plan cuts it across tasks (fix-up) or not (walker).  Replaces
  *     vqgnn_gat_coef + vqgnn_spmm_task + vqgnn_gat_normalize; the coefficients are
