@@ -321,7 +321,7 @@ int vqgnn_spmm_task(const int32_t* rowptr, int32_t n_rows, int32_t n_cols, int64
  *    vqgnn_spmm_task over [X ; gather_codewords(...)]: the same output.
  *    vqgnn_spmm_task_records_cb: copy of a plan's records (vqgnn_spmm_task_plan)
  *      rewritten in place: a column j >= B becomes B + subset[j] (the node
- *      whose codes give the row); requires B + n_nodes < 2^26 - 1.
+ *      whose codes give the row); requires B + n_nodes <= 2^26.
  *    vqgnn_spmm_task_cb: out = A @ x_in for the rewritten records; codes
  *      [n_nodes][ldc] int16 (c_indices, every code in [0, M)), codewords =
  *      emb_out [n_branches][M][ldw] (branch stride bstride, 16-byte aligned

@@ -538,184 +538,12 @@ spmm_task_kernel(TaskArgs a) {
   task_walk<G, NC, U, FAR, GAT, PART>(a, wv, nwaves);
 }
 
-// Codebook-source walk, pipelined across blocks (round 5): the round-4 walk
-// (32 lanes per task, two tasks per wave in lock-step, float4 columns) with
-// block b + 1's code and row loads issued BEFORE block b is consumed, so a
-// wave keeps U..2U edges in flight instead of waiting for each block's
-// slowest gather with nothing else outstanding.  Per block a wave keeps only
-// the record word pair (2 VGPRs): the row offsets are broadcast when the
-// loads are issued, the row-end words and weights when the block is consumed.
-// Every slot issues one code load (X edges: an offset past the range, 0 with
-// no access) and one row load (codebook edges: likewise), unconditionally,
-// so the compiler's wait counts stay exact; the codewords are read from the
-// LDS image once the block's codes have landed.  Same records, fma chain and
-// carries as task_walk<CB>: bit-identical output.
-template <int U>
-__device__ __forceinline__ void cb_walk_pipe(const TaskArgs& a, int wv, int nwaves,
-                                             const char* cb_img) {
-  constexpr int G = 32, TPW = 2;
-  const int lane = threadIdx.x & 63;
-  const int g = lane / G, k = lane % G;
-  const int t = wv * TPW + g;
-  const int nnz = min(a.nnz, a.rowptr[a.n_rows]);
-  if (wv >= nwaves || wv * TPW >= a.ntasks) return;
-  const int wbase = a.task_start[wv * TPW];
-  if (wbase >= nnz) return;
-  const bool tv = t < a.ntasks;
-  const int e0 = tv ? min(a.task_start[t], nnz) : nnz;
-  const bool valid = e0 < nnz;
-  const int e1 = valid ? min(nnz, a.task_start[t + 1]) : e0;
-  const int c4base = (int)blockIdx.y * G + k;
-  const uint32_t lane_off = (uint32_t)c4base * 16u;
-  const uint32_t lane_boff = (uint32_t)((4 * c4base) / a.cb_D) * 2u;
-  const uint32_t lane16 = (uint32_t)k * 16u;
-  int r = valid ? a.task_row[t] : 0;
-  bool head = valid && a.rowptr[r] < e0;
-  const __amdgpu_buffer_rsrc_t rsx =
-      __builtin_amdgcn_make_buffer_rsrc((void*)a.ubase, 0, (int)a.span, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rsr = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(a.rec + wbase), 0,
-      (int)(uint32_t)min((int64_t)(a.nnz - wbase) * 8, (int64_t)0x7FFFFFFF), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rsc =
-      __builtin_amdgcn_make_buffer_rsrc((void*)a.codes, 0, (int)a.codes_bytes, 0x00020000);
-  constexpr int kAnd = 0x1F & ~(G - 1);
-  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-
-  auto load_rec = [&](int e) -> int2 {
-    return __builtin_bit_cast(
-        int2, __builtin_amdgcn_raw_buffer_load_b64(rsr, (uint32_t)(e - wbase + k) * 8u, 0, 0));
-  };
-  // records outside [e0, e1) (and lanes >= U): the column kColMask (loads
-  // nothing, reads no codeword), weight 0, no row end
-  auto mask_rec = [&](int2 q, int e) -> int2 {
-    const int eu = e + k;
-    return (k < U && eu >= e0 && eu < e1) ? q : make_int2((int)kColMask, 0);
-  };
-  int len = e1 - e0;
-  len = max(len, __shfl_xor(len, 32));
-  const int nblk = __builtin_amdgcn_readfirstlane((len + U - 1) / U);
-
-  // codes (all lanes; an X edge's offset is past the range) and rows (all
-  // lanes; a codebook edge's offset, bit 31 set, is past the range) of the
-  // block whose masked records q are given
-  auto issue = [&](int2 q, uint32_t (&cd)[U], float4 (&v)[U]) {
-    const uint32_t x = (uint32_t)q.x;
-    const uint32_t j = x & kColMask;
-    const bool s1 = (int)j < a.B;
-    // a masked record (outside the task, or past its end) loads nothing:
-    // 0xFFFF0000 is past both ranges (X < 2^31; codes, XOR 2^31, <= 0x7FFF0000
-    // bytes)
-    const uint32_t roff = x == kColMask ? 0xFFFF0000u
-                        : s1 ? __umul24(x, a.ldxb) + a.offx
-                             : 0x80000000u | __umul24(j - (uint32_t)a.B, a.ldcb);
-    int co[U];
-    group_bcast<kAnd>((int)roff, co, std::make_integer_sequence<int, U>{});
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-      cd[u] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(
-          rsc, ((uint32_t)co[u] ^ 0x80000000u) + lane_boff, 0, 0);
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-      v[u] = __builtin_bit_cast(
-          float4, __builtin_amdgcn_raw_buffer_load_b128(rsx, (uint32_t)co[u] + lane_off, 0, 0));
-  };
-  auto consume = [&](int2 q, int e, const uint32_t (&cd)[U], float4 (&v)[U]) {
-    int cx[U], cw[U];
-    group_bcast<kAnd>(q.x, cx, std::make_integer_sequence<int, U>{});
-    group_bcast<kAnd>(q.y, cw, std::make_integer_sequence<int, U>{});
-    // the block's codewords from the LDS image (codebook edges only)
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int j = (int)((uint32_t)cx[u] & kColMask);
-      if (j >= a.B && j != (int)kColMask)
-        v[u] = *reinterpret_cast<const float4*>(cb_img + (cd[u] & 0xffffu) * 512u + lane16);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const float w = __int_as_float(cw[u]);
-      acc.x = fmaf(w, v[u].x, acc.x);
-      acc.y = fmaf(w, v[u].y, acc.y);
-      acc.z = fmaf(w, v[u].z, acc.z);
-      acc.w = fmaf(w, v[u].w, acc.w);
-      const uint32_t x = (uint32_t)cx[u];
-      if (x & kEndBit) {                   // the row ends at this edge
-        float* dst = head ? a.carry + (int64_t)t * 2 * a.cf
-                          : reinterpret_cast<float*>(reinterpret_cast<char*>(a.out) +
-                                                     (uint64_t)(uint32_t)__umul24((uint32_t)r, a.ldob));
-        *reinterpret_cast<float4*>(dst + 4 * c4base) = acc;
-        acc = make_float4(0.f, 0.f, 0.f, 0.f);
-        const uint32_t skip = (x >> kSkipShift) & kSkipEsc;
-        r = skip == kSkipEsc ? upper_bound_i32(a.rowptr, a.n_rows, e + u + 1) - 1
-                             : r + 1 + (int)skip;
-        head = false;
-      }
-    }
-  };
-
-  uint32_t cdA[U], cdB[U];
-  float4 vA[U], vB[U];
-  int2 qA = mask_rec(load_rec(e0), e0);
-  int2 r1 = load_rec(e0 + U);
-  issue(qA, cdA, vA);
-  for (int bi = 0; bi < nblk; bi += 2) {
-    const int e = e0 + bi * U;
-    const int2 r2 = load_rec(e + 2 * U);
-    // the next block's loads are issued unconditionally (past the walk its
-    // records are masked: nothing is read), so every path issues the same
-    // loads and the compiler's wait counts stay exact
-    const int2 qB = mask_rec(r1, e + U);
-    issue(qB, cdB, vB);
-    consume(qA, e, cdA, vA);
-    if (bi + 1 >= nblk) break;
-    r1 = load_rec(e + 3 * U);
-    qA = mask_rec(r2, e + 2 * U);
-    issue(qA, cdA, vA);
-    consume(qB, e + U, cdB, vB);
-  }
-  const bool open = valid && !(__builtin_amdgcn_raw_buffer_load_b32(rsr, (uint32_t)(e1 - 1 - wbase) * 8u,
-                                                                    0, 0) & (int)kEndBit);
-  if (open) *reinterpret_cast<float4*>(a.carry + ((int64_t)t * 2 + 1) * a.cf + 4 * c4base) = acc;
-}
-
-template <int U>
-__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4)))
-spmm_task_cb_pipe_kernel(TaskArgs a, int nunits) {
-  extern __shared__ __attribute__((aligned(16))) char cb_smem[];
-  const int tile = blockIdx.y;
-  const int F4 = a.F >> 2;
-  for (int i = threadIdx.x; i < a.cb_M * 32; i += 1024) {
-    const int m = i >> 5, c4 = tile * 32 + (i & 31);
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (c4 < F4) {
-      const int col = 4 * c4, b = col / a.cb_D, d = col % a.cb_D;
-      v = *reinterpret_cast<const float4*>(a.cbe + b * a.cb_bstride + (int64_t)m * a.cb_ldw + d);
-    }
-    *reinterpret_cast<float4*>(cb_smem + (size_t)i * 16) = v;
-  }
-  __syncthreads();
-  const int wave = threadIdx.x >> 6;
-  const int g = xcd_remap(blockIdx.x, gridDim.x);
-  const int stride = (int)gridDim.x * 16;
-  for (int u0 = g * 16; u0 < nunits; u0 += stride) {
-    const int wv = __builtin_amdgcn_readfirstlane(u0 + wave);
-    cb_walk_pipe<U>(a, wv, nunits, cb_smem);
-  }
-}
-
 // Codebook-source task kernel: persistent 16-wave workgroups (the LDS
 // image leaves one per CU), one per CU and column tile; the workgroup stages
 // its tile's codeword features -- image row m = the 128 columns of codeword
 // m's branches, 512 B, so lane k always reads banks 4k..4k+3: conflict-free
 // whatever the codes -- and its waves walk task pairs round-robin.
 constexpr int kCbThreads = 1024;
-#ifndef VQGNN_CB_STREAM_U
-#define VQGNN_CB_STREAM_U 16
-#endif
-constexpr int kCbStreamU = VQGNN_CB_STREAM_U;   // edges per block of the stream walker
-#ifndef VQGNN_CB_PIPE_U
-#define VQGNN_CB_PIPE_U 8
-#endif
-constexpr int kCbPipeU = VQGNN_CB_PIPE_U;       // edges per block of the pipelined walk
 
 template <int U>
 __global__ void __launch_bounds__(kCbThreads) __attribute__((amdgpu_waves_per_eu(4)))
@@ -740,214 +568,6 @@ spmm_task_cb_kernel(TaskArgs a, int nunits) {
     const int wv = __builtin_amdgcn_readfirstlane(u0 + wave);
     task_walk<32, 1, U, false, false, false, true>(a, wv, nunits);
   }
-}
-
-// scalar selects (s_cselect): c, a, b wave-uniform.  Written out because the
-// compiler lowers a select between two scalars it loaded from the kernel
-// arguments as a load through a selected address (private memory, per-lane)
-__device__ __forceinline__ uint64_t sel64(uint32_t c, uint64_t a, uint64_t b) {
-  uint64_t r;
-  asm volatile("s_cmp_lg_u32 %1, 0\n\ts_cselect_b64 %0, %2, %3" : "=s"(r) : "s"(c), "s"(a), "s"(b)
-               : "scc");
-  return r;
-}
-__device__ __forceinline__ uint32_t sel32(uint32_t c, uint32_t a, uint32_t b) {
-  uint32_t r;
-  asm volatile("s_cmp_lg_u32 %1, 0\n\ts_cselect_b32 %0, %2, %3" : "=s"(r) : "s"(c), "s"(a), "s"(b)
-               : "scc");
-  return r;
-}
-
-// a wave-uniform 64-bit value the compiler can keep in SGPRs
-__device__ __forceinline__ uint64_t uni64(uint64_t v) {
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-  return ((uint64_t)hi << 32) | lo;
-}
-
-// Codebook-source stream walker (round 5, the default for vqgnn_spmm_task_cb).
-// One wave walks a run of `tpw` consecutive tasks of the plan as ONE edge
-// stream, every edge wave-uniform: lane l owns the float2 columns 2l, 2l + 1
-// of the 128-column tile, and each edge's record reaches the wave as scalars
-// (v_readlane of the record lane's words), so the source row's byte offset
-// is the buffer load's soffset and the X / codebook choice and the row ends
-// are scalar branches (no per-lane record broadcasts).  The loads stream:
-// block k + 1's row (X edge) or code (codebook edge) loads are issued before
-// block k is consumed, and the records two blocks ahead, so U..2U edges are
-// in flight per wave throughout the run instead of a block of U waiting for
-// its slowest gather.  A task boundary inside the run stores the open row as
-// that task's tail carry and starts the next task's head -- the partials and
-// their order are those of one walk per task, so the output is
-// bit-identical to spmm_task_cb_kernel (and to gather + spmm_task_kernel).
-// One run of tasks [t0, t1) (t1 - t0 <= 63) of the stream walker.
-template <int U>
-__device__ __forceinline__ void stream_cb_run(const TaskArgs& a, int t0, int t1, int nnz, int lane,
-                                              const char* cb_smem) {
-  // the run's task starts, one per lane (a boundary reads its lane: no load,
-  // so no wait on the stream of row loads in flight)
-  const int tsv = lane <= t1 - t0 ? min(a.task_start[t0 + lane], nnz) : nnz;
-  const int E0 = __builtin_amdgcn_readlane(tsv, 0);
-  const int E1 = __builtin_amdgcn_readlane(tsv, t1 - t0);
-  if (E0 >= E1) return;
-  const int tile = blockIdx.y;
-  // the run's records from E0 (past E1: zeros, never consumed)
-  const __amdgpu_buffer_rsrc_t rsr = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(a.rec + E0), 0, (E1 - E0) * 8, 0x00020000);
-  // both sources' bases and ranges as values (readfirstlane: a select of two
-  // kernel-argument loads would otherwise become a load through a selected
-  // address, copying the arguments to private memory)
-  const uint64_t pcodes = uni64((uint64_t)(uintptr_t)a.codes);
-  const uint64_t pxrows = uni64((uint64_t)(uintptr_t)a.ubase);
-  const int ncodes = __builtin_amdgcn_readfirstlane((int)a.codes_bytes);
-  const int nxrows = __builtin_amdgcn_readfirstlane((int)a.span);
-  const int col0 = tile * 128 + 2 * lane;                  // this lane's first column
-  const uint32_t xvoff = (uint32_t)col0 * 4u;              // byte offset in an X row
-  // its branch's code in a code row: the aligned 8 bytes holding it, and its
-  // bit position inside them (code rows are 8-byte aligned: ldc % 4 == 0)
-  const uint32_t cvoff8 = ((uint32_t)(col0 / a.cb_D) * 2u) & ~7u;
-  const uint32_t cshift = (((uint32_t)(col0 / a.cb_D) * 2u) & 7u) * 8u;
-  const char* img = cb_smem + lane * 8;                     // image row m at m * 512
-  const bool cv = col0 < a.F;                               // (F a multiple of 128: always)
-
-  int cur = t0;                                             // the task holding the next edge
-  int nbnd = t0 + 1 < t1 ? __builtin_amdgcn_readlane(tsv, 1) : 0x7fffffff;
-  int r = a.task_row[t0];
-  bool head = a.rowptr[r] < E0;                             // first row began in an earlier task
-  bool open = false;                                        // acc holds part of a row
-  float2 acc = make_float2(0.f, 0.f);
-
-  struct Blk {
-    int eb, n;            // first edge, edges in the block (<= 0: none)
-    int x;                // record lane u: column | skip << 26 | end << 31
-    int w;                // weight bits
-    uint32_t off;         // X: row byte offset in rsx; codebook: 2^31 | code row offset
-    uint64_t cbm, endm;   // codebook edges, row ends (bit u)
-  };
-  auto load_rec = [&](int eb) -> int2 {
-    return __builtin_bit_cast(
-        int2, __builtin_amdgcn_raw_buffer_load_b64(rsr, (uint32_t)(eb - E0 + lane) * 8u, 0, 0));
-  };
-  auto prep = [&](int2 q, int eb) -> Blk {
-    Blk bk;
-    bk.eb = eb;
-    bk.n = __builtin_amdgcn_readfirstlane(min(U, E1 - eb));
-    const bool in = lane < bk.n;
-    const uint32_t x = (uint32_t)q.x;
-    const uint32_t j = x & kColMask;
-    const bool cb = (int)j >= a.B;
-    bk.x = q.x;
-    bk.w = q.y;
-    bk.off = cb ? 0x80000000u | __umul24(j - (uint32_t)a.B, a.ldcb) : __umul24(x, a.ldxb) + a.offx;
-    bk.cbm = uni64(__ballot(in && cb));
-    bk.endm = uni64(__ballot(in && (x & kEndBit)));
-    return bk;
-  };
-  // exactly one 8-byte load per slot, the same instruction on every path: an
-  // X edge reads the lane's float2 of the row, a codebook edge the aligned
-  // 8 bytes of the node's code row holding its branch's code (resource and
-  // lane offset chosen by scalar selects, no branch: the compiler's wait
-  // counts stay exact); edges past the block read past the X range (0, no
-  // memory access)
-  auto issue = [&](const Blk& bk, float2 (&v)[U]) {
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t o = (uint32_t)__builtin_amdgcn_readlane((int)bk.off, u);
-      const uint32_t cbu = (uint32_t)(bk.cbm >> u) & 1u;
-      const uint32_t so = cbu ? (o & 0x7fffffffu) : (u < bk.n ? o : 0x80000000u);
-      // (the descriptor built from selected scalars: a select between two
-      // descriptors is lowered through private memory)
-      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-          (void*)sel64(cbu, pcodes, pxrows), 0, (int)sel32(cbu, ncodes, nxrows), 0x00020000);
-      v[u] = __builtin_bit_cast(float2,
-                                __builtin_amdgcn_raw_buffer_load_b64(rs, (cbu ? cvoff8 : xvoff) + so, 0, 0));
-    }
-  };
-  auto consume = [&](const Blk& bk, float2 (&v)[U]) {
-    // the codewords of the block's codebook edges from the LDS image (their
-    // codes arrived with the X rows), all issued before the fma chain
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-      if ((bk.cbm >> u) & 1) {
-        const uint64_t c4 = __builtin_bit_cast(uint64_t, v[u]);    // codes of 4 branches
-        const uint32_t code = (uint32_t)(c4 >> cshift) & 0xffffu;
-        v[u] = *reinterpret_cast<const float2*>(img + code * 512u);
-      }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (u < bk.n) {
-        const int e = bk.eb + u;
-        while (e == nbnd) {             // a task boundary inside the run
-          if (open && cv)
-            *reinterpret_cast<float2*>(a.carry + ((int64_t)cur * 2 + 1) * a.cf + col0) = acc;
-          acc = make_float2(0.f, 0.f);
-          head = open;                  // the open row continues as the next task's head
-          ++cur;
-          nbnd = cur + 1 < t1 ? __builtin_amdgcn_readlane(tsv, cur + 1 - t0) : 0x7fffffff;
-        }
-        const float w = __int_as_float(__builtin_amdgcn_readlane(bk.w, u));
-        acc.x = fmaf(w, v[u].x, acc.x);
-        acc.y = fmaf(w, v[u].y, acc.y);
-        open = true;
-        if ((bk.endm >> u) & 1) {       // the row ends at this edge
-          float* dst = head ? a.carry + (int64_t)cur * 2 * a.cf
-                            : reinterpret_cast<float*>(reinterpret_cast<char*>(a.out) +
-                                                       (uint64_t)(uint32_t)__umul24((uint32_t)r, a.ldob));
-          if (cv) *reinterpret_cast<float2*>(dst + col0) = acc;
-          acc = make_float2(0.f, 0.f);
-          head = false;
-          open = false;
-          const uint32_t skip =
-              ((uint32_t)__builtin_amdgcn_readlane(bk.x, u) >> kSkipShift) & kSkipEsc;
-          r = skip == kSkipEsc ? upper_bound_i32(a.rowptr, a.n_rows, e + 1) - 1 : r + 1 + (int)skip;
-        }
-      }
-    }
-  };
-
-  const int nblk = (E1 - E0 + U - 1) / U;
-  float2 va[U], vb[U];
-  int2 q1 = load_rec(E0 + U);
-  Blk b0 = prep(load_rec(E0), E0);
-  issue(b0, va);
-  for (int k = 0; k < nblk; k += 2) {
-    const int eb = E0 + k * U;
-    const int2 q2 = load_rec(eb + 2 * U);
-    const Blk b1 = prep(q1, eb + U);
-    issue(b1, vb);
-    consume(b0, va);
-    if (k + 1 >= nblk) break;
-    q1 = load_rec(eb + 3 * U);
-    b0 = prep(q2, eb + 2 * U);
-    issue(b0, va);
-    consume(b1, vb);
-  }
-  if (open && cv)                       // the run's last row continues in the next task
-    *reinterpret_cast<float2*>(a.carry + ((int64_t)cur * 2 + 1) * a.cf + col0) = acc;
-}
-
-template <int U>
-__global__ void __launch_bounds__(kCbThreads) __attribute__((amdgpu_waves_per_eu(4)))
-spmm_stream_cb_kernel(TaskArgs a, int tpw) {
-  extern __shared__ __attribute__((aligned(16))) char cb_smem[];
-  const int tile = blockIdx.y;
-  const int F4 = a.F >> 2;
-  for (int i = threadIdx.x; i < a.cb_M * 32; i += kCbThreads) {
-    const int m = i >> 5, c4 = tile * 32 + (i & 31);
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (c4 < F4) {
-      const int col = 4 * c4, b = col / a.cb_D, d = col % a.cb_D;
-      v = *reinterpret_cast<const float4*>(a.cbe + b * a.cb_bstride + (int64_t)m * a.cb_ldw + d);
-    }
-    *reinterpret_cast<float4*>(cb_smem + (size_t)i * 16) = v;
-  }
-  __syncthreads();
-  const int lane = threadIdx.x & 63;
-  const int gw = __builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, gridDim.x) * (kCbThreads / 64) +
-                                                (int)(threadIdx.x >> 6));
-  const int nwaves = (int)gridDim.x * (kCbThreads / 64);
-  const int nnz = min(a.nnz, a.rowptr[a.n_rows]);
-  for (int t0 = gw * tpw; t0 < a.ntasks; t0 += nwaves * tpw)   // no barrier below this point
-    stream_cb_run<U>(a, t0, min(a.ntasks, t0 + tpw), nnz, lane, cb_smem);
 }
 
 // One wave per fix-up job.  A cut row: out[row] = tail[ts] + ... + tail[t-1]
@@ -1266,8 +886,8 @@ extern "C" int vqgnn_spmm_task_records_cb(int64_t* records, int64_t nnz, int32_t
                 "spmm_task_records_cb: bad arguments");
   VQGNN_REQUIRE(nnz == 0 || (records && (n_cols == B || nodes)),
                 "spmm_task_records_cb: null pointer");
-  VQGNN_REQUIRE((int64_t)B + n_nodes < (int64_t)kColMask,
-                "spmm_task_records_cb: B + %lld nodes reach 2^26 - 1", (long long)n_nodes);
+  VQGNN_REQUIRE((int64_t)B + n_nodes <= (int64_t)kColMask,
+                "spmm_task_records_cb: B + %lld nodes exceed 2^26", (long long)n_nodes);
   if (nnz > 0 && n_cols > B)
     hipLaunchKernelGGL(task_remap_cb_kernel, dim3((unsigned)((nnz + 255) / 256)), dim3(256), 0,
                        as_stream(stream), reinterpret_cast<int2*>(records), (int)nnz, B, n_cols, nodes,
@@ -1290,8 +910,8 @@ static const char* cb_unsupported(int32_t n_rows, int32_t B, int64_t ldx, int32_
   if (F / D > n_branches) return "F / D code columns exceed the codebook's branches";
   if (M <= 0 || M > 300) return "M above the LDS image (300)";
   if (ldc < F / D || n_nodes < 0 || n_nodes >= (1 << 24) ||
-      n_nodes * ldc * 2 > (int64_t)0x7FFF0000 || ldc * 2 >= (1 << 24) ||
-      (int64_t)B + n_nodes >= (int64_t)kColMask)   // (kColMask: the walk's masked-record column)
+      n_nodes * ldc * 2 >= ((int64_t)1 << 31) || ldc * 2 >= (1 << 24) ||
+      (int64_t)B + n_nodes > (int64_t)kColMask)
     return "codes out of range";
   if (n_rows < 0 || n_rows >= (1 << 24) || B < 0 || B >= (1 << 24)) return "rows above 2^24";
   if (ldx < F || ldo < F || ldx * 4 >= (1 << 24) || ldo * 4 >= (1 << 24))
@@ -1352,43 +972,11 @@ extern "C" int vqgnn_spmm_task_cb(const int32_t* rowptr, int32_t n_rows, int64_t
     if (hipGetDevice(&dev) == hipSuccess)
       (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     (void)hipGetLastError();
-    constexpr int kWavesPerWg = kCbThreads / 64;
-    const int walk = task_env("VQGNN_CB_WALK", 0);
-    if (walk == 2) {        // pipelined round-4 walk (the default)
-      static const bool pattr = [] {
-        (void)hipFuncSetAttribute((const void*)spmm_task_cb_pipe_kernel<kCbPipeU>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        return true;
-      }();
-      (void)pattr;
-      const int nunits = (a.ntasks + 1) / 2;
-      int wgs = (nunits + kWavesPerWg - 1) / kWavesPerWg;
-      wgs = wgs < cus ? wgs : cus;
-      hipLaunchKernelGGL(spmm_task_cb_pipe_kernel<kCbPipeU>, dim3(wgs, F / 128), dim3(kCbThreads),
-                         lds, s, a, nunits);
-    } else if (walk == 1 && ldc % 4 == 0 && ((uintptr_t)codes & 7) == 0) {
-      // stream walker: runs of tpw <= 63 consecutive tasks, one per wave of
-      // one round of persistent waves where they suffice (one 16-wave
-      // workgroup per CU and column tile), else looped
-      int wgs = (a.ntasks + kWavesPerWg - 1) / kWavesPerWg;
-      wgs = wgs < cus ? wgs : cus;
-      int tpw = (a.ntasks + wgs * kWavesPerWg - 1) / (wgs * kWavesPerWg);
-      tpw = tpw < 63 ? tpw : 63;
-      static const bool sattr = [] {
-        (void)hipFuncSetAttribute((const void*)spmm_stream_cb_kernel<kCbStreamU>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        return true;
-      }();
-      (void)sattr;
-      hipLaunchKernelGGL(spmm_stream_cb_kernel<kCbStreamU>, dim3(wgs, F / 128), dim3(kCbThreads),
-                         lds, s, a, tpw);
-    } else {   // VQGNN_CB_WALK=0: the round-4 walker (two tasks per wave, broadcast records)
-      const int nunits = (a.ntasks + 1) / 2;
-      int wgs = (nunits + kWavesPerWg - 1) / kWavesPerWg;
-      wgs = wgs < cus ? wgs : cus;
-      hipLaunchKernelGGL(spmm_task_cb_kernel<8>, dim3(wgs, F / 128), dim3(kCbThreads), lds, s, a,
-                         nunits);
-    }
+    const int nunits = (a.ntasks + 1) / 2;
+    int wgs = (nunits + kCbThreads / 64 - 1) / (kCbThreads / 64);
+    wgs = wgs < cus ? wgs : cus;
+    hipLaunchKernelGGL(spmm_task_cb_kernel<8>, dim3(wgs, F / 128), dim3(kCbThreads), lds, s, a,
+                       nunits);
   }
   task_fixup<false>(a, s);
   return check_launch("spmm_task_cb");
