@@ -410,7 +410,7 @@ int vqgnn_gat_edge_grad(const int32_t* rows, const int32_t* col, const float* co
  *     coefficient sum, and rows < norm_B normalised by that sum + 1e-16
  *     before the store (models.py:188; norm_B = 0: no normalisation) -- as
  *     ONE v_rcp_f32 of (sum + 1e-16) times each column, not the reference's
- *     IEEE division: within 2.5 * 2^-23 relative (<= 5 ulp) of
+ *     IEEE division: within 2^-20 relative (measured <= 5 ulp) of
  *     vqgnn_gat_normalize's true quotient
  *     (pinned in tests/test_gpu_gat.py), and the same bits for a row whether
  *     the plan cuts it across tasks (fix-up) or not (walker).  Replaces

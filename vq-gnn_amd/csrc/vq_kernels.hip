@@ -1405,6 +1405,15 @@ __device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
   return r;
 }
 
+// Position of codeword m in the resolve's f32 planes (ef k-planes, |e|^2):
+// the two 16-codeword halves of a tile pair swap places when bit 1 of the
+// pair index is set.  A resolve read (one k-plane, one half t, a run of 4
+// codewords of the winning quad) then falls on bank slot 8 (pair & 1) +
+// 4 (t ^ (pair >> 1 & 1)) + quad: 16 slots over the 32 (pair, quad) sets of
+// a 256-codeword chunk instead of 8, fewer lanes of a 16-lane group on one
+// bank.  Runs of 4 stay contiguous; chunks are multiples of 32 codewords.
+__device__ __forceinline__ int flt_pos(int m) { return m ^ (((m >> 6) & 1) << 4); }
+
 // stage codebook rows [mc0, mc0 + chunk + slack) of E: planes -2 e_hi,
 // -2 e_lo, (|e|^2 split, 1, 1, 1, 0, 0) and |e|^2 in f32 (vq.py's order);
 // past mcount: zero planes, |e|^2 = +inf.  Codewords with |e|^2 >= 2^15 (or
@@ -1454,10 +1463,10 @@ __device__ __forceinline__ void stage_filter(const float* __restrict__ E, int ld
     p0[m] = hi;
     p1[m] = lo;
     p2[m] = sp;
-    sef[m] = mv ? s : INFINITY;
+    sef[flt_pos(m)] = mv ? s : INFINITY;
     if (ef) {                     // k-planes [8][cs]: a run of 4 codewords is one float4
 #pragma unroll
-      for (int k = 0; k < 8; ++k) ef[k * cs + m] = e[k];
+      for (int k = 0; k < 8; ++k) ef[k * cs + flt_pos(m)] = e[k];
     }
   }
 }
@@ -1867,18 +1876,19 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
           const int m0 = pw * 32 + t * 16 + 4 * qw;
+          const int p0 = flt_pos(m0);
           float d4[4];
 #pragma unroll
           for (int k = 0; k < 8; ++k) {
             if (k < W) {
-              const float4 ek = *reinterpret_cast<const float4*>(ef + k * cs + m0);
+              const float4 ek = *reinterpret_cast<const float4*>(ef + k * cs + p0);
               const float ev[4] = {ek.x, ek.y, ek.z, ek.w};
 #pragma unroll
               for (int c = 0; c < 4; ++c)
                 d4[c] = (k == 0) ? __fmul_rn(ev[c], xr[k]) : fmaf(ev[c], xr[k], d4[c]);
             }
           }
-          const float4 s4 = *reinterpret_cast<const float4*>(sef + m0);
+          const float4 s4 = *reinterpret_cast<const float4*>(sef + p0);
           const float sv[4] = {s4.x, s4.y, s4.z, s4.w};
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
@@ -1914,7 +1924,7 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
 #pragma unroll
         for (int k = 0; k < 8; ++k)
           if (k < W) dot = (k == 0) ? __fmul_rn(e[k], xr[k]) : fmaf(e[k], xr[k], dot);
-        const float se_c = sef[cv ? ci : 0];
+        const float se_c = sef[cv ? flt_pos(ci) : 0];
         const float dd = cv ? fmaf(-2.f, dot, __fadd_rn(sx, se_c)) : INFINITY;
         if (dd < dm) {
           dm = dd;
