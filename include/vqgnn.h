@@ -325,11 +325,13 @@ int vqgnn_spmm_task(const int32_t* rowptr, int32_t n_rows, int32_t n_cols, int64
  *    vqgnn_spmm_task_cb: out = A @ x_in for the rewritten records; codes
  *      [n_nodes][ldc] int16 (c_indices, every code in [0, M)), codewords =
  *      emb_out [n_branches][M][ldw] (branch stride bstride, 16-byte aligned
- *      rows); the F / D code columns read must not exceed n_branches; F a
- *      multiple of 128, D a multiple of 4, M <= 300 (the LDS image: M x 512
- *      bytes per 128-column tile, vqgnn_spmm_task_cb_lds); X and out on the
- *      32-bit near path.  Any other shape: VQGNN_ERR_INVALID (use
- *      vqgnn_gather_codewords + vqgnn_spmm_task, which has a 64-bit path).
+ *      rows); the F / D code columns read must not exceed n_branches; D a
+ *      multiple of 4; the image of a column tile of 4G columns is M x 16G
+ *      bytes <= 160 KiB with 4G dividing F (G = 32: M <= 320 at F % 128 ==
+ *      0; G = 16: M <= 640 at F % 64 == 0; G = 8: M <= 1,280 at F % 32 ==
+ *      0), vqgnn_spmm_task_cb_lds; X and out on the 32-bit near path.  Any
+ *      other shape: VQGNN_ERR_INVALID (use vqgnn_gather_codewords +
+ *      vqgnn_spmm_task, which has a 64-bit path).
  *    vqgnn_spmm_task_cb_supported: 1 iff vqgnn_spmm_task_cb accepts this
  *      shape (the same checks, no launch), so a host falls back before the
  *      call instead of catching its error.                                   */

@@ -8,7 +8,9 @@ Two forms:
          models.py:181-185): per layer gather + SpMM forward, A^T backward;
   hook   vq_update_in_backward=True (v1 semantics): each
          layer's backward also runs the batched VQ update (assign + EMA) on
-         dOut[:B].
+         dOut[:B];
+  hook_overlap  the same with that update on a side stream beside the
+         layer's A^T product (VQGNN_HOOK_OVERLAP=1).
 Prints one JSON line per form: ms per step, model edges/s = 3 * nnz / step.
 """
 import argparse
@@ -37,7 +39,9 @@ def run(form, steps, warmup, cfg_name):
     torch.manual_seed(0)
     model = LowRankGNN(F, F, 40, 3, 0.0, M, 4, g.N, no_second_fc=True, skip=True,
                        grad_scale=[1, 1], act='relu', bn_flag=True, warm_up_flag=True,
-                       conv_type=cfg["conv"], vq_update_in_backward=(form == "hook")).to(dev)
+                       conv_type=cfg["conv"],
+                       vq_update_in_backward=form.startswith("hook")).to(dev)
+    os.environ["VQGNN_HOOK_OVERLAP"] = "1" if form == "hook_overlap" else "0"
     batch_A = batch_to_device(b, dev)
     x = torch.randn(b.B, F, device=dev)
     y = torch.randint(0, 40, (b.B,), device=dev)
@@ -75,7 +79,7 @@ def main():
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--config", default="arxiv_gcn")
-    p.add_argument("--forms", default="v2,hook")
+    p.add_argument("--forms", default="v2,hook,hook_overlap")
     a = p.parse_args()
     for form in a.forms.split(","):
         print(json.dumps(run(form, a.steps, a.warmup, a.config)), flush=True)

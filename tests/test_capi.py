@@ -89,8 +89,11 @@ def test_codebook_reads_bounded_by_its_branch_count():
     assert h.vqgnn_spmm_task_cb_supported(100, 50, 128, 128, 128, 1000, 32, 16, 256, 4) == 0
     assert h.vqgnn_spmm_task_cb_supported(100, 50, 128, 128, 128, 1000, 32, 32, 256, 4) == 1
     # the kernel's other limits, mirrored by the query
-    assert h.vqgnn_spmm_task_cb_supported(100, 50, 128, 128, 128, 1000, 32, 32, 301, 4) == 0
+    assert h.vqgnn_spmm_task_cb_supported(100, 50, 128, 128, 128, 1000, 32, 32, 1281, 4) == 0
+    assert h.vqgnn_spmm_task_cb_supported(100, 50, 128, 128, 128, 1000, 32, 32, 1024, 4) == 1
+    assert h.vqgnn_spmm_task_cb_supported(100, 50, 96, 96, 96, 1000, 24, 24, 640, 4) == 1  # G = 8
+    assert h.vqgnn_spmm_task_cb_lds(256) == 256 * 512 and h.vqgnn_spmm_task_cb_lds(1024) == 1024 * 128
     assert h.vqgnn_spmm_task_cb_supported(1 << 24, 50, 128, 128, 128, 1000, 32, 32, 256, 4) == 0
     assert h.vqgnn_spmm_task_cb_supported(100, 5_000_000, 128, 128, 128, 1000, 32, 32, 256,
                                           4) == 0          # X past the 2 GiB near range
-    assert h.vqgnn_spmm_task_cb_supported(100, 50, 128, 64, 128, 1000, 16, 16, 256, 4) == 0
+    assert h.vqgnn_spmm_task_cb_supported(100, 50, 128, 40, 128, 1000, 16, 16, 256, 4) == 0

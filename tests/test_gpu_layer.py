@@ -314,3 +314,36 @@ def test_model_gat_train_step():
         loss.backward()
         opt.step()
         assert torch.isfinite(loss)
+
+
+@pytest.mark.parametrize("conv", ["GCN", "GAT"])
+def test_backward_update_on_side_stream_is_identical(conv, monkeypatch):
+    """VQGNN_HOOK_OVERLAP=1 runs the hook's batched update on a side stream
+    beside the layer's A^T product (convs._VQHook.start): the same codes,
+    codebook state and input gradient, bit for bit, as the update run in
+    stream order before the product."""
+    g, b = _small_batch(conv, seed=7)
+    F_in, F_out, M = 32, 16, 64
+    batch_A = graph.batch_to_device(b, DEV)
+    x = torch.randn(b.B, F_in, generator=torch.Generator().manual_seed(7)).to(DEV)
+    R = torch.randn(b.B, F_out, generator=torch.Generator().manual_seed(8)).to(DEV)
+    res = {}
+    for overlap in ("0", "1"):
+        monkeypatch.setenv("VQGNN_HOOK_OVERLAP", overlap)
+        torch.manual_seed(5)
+        layer = _layer(F_in, F_out, M, g.N, conv, vq_update_in_backward=True).to(DEV).train()
+        layer(x, batch_A, 1.0, False)             # init pass
+        for blk in layer.gnn_block:
+            blk.inited = True
+        xg = x.clone().requires_grad_(True)
+        for _ in range(2):
+            out, *_ = layer(xg, batch_A, 1.0, False)
+            (out * R).sum().backward()
+        torch.cuda.synchronize()
+        bank = layer._bank
+        res[overlap] = dict(codes=layer._codes.clone(), emb=bank.emb.clone(),
+                            emb_out=bank.emb_out.clone(), cs=bank.cs.clone(),
+                            ema_w=bank.ema_w.clone(), rm_g=bank.rm_g.clone(),
+                            rv_g=bank.rv_g.clone(), dx=xg.grad.clone())
+    for k in res["0"]:
+        assert torch.equal(res["0"][k], res["1"][k]), k

@@ -233,20 +233,41 @@ def test_codebook_source_arxiv_batch_and_strides():
     _check(out, b.rowptr, b.col, b.val, xin)
 
 
+@pytest.mark.parametrize("F,M,G", [(128, 512, 16), (128, 1024, 8), (64, 640, 16), (96, 1280, 8),
+                                   (32, 300, 8)])
+def test_codebook_source_narrow_tiles(F, M, G):
+    """Codebooks too large for a 128-column image (M > 320) walk narrower
+    column tiles of 4G columns (include/vqgnn.h §6b; reddit / arxiv-GAT use M =
+    1,024): bit-identical to gather + two-source SpMM and within 1e-5 of the
+    fp64 sum, hub rows and empty rows included."""
+    rng = np.random.default_rng(F + M)
+    B, n, N, D = 600, 1500, 4000, 4
+    a, rowptr, col, val, subset, codes, emb_out, X, plan = _cb_case(rng, B, n, N, F, M, D)
+    assert kernels.codebook_source_ok(X, F, M, D, codes=codes, n_rows=n, n_branches=F // D)
+    assert kernels.lib().vqgnn_spmm_task_cb_lds(M) == M * 16 * G
+    xf, _ = kernels.gather_codewords(subset, B, codes, emb_out, D)
+    ref = kernels.spmm(a.rowptr, a.col, a.value, n, a.nnz(), X, F, X2=xf, B=B, plan=plan)
+    out = kernels.spmm_codebook(a.rowptr, n, a.nnz(), X, F, B, codes, emb_out, D,
+                                plan.with_codebook_source(B, subset, N))
+    assert torch.equal(out, ref)
+    _check(out, rowptr, col, val, torch.cat([X, xf]).cpu().numpy())
+
+
 def test_codebook_source_rejects_unsupported():
     rng = np.random.default_rng(3)
     a, rowptr, col, val, subset, codes, emb_out, X, plan = _cb_case(rng, 50, 100, 300, 128, 256,
                                                                     4)
     pcb = plan.with_codebook_source(50, subset, 300)
-    with pytest.raises(RuntimeError, match="M=400"):
-        big = torch.randn(32, 400, 8, device=DEV)
-        kernels.spmm_codebook(a.rowptr, 100, a.nnz(), X, 128, 50, codes, big, 4, pcb)
+    with pytest.raises(RuntimeError, match="M=1300"):           # no tile fits 1,300 codewords
+        big = torch.randint(0, 1300, (300, 32), dtype=torch.int16, device=DEV)
+        kernels.spmm_codebook(a.rowptr, 100, a.nnz(), X, 128, 50, big,
+                              torch.randn(32, 1300, 8, device=DEV), 4, pcb)
     with pytest.raises(ValueError, match="with_codebook_source"):
         kernels.spmm_codebook(a.rowptr, 100, a.nnz(), X, 128, 50, codes, emb_out, 4, plan)
-    X64 = torch.randn(50, 64, device=DEV)
-    with pytest.raises(RuntimeError, match="multiple of 128"):
-        kernels.spmm_codebook(a.rowptr, 100, a.nnz(), X64, 64, 50, codes[:, :16],
-                              emb_out[:16], 4, pcb)
+    X40 = torch.randn(50, 40, device=DEV)
+    with pytest.raises(RuntimeError, match="multiple of 32"):
+        kernels.spmm_codebook(a.rowptr, 100, a.nnz(), X40, 40, 50, codes[:, :10],
+                              emb_out[:10], 4, pcb)
     # F / D = 32 code columns against a 16-branch codebook: rejected, no read
     with pytest.raises(RuntimeError, match="branches"):
         kernels.spmm_codebook(a.rowptr, 100, a.nnz(), X, 128, 50, codes, emb_out[:16], 4, pcb)
@@ -261,7 +282,7 @@ def test_codebook_source_rejects_unsupported():
     # CodebookInput falls back to the gathered rows where the kernel cannot
     from vq_gnn_amd.convs import CodebookInput
     assert CodebookInput(X, subset, codes, emb_out, 4).supported(100)
-    assert not CodebookInput(X, subset, codes, big, 4).supported(100)
+    assert not CodebookInput(X, subset, codes, torch.randn(32, 1300, 8, device=DEV), 4).supported(100)
     assert not CodebookInput(X, subset, codes, emb_out[:16], 4).supported(100)
 
 

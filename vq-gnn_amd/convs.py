@@ -14,6 +14,7 @@ each out-of-batch row's codewords from an LDS image of the codebook.
 from __future__ import annotations
 
 import math
+import os
 from typing import NamedTuple
 
 import torch
@@ -78,6 +79,39 @@ class _VQHook:
     def __call__(self, grad_out_B):
         self.layer._backward_vq_update(self.x, grad_out_B, self.batch_idx)
 
+    def start(self, grad_out_B):
+        """Run the update; with VQGNN_HOOK_OVERLAP=1 (single process) on a side
+        stream beside the caller's A^T product (the two are independent:
+        the update reads X and dOut[:B], writes codes and codebook; the
+        product reads dOut and the transposed adjacency).  Returns the side
+        stream to join after the product, or None."""
+        if os.environ.get("VQGNN_HOOK_OVERLAP", "0") != "1" or \
+                getattr(self.layer._bank, "comm", None) is not None:
+            self(grad_out_B)
+            return None
+        main = torch.cuda.current_stream()
+        side = _side_stream(grad_out_B.device)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            self(grad_out_B)
+        grad_out_B.record_stream(side)
+        return side
+
+
+_SIDE = {}
+
+
+def _side_stream(dev):
+    s = _SIDE.get(dev)
+    if s is None:
+        s = _SIDE[dev] = torch.cuda.Stream(device=dev)
+    return s
+
+
+def _join(side):
+    if side is not None:
+        torch.cuda.current_stream().wait_stream(side)
+
 
 class GatherSpMMFunction(torch.autograd.Function):
     """out = A @ [x ; x_first]; d/dx = (A^T @ dout)[:B] (x_first_order is a
@@ -98,8 +132,7 @@ class GatherSpMMFunction(torch.autograd.Function):
     def backward(ctx, dout):
         B = ctx.B
         dout = dout.contiguous()
-        if ctx.hook is not None:
-            ctx.hook(dout[:B])
+        side = ctx.hook.start(dout[:B]) if ctx.hook is not None else None
         dx = None
         if ctx.needs_input_grad[0]:
             at = ctx.adj.transposed()
@@ -108,6 +141,7 @@ class GatherSpMMFunction(torch.autograd.Function):
             # the walk with the full nnz, so no host read of t_rowptr[B] is needed
             dx = kernels.spmm(at.rowptr, at.col, at.value, B, at.nnz(), dout, F,
                               plan=at.plan(F, n_rows=B))
+        _join(side)
         return dx, None, None, None, None
 
 

@@ -27,6 +27,7 @@ import torch
 from torch import nn
 
 from . import kernels
+from .convs import _join
 from .sparse import as_csr
 
 
@@ -90,8 +91,7 @@ class GATFunction(torch.autograd.Function):
             dden[:B] = -(dz[:B] * z[:B]).sum(1) / q
         else:
             dy = dz
-        if ctx.hook is not None:
-            ctx.hook(dy[:B])
+        side = ctx.hook.start(dy[:B]) if ctx.hook is not None else None
         # coefficient chain -> d alpha_l, d alpha_r, d s
         dal, dar, dsr = kernels.gat_edge_grad(adj.rows(), adj.col, coef, nnz, xc, F, dy, dden,
                                               als, ars, params, X2=x_first, B=B,
@@ -132,6 +132,7 @@ class GATFunction(torch.autograd.Function):
             cplan = t.plan(F, kind="task").with_values(t.col, tcoef)
             dx = kernels.spmm(t.rowptr, t.col, tcoef, B, nnz, dy, F, plan=cplan)
             dx += dal[:B, None] * att_l.view(-1)[:F] + dar[:B, None] * att_r.view(-1)[:F]
+        _join(side)
         return dx, None, d_att_l, d_att_r, None, None, None, None, None, None, None
 
 

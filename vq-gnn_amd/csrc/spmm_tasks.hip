@@ -222,7 +222,7 @@ __device__ __forceinline__ float gat_edge_coef(const TaskArgs& a, int e, uint32_
 // returns 0 without a memory access) instead of reading the next row
 template <int G, int NC, int U, bool FAR, bool GAT, bool PART, bool CB = false>
 __device__ __forceinline__ void task_walk(const TaskArgs& a, int wv, int nwaves) {
-  static_assert(!CB || (G == 32 && NC == 1 && !FAR && !GAT && !PART), "CB: the default near shape");
+  static_assert(!CB || (NC == 1 && !FAR && !GAT && !PART), "CB: the near shape, one piece per lane");
   constexpr int TPW = 64 / G;
   const int lane = threadIdx.x & 63;
   const int g = lane / G, k = lane % G;
@@ -356,7 +356,7 @@ __device__ __forceinline__ void task_walk(const TaskArgs& a, int wv, int nwaves)
 #pragma unroll
       for (int u = 0; u < U; ++u)
         if (bk.co[u] < 0)
-          v[u][0] = *reinterpret_cast<const float4*>(cb_img + (cd[u] & 0xffffu) * 512u + lane16);
+          v[u][0] = *reinterpret_cast<const float4*>(cb_img + (cd[u] & 0xffffu) * (16u * G) + lane16);
       return;
     }
 #pragma unroll
@@ -540,19 +540,23 @@ spmm_task_kernel(TaskArgs a) {
 
 // Codebook-source task kernel: persistent 16-wave workgroups (the LDS
 // image leaves one per CU), one per CU and column tile; the workgroup stages
-// its tile's codeword features -- image row m = the 128 columns of codeword
-// m's branches, 512 B, so lane k always reads banks 4k..4k+3: conflict-free
-// whatever the codes -- and its waves walk task pairs round-robin.
+// its tile's codeword features -- image row m = the 4G columns of codeword
+// m's branches (G float4 pieces: 512 B at G = 32), so lane k always reads
+// banks 4k..4k+3 of its row: conflict-free within a task whatever the codes
+// -- and its waves walk task groups round-robin.  G = 32 (128-column tiles)
+// serves M <= 320; G = 16 (64 columns) M <= 640, G = 8 (32 columns) M <=
+// 1,280: narrower tiles fit larger codebooks, each tile walking every edge.
 constexpr int kCbThreads = 1024;
+constexpr size_t kCbLdsMax = 160 * 1024;
 
-template <int U>
+template <int G, int U>
 __global__ void __launch_bounds__(kCbThreads) __attribute__((amdgpu_waves_per_eu(4)))
 spmm_task_cb_kernel(TaskArgs a, int nunits) {
   extern __shared__ __attribute__((aligned(16))) char cb_smem[];
   const int tile = blockIdx.y;
   const int F4 = a.F >> 2;
-  for (int i = threadIdx.x; i < a.cb_M * 32; i += kCbThreads) {
-    const int m = i >> 5, c4 = tile * 32 + (i & 31);
+  for (int i = threadIdx.x; i < a.cb_M * G; i += kCbThreads) {
+    const int m = i / G, c4 = tile * G + (i % G);
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
     if (c4 < F4) {
       const int col = 4 * c4, b = col / a.cb_D, d = col % a.cb_D;
@@ -566,8 +570,16 @@ spmm_task_cb_kernel(TaskArgs a, int nunits) {
   const int stride = (int)gridDim.x * (kCbThreads / 64);
   for (int u0 = g * (kCbThreads / 64); u0 < nunits; u0 += stride) {
     const int wv = __builtin_amdgcn_readfirstlane(u0 + wave);
-    task_walk<32, 1, U, false, false, false, true>(a, wv, nunits);
+    task_walk<G, 1, U, false, false, false, true>(a, wv, nunits);
   }
+}
+
+// lanes per task of the codebook-source walk for a codebook of M codewords
+// over F columns: the widest tile whose LDS image fits (0: none)
+static int cb_lanes(int F, int M) {
+  for (int G = 32; G >= 8; G >>= 1)
+    if (F % (4 * G) == 0 && (size_t)M * G * 16 <= kCbLdsMax) return G;
+  return 0;
 }
 
 // One wave per fix-up job.  A cut row: out[row] = tail[ts] + ... + tail[t-1]
@@ -896,7 +908,12 @@ extern "C" int vqgnn_spmm_task_records_cb(int64_t* records, int64_t nnz, int32_t
 }
 
 extern "C" size_t vqgnn_spmm_task_cb_lds(int32_t M) {
-  return M > 0 ? (size_t)M * 512 : 0;
+  // bytes of the LDS image per column tile at the tile width M allows (any F
+  // the width divides); 0 when no tile fits
+  if (M <= 0) return 0;
+  for (int G = 32; G >= 8; G >>= 1)
+    if ((size_t)M * G * 16 <= kCbLdsMax) return (size_t)M * G * 16;
+  return 0;
 }
 
 // The shapes vqgnn_spmm_task_cb serves (its own checks below plus the near
@@ -905,10 +922,12 @@ extern "C" size_t vqgnn_spmm_task_cb_lds(int32_t M) {
 static const char* cb_unsupported(int32_t n_rows, int32_t B, int64_t ldx, int32_t F, int64_t ldo,
                                   int64_t n_nodes, int64_t ldc, int32_t n_branches, int32_t M,
                                   int32_t D) {
-  if (F <= 0 || F % 128 != 0) return "F must be a multiple of 128";
+  if (F <= 0 || F % 32 != 0) return "F must be a multiple of 32";
   if (D <= 0 || D % 4 != 0 || F % D != 0) return "D must be a multiple of 4 dividing F";
   if (F / D > n_branches) return "F / D code columns exceed the codebook's branches";
-  if (M <= 0 || M > 300) return "M above the LDS image (300)";
+  if (M <= 0 || cb_lanes(F, M) == 0)
+    return "M above the LDS image (M x 16G bytes <= 160 KiB with 4G | F: M <= 320 at F % 128 "
+           "== 0, 640 at F % 64 == 0, 1280)";
   if (ldc < F / D || n_nodes < 0 || n_nodes >= (1 << 24) ||
       n_nodes * ldc * 2 >= ((int64_t)1 << 31) || ldc * 2 >= (1 << 24) ||
       (int64_t)B + n_nodes > (int64_t)kColMask)
@@ -959,12 +978,15 @@ extern "C" int vqgnn_spmm_task_cb(const int32_t* rowptr, int32_t n_rows, int64_t
   a.cb_D = D;
   hipStream_t s = as_stream(stream);
   if (nnz > 0) {
-    const size_t lds = vqgnn_spmm_task_cb_lds(M);
-    // U = 8 edges per block (96 VGPRs); U = 12 measured the same (77.6 against
-    // 77.7 us on the arxiv batch), U = 16 spills
+    const int G = cb_lanes(F, M);
+    const size_t lds = (size_t)M * G * 16;
+    // U = 8 edges per block (96 VGPRs at G = 32); U = 12 measured the same
+    // (77.6 against 77.7 us on the arxiv batch), U = 16 spills
     static const bool attr_set = [] {
-      (void)hipFuncSetAttribute((const void*)spmm_task_cb_kernel<8>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      for (const void* f : {(const void*)spmm_task_cb_kernel<32, 8>,
+                            (const void*)spmm_task_cb_kernel<16, 8>,
+                            (const void*)spmm_task_cb_kernel<8, 8>})
+        (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kCbLdsMax);
       return true;
     }();
     (void)attr_set;
@@ -972,11 +994,17 @@ extern "C" int vqgnn_spmm_task_cb(const int32_t* rowptr, int32_t n_rows, int64_t
     if (hipGetDevice(&dev) == hipSuccess)
       (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     (void)hipGetLastError();
-    const int nunits = (a.ntasks + 1) / 2;
+    const int tpw = 64 / G;                                  // tasks per wave
+    const int nunits = (a.ntasks + tpw - 1) / tpw;
     int wgs = (nunits + kCbThreads / 64 - 1) / (kCbThreads / 64);
     wgs = wgs < cus ? wgs : cus;
-    hipLaunchKernelGGL(spmm_task_cb_kernel<8>, dim3(wgs, F / 128), dim3(kCbThreads), lds, s, a,
-                       nunits);
+    const dim3 grid(wgs, F / (4 * G));
+    if (G == 32)
+      hipLaunchKernelGGL((spmm_task_cb_kernel<32, 8>), grid, dim3(kCbThreads), lds, s, a, nunits);
+    else if (G == 16)
+      hipLaunchKernelGGL((spmm_task_cb_kernel<16, 8>), grid, dim3(kCbThreads), lds, s, a, nunits);
+    else
+      hipLaunchKernelGGL((spmm_task_cb_kernel<8, 8>), grid, dim3(kCbThreads), lds, s, a, nunits);
   }
   task_fixup<false>(a, s);
   return check_launch("spmm_task_cb");

@@ -428,9 +428,6 @@ def spmm(rowptr, col, val, n_rows, nnz, X, F, X2=None, B=None, out=None, plan=No
     raise TypeError(f"spmm: plan must be a TaskPlan (CSR.plan), got {type(plan)}")
 
 
-CB_MAX_M = 300      # the codebook-source SpMM's LDS image: (M + 1) x 512 B
-
-
 def codebook_source_ok(X, F, M, D, out=None, codes=None, n_rows=None, n_branches=None):
     """Whether spmm_codebook serves this layer shape (include/vqgnn.h §6b):
     the kernel's own checks (vqgnn_spmm_task_cb_supported) plus the host-side
