@@ -712,6 +712,8 @@ struct AssignGeom {
   bool filter;        // vq_filter_kernel (W <= 8) instead of vq_assign_kernel
   size_t lds;         // dynamic LDS of the filter kernel's launch
   int elds;           // filter: f32 codebook copy in LDS for the resolve
+  bool co;            // filter, several chunks: chunk-outer passes (each chunk staged
+                      // once per workgroup; per-row state between passes in the workspace)
 };
 
 template <int KC>
@@ -810,7 +812,7 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
                  const int64_t* __restrict__ batch_idx, int* __restrict__ idx32,
                  unsigned long long* __restrict__ partial, int* __restrict__ flags,
                  int rows_per_part, int chunk, int shift_f, int shift_g, int m_sweep, int elds,
-                 BnFold fold);
+                 BnFold fold, unsigned long long* __restrict__ co_state);
 
 // the filter's row-load mode: 2 -> W = 8 = 2D, D = 4; 1 -> W = D = 4 (float4
 // rows, aligned); 0 -> general
@@ -907,6 +909,9 @@ static AssignGeom assign_geom(int B, int nb, int M, int W) {
     int c = g.mpad;
     if (!g.fused)
       while (c > 32 && flt_lds_bytes(c) > kLdsBudget) c = (c / 2 + 31) / 32 * 32;
+    // measurement knob: a smaller staged chunk of the filter (multiple of 32)
+    const int fenv = env_int_vq("VQGNN_FLT_CHUNK", 0);
+    if (!g.fused && fenv >= 32 && fenv < c) c = fenv / 32 * 32;
     g.chunk = c;
   } else if (cb_lds_bytes(g.kc, g.mpad) + acc <= kLdsBudget) {
     // fused EMA when codebook + accumulators share the LDS
@@ -955,6 +960,9 @@ static AssignGeom assign_geom(int B, int nb, int M, int W) {
       g.lds += ef;
     }
   }
+  // several chunks: chunk-outer passes unless VQGNN_ASG_CO=0 (chunk-inner:
+  // every chunk restaged for every 1,024-row iteration)
+  g.co = g.filter && g.chunk < M && env_int_vq("VQGNN_ASG_CO", 1) != 0;
   // rows per workgroup iteration: the filter's lanes own one row each
   const int rows_per_iter = g.filter ? g.wv * 64 : g.wv * 16 * kAsgGroups;
   const int row_blocks = (B + rows_per_iter - 1) / rows_per_iter;
@@ -1514,7 +1522,7 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
                  const int64_t* __restrict__ batch_idx, int* __restrict__ idx32,
                  unsigned long long* __restrict__ partial, int* __restrict__ flags,
                  int rows_per_part, int chunk, int shift_f, int shift_g, int m_sweep, int elds,
-                 BnFold fold) {
+                 BnFold fold, unsigned long long* __restrict__ co_state) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int NT = WV * 64;
   const int W = WM == 2 ? 8 : (WM == 1 ? 4 : W_);          // compile-time in the row modes
@@ -1678,6 +1686,23 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
   // its node id for the code scatter too (a dependent load right before the
   // store would stall the wave on a memory round trip every iteration)
   int64_t nid = 0;
+  // chunk-outer (several chunks, co_state given): pass c stages chunk c once
+  // and runs every row against it, carrying each row's best exact distance,
+  // index and near-tie flag to the next pass in co_state; only the last pass
+  // writes the outputs.  Chunk-inner (one pass): every row iteration walks
+  // all chunks, restaging each.  Same comparisons in the same chunk order:
+  // the same indices.
+  // (a fused launch holds its whole codebook in one chunk: never chunk-outer,
+  // and its registers stay those of the one-pass loop)
+  const bool co = !FUSED && co_state != nullptr && nchunks > 1;
+  const int npass = co ? nchunks : 1;
+  for (int pass = 0; pass < npass; ++pass) {
+  if (co) {
+    __syncthreads();
+    stage_filter<NT>(E, ldw, W, pass * chunk, min(chunk, M - pass * chunk), chunk, lds, tid,
+                     &s_bigmin, ef);
+    __syncthreads();
+  }
   if (n_iters > 0) {
     const int r0 = min(part_begin + wave * 64 + lane, part_end - 1);
     load_raw(r0, raw);
@@ -1735,11 +1760,17 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
     float best = INFINITY;
     int bidx = 0;
     bool ntie = !(sx < 65536.f);
+    if (co && pass > 0 && live) {                     // the earlier chunks' result
+      const unsigned long long st = co_state[(int64_t)b * B + row0 + lane];
+      best = __uint_as_float((uint32_t)(st >> 32));
+      bidx = (int)((uint32_t)st & 0x7fffffffu);
+      ntie = ((uint32_t)st >> 31) != 0;
+    }
 
-    for (int ch = 0; ch < nchunks; ++ch) {
+    for (int ch = co ? pass : 0; ch < (co ? pass + 1 : nchunks); ++ch) {
       const int mc0 = ch * chunk;
       const int mcount = min(chunk, M - mc0);
-      if (nchunks > 1) {
+      if (nchunks > 1 && !co) {
         __syncthreads();
         stage_filter<NT>(E, ldw, W, mc0, mcount, chunk, lds, tid, &s_bigmin, ef);
         __syncthreads();
@@ -2007,6 +2038,13 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
       }
       ntie = ntie || (!exact_ok && m_sweep >= mcount);
     }
+    if (co && pass + 1 < npass) {                     // not the last chunk: carry the state
+      if (live)
+        co_state[(int64_t)b * B + row0 + lane] =
+            ((unsigned long long)__float_as_uint(best) << 32) | ((uint32_t)ntie << 31) |
+            (uint32_t)bidx;
+      continue;
+    }
 
     // ---- outputs (owner lane); a near-tie row is appended to the
     // workgroup's list instead (resolved after the row loop)
@@ -2033,6 +2071,7 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
       }
     }
   }
+  }   // pass
 
   // ---- near-tie rows of this workgroup: one wave per row sweeps every
   // codeword in vq.py's arithmetic (BatchNorm apply, |x|^2 and |e|^2 summed
@@ -2692,10 +2731,16 @@ static size_t flag_bytes(const AssignGeom& g, int nb) {
   return align_up((size_t)g.parts * nb * g.rows_per_part * sizeof(int), 256);
 }
 
+// chunk-outer passes: one packed state word per (branch, row) -- the best
+// exact distance so far (high 32 bits), the near-tie flag (bit 31), its index
+static size_t co_bytes(const AssignGeom& g, int B, int nb) {
+  return g.co ? align_up((size_t)nb * B * sizeof(unsigned long long), 256) : 0;
+}
+
 extern "C" size_t vqgnn_vq_assign_workspace(int32_t B, int32_t nb, int32_t M, int32_t W) {
   if (B <= 0 || nb <= 0 || M <= 0 || W <= 0) return 0;
   const AssignGeom g = assign_geom(B, nb, M, W);
-  return idx32_bytes(g, B, nb) + flag_bytes(g, nb);
+  return idx32_bytes(g, B, nb) + flag_bytes(g, nb) + co_bytes(g, B, nb);
 }
 
 // Measurement facility for bench.py: while enabled, every vq_assign_kernel
@@ -2840,6 +2885,10 @@ static int launch_filter(const float* X, int64_t ldx, const float* G, int64_t ld
   const BnFold fold = bn_fold ? *bn_fold : BnFold{};
   int* idx32 = (want_ema && !g.fused) ? reinterpret_cast<int*>(workspace) : nullptr;
   int* flags = reinterpret_cast<int*>(reinterpret_cast<char*>(workspace) + idx32_bytes(g, B, nb));
+  unsigned long long* co_state =
+      g.co ? reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(workspace) +
+                                                   idx32_bytes(g, B, nb) + flag_bytes(g, nb))
+           : nullptr;
   // the geometry sized the slab in when the EMA statistics fuse; without
   // them the kernel does not touch it (the same LDS is reserved)
   size_t lds = g.lds;
@@ -2865,7 +2914,7 @@ static int launch_filter(const float* X, int64_t ldx, const float* G, int64_t ld
                           (uint32_t)lds, s, ev0, ev1, 0, X, ldx, G, ldg, B, nb, D, M, W,       \
                           coef, grad_scale, emb, ldw, emb_bstride, idx_out, codes, ldc,        \
                           batch_idx, idx32, parts, flags, g.rows_per_part, g.chunk, sh.f,      \
-                          sh.g, m_sweep, g.elds, fold);                                        \
+                          sh.g, m_sweep, g.elds, fold, co_state);                              \
   } while (0)
 #define FLT_LAUNCH_WV(FU, WMV)                                                                \
   do {                                                                                        \
