@@ -1,8 +1,9 @@
 #!/bin/bash
-# Round 5: pipelined sweep, chunk-outer passes, narrow codebook tiles.  Parity
-# tests (SpMM, VQ goldens incl. M = 4,096, configs incl. ppi), the assign A/B
-# against ab_base.so and across chunk settings at ppi, and the reddit
-# layer-2 step with the codebook source (M = 1,024) against gathered rows.
+# Round 5: chunk-outer passes, narrow codebook tiles.  Parity tests (SpMM,
+# VQ goldens incl. M = 4,096 and the repeat-launch guard, configs incl. ppi),
+# the assign A/B against ab_base.so (round-4 build), chunk settings at ppi,
+# and the reddit layer-2 step with the codebook source (M = 1,024) against
+# gathered rows.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 O=gpurun_out/r05e

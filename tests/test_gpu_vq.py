@@ -63,6 +63,32 @@ def test_assign_bit_exact_given_coefficients(M, D, W, B, tie):
     assert ((st[:, 1:] - dw).abs() <= tol + 1e-7).all()
 
 
+@pytest.mark.parametrize("M,B", [(1024, 2100), (1030, 2100), (4096, 1500)])
+def test_assign_repeat_launches_identical(M, B):
+    """The same assign launched 12 times gives the oracle's indices every
+    time.  Guards the sweep's MFMA/VALU schedule: a software-pipelined sweep
+    (round 5, removed) picked a near-best codeword for a few rows of some
+    launches and not others ("Pipelined sweep")."""
+    D, W = 4, 8
+    g = torch.Generator().manual_seed(M * 7 + B)
+    X = torch.randn(B, D, generator=g) * 2 + 0.5
+    G = torch.randn(B, D, generator=g) * 1e-3
+    emb = torch.randn(M, 2 * D, generator=g)
+    af, bf = vq_ref.bn_coefficients(X, True, torch.zeros(D), torch.ones(D), 1e-5)
+    ag, bg = vq_ref.bn_coefficients(G, True, torch.zeros(D), torch.ones(D), 1e-24)
+    idx_ref, _ = vq_ref.assign_with_coef(X, G, af, bf, ag, bg, 0.75, emb)
+    coef = _coef_tensor(af, bf, ag, bg)
+    Xd, Gd, Ed = X.to(DEV), G.to(DEV), emb.view(1, M, 2 * D).to(DEV)
+    bad = []
+    for rep in range(12):
+        idx = torch.empty(1, B, dtype=torch.long, device=DEV)
+        kernels.vq_assign(Xd, Gd, coef, 0.75, Ed, D, W, idx_out=idx)
+        n = int((idx.cpu()[0] != idx_ref).sum())
+        if n:
+            bad.append((rep, n))
+    assert not bad, f"(launch, mismatching rows): {bad}"
+
+
 @pytest.mark.parametrize("M,W", [(256, 8), (256, 4), (1024, 8), (4096, 8), (40, 8)])
 def test_assign_near_ties_resolved_exactly(M, W):
     """The filtered sweep (f16-split scores on the MFMA) sends rows whose

@@ -788,10 +788,6 @@ vq_assign_kernel(const float* __restrict__ X, int64_t ldx,
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
 constexpr int kFltSlack = 32;          // one tile pair of prefetch past a chunk
-#ifndef VQGNN_PIPE_SWEEP
-#define VQGNN_PIPE_SWEEP 1
-#endif
-constexpr bool kPipeSweep = VQGNN_PIPE_SWEEP;   // software-pipelined sweep (row modes)
 constexpr int kFltBytesPerCode = 52;   // 3 f16 planes of 16 B + |e|^2 (f32)
 
 static size_t flt_lds_bytes(int chunk) {
@@ -1791,67 +1787,8 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
       const uint32_t pmask = npair > 1 ? (2u << (31 - __builtin_clz((uint32_t)npair - 1))) - 1 : 0u;
       const floatx4 zero = {0.f, 0.f, 0.f, 0.f};
       auto ld_a = [&](int off) { return *reinterpret_cast<const half8*>(ap + off); };
-      // Software-pipelined sweep (row modes, round 5): a pair's two tiles are
-      // issued one after the other, and each tile's four MFMAs are
-      // interleaved with the fold of the tile before them -- tile 0 of pair
-      // p with the completion of pair p - 1 (its tile 1 against the partial
-      // minimum of its tile 0, then the pair-index bits and the statistics),
-      // tile 1 with the partial minimum of tile 0 -- so the wave's VALU runs
-      // while its own MFMAs execute, with the same accumulators (T0, T1) and
-      // the same statistics as the unpipelined fold.  At p = 0 the "previous
-      // pair" is the all-ones state below, whose fold is a no-op.
-      floatx4 T0[4], T1[4];
-      uint32_t mmp[4];
-      // ~pmask in a VGPR: the pair tag (mm & ~pmask) | p is then one
-      // v_and_or_b32 with p its only scalar operand, and stays a plain VALU
-      // instruction for the schedule below (inline asm would not count)
-      uint32_t npm_v;
-      asm volatile("v_mov_b32 %0, %1" : "=v"(npm_v) : "s"(~pmask));
-      if constexpr (WM != 0) {
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const float ones = __uint_as_float(0xffffffffu);
-          T1[g] = floatx4{ones, ones, ones, ones};
-          mmp[g] = 0xffffffffu;
-        }
-      }
-      auto fold_pair = [&](int g, uint32_t pq) {   // complete a pair: T1[g] against mmp[g]
-        uint32_t mm = min(min(mmp[g], __float_as_uint(T1[g][0])), __float_as_uint(T1[g][1]));
-        mm = min(min(mm, __float_as_uint(T1[g][2])), __float_as_uint(T1[g][3]));
-        const uint32_t mt = (mm & npm_v) | pq;       // one v_and_or_b32 (one SGPR operand)
-        s2[g] = umed3(mt, cb[g], s2[g]);              // min(s2, max(mt, cb)): cb <= s2
-        cb[g] = min(mt, cb[g]);                       // equal scores: the earliest pair
-      };
-      int plast = 0;
-      auto sweep_pipe = [&](const half8 a0, const half8 a1, int p) {
-        // tile 0 of pair p, beside the completion of pair p - 1
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          T0[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, bop[g], zero, 0, 0, 0);
-          fold_pair(g, (uint32_t)(p - 1));
-        }
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);
-        }
-        // tile 1 of pair p, beside tile 0's partial minimum
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          T1[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, bop[g], zero, 0, 0, 0);
-          mmp[g] = min(min(__float_as_uint(T0[g][0]), __float_as_uint(T0[g][1])),
-                       min(__float_as_uint(T0[g][2]), __float_as_uint(T0[g][3])));
-        }
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
-        }
-        plast = p;
-      };
       auto sweep_pair = [&](const half8 a0, const half8 a1, int p) {
         if constexpr (WM != 0) {
-          if (kPipeSweep) return sweep_pipe(a0, a1, p);
           // both tiles' eight MFMAs issue back to back into their own
           // accumulators, then the VALU folds them (sched_group_barrier:
           // without it the compiler reads each MFMA's result right after it,
@@ -1926,12 +1863,6 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
       } else {
         for (int p = 0; p * 32 < mlim; ++p, ap += 512) sweep_pair(ld_a(0), ld_a(256), p);
       }
-      if constexpr (WM != 0) {
-        if (kPipeSweep && mlim > 0) {             // complete the last pair
-#pragma unroll
-          for (int g = 0; g < 4; ++g) fold_pair(g, (uint32_t)plast);
-        }
-      }
       // ---- hand the owner lane the four quads' statistics of its row: a
       // 4 x 4 transpose over (quad, group); keys carry their quad (index order
       // = pair, then quad)
@@ -1990,10 +1921,13 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
           }
           const float4 s4 = *reinterpret_cast<const float4*>(sef + p0);
           const float sv[4] = {s4.x, s4.y, s4.z, s4.w};
+          float dq[4];
+#pragma unroll
+          for (int c = 0; c < 4; ++c) dq[c] = fmaf(-2.f, d4[c], __fadd_rn(sx, sv[c]));
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
             const int ci = m0 + c;
-            const float dd = ci < mcount ? fmaf(-2.f, d4[c], __fadd_rn(sx, sv[c])) : INFINITY;
+            const float dd = ci < mcount ? dq[c] : INFINITY;
             if (dd < dm) {
               dm = dd;
               im = ci;
