@@ -170,7 +170,8 @@ def main():
     spmm_plan = adj.plan(F, B=B)
     use_cb = (gat is None and not args.gather_rows and
               hasattr(kernels.lib(), "vqgnn_spmm_task_cb") and   # (older A/B builds lack it)
-              kernels.codebook_source_ok(Xd, F, M, D, codes=codes, n_rows=n, n_branches=nb))
+              kernels.codebook_source_ok(Xd, F, M, D, codes=codes, n_rows=n, n_branches=nb)
+              and kernels.codebook_source_preferred(M))
     if use_cb:   # per batch as well: the records with out-of-batch columns -> nodes
         spmm_plan = adj.plan_codebook(B, subset, N_graph)
     plan_ms = time_plan(adj, n, nnz, cb=(B, subset, N_graph) if use_cb else None)

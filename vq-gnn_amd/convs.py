@@ -219,7 +219,9 @@ class OurGCNConv(nn.Module):
     def forward(self, x, edge_index, edge_weight=None, _hook=None):
         adj = as_csr(edge_index)
         if isinstance(x, CodebookInput):
-            if x.supported(adj.size(0)):
+            # narrower tiles than the full-width walk lose to the gather
+            # (kernels.codebook_source_preferred)
+            if x.supported(adj.size(0)) and kernels.codebook_source_preferred(x.emb_out.shape[1]):
                 anchor = None
                 if _hook is not None and not x.x.requires_grad:
                     anchor = torch.zeros((), device=x.x.device, requires_grad=True)

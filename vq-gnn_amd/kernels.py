@@ -449,6 +449,15 @@ def codebook_source_ok(X, F, M, D, out=None, codes=None, n_rows=None, n_branches
                                                    int(D)))
 
 
+def codebook_source_preferred(M):
+    """Whether the codebook source is the faster aggregation for a codebook of
+    M codewords: only where its LDS image fits the full-width walk (32 lanes
+    per task, 128-column tiles: M <= 320).  At M = 1,024 the 32-column tiles
+    walk every edge four times: 129 us against 103 us for gather + two-source
+    SpMM on the arxiv GAT batch (profiles/r05_cb_m1024_probe.txt)."""
+    return int(lib().vqgnn_spmm_task_cb_lds(int(M))) == int(M) * 16 * 32
+
+
 def spmm_codebook(rowptr, n_rows, nnz, X, F, B, codes, emb_out, D, plan_cb, out=None):
     """out = A @ [X[:B] ; x_first_order] with x_first_order's rows (the
     codeword feature halves of each out-of-batch node's codes, models.py:
