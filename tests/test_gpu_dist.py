@@ -90,9 +90,9 @@ def test_two_ranks_match_union_batch(tmp_path):
     # the fixed-point bound (finite state) and the replicas agree
     for tag in ("over500", "over700"):
         assert int(r0[f"{tag}_raised"]) == 1 and int(r1[f"{tag}_raised"]) == 1, tag
-        # (codes are not compared: the over-capacity rank's rows past the
-        # capacity are scattered into its own replica only, vq.py)
-        for k in ("emb", "emb_out", "ema_w", "cs"):
+        # codes too: rows past the capacity are scattered nowhere, so the
+        # replicas keep identical c_indices (vq.py _exchange_codes)
+        for k in ("emb", "emb_out", "ema_w", "cs", "codes"):
             np.testing.assert_array_equal(r0[f"{tag}_{k}"], r1[f"{tag}_{k}"], err_msg=tag + k)
         for k in ("emb_out", "ema_w", "cs"):
             assert np.isfinite(r0[f"{tag}_{k}"]).all(), tag + k

@@ -145,9 +145,10 @@ class VQBank(nn.Module):
         """Own codes now (scattered by the pack kernel), everyone's
         asynchronously (landed by sync_codes).  Rows past max_B (a batch over
         the CodebookSync capacity, raised at the next check on every rank)
-        are scattered locally only, so the collective keeps its shape."""
+        are not scattered at all: every replica keeps those nodes' previous
+        codes, so the replicas stay identical even for a caller that catches
+        the error, and the collective keeps its shape."""
         if local.shape[0] > max_B:
-            kernels.scatter_codes(batch_idx[max_B:], local[max_B:], codes)
             batch_idx, local = batch_idx[:max_B], local[:max_B]
         self._pending_codes = self.comm.start_codes_exchange(batch_idx, local, codes,
                                                              max_B, self.M)
