@@ -548,21 +548,35 @@ spmm_task_kernel(TaskArgs a) {
 // 1,280: narrower tiles fit larger codebooks, each tile walking every edge.
 constexpr int kCbThreads = 1024;
 constexpr size_t kCbLdsMax = 160 * 1024;
+constexpr int kCbStage = (int)(kCbLdsMax / 16 / kCbThreads);   // image pieces per thread (10)
 
 template <int G, int U>
 __global__ void __launch_bounds__(kCbThreads) __attribute__((amdgpu_waves_per_eu(4)))
 spmm_task_cb_kernel(TaskArgs a, int nunits) {
   extern __shared__ __attribute__((aligned(16))) char cb_smem[];
   const int tile = blockIdx.y;
-  const int F4 = a.F >> 2;
-  for (int i = threadIdx.x; i < a.cb_M * G; i += kCbThreads) {
-    const int m = i / G, c4 = tile * G + (i % G);
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (c4 < F4) {
-      const int col = 4 * c4, b = col / a.cb_D, d = col % a.cb_D;
-      v = *reinterpret_cast<const float4*>(a.cbe + b * a.cb_bstride + (int64_t)m * a.cb_ldw + d);
-    }
-    *reinterpret_cast<float4*>(cb_smem + (size_t)i * 16) = v;
+  // every piece of this thread's share of the image in flight at once (at
+  // most kCbStage float4 per thread: M x G <= 10,240), then the LDS writes:
+  // a load-then-write loop waited one memory round trip per piece, eight of
+  // them at M = 256 before any wave could walk.  Loads past the image repeat
+  // its last piece.
+  // (the tile's columns lie inside F: cb_lanes needs F % 4G == 0)
+  const int npc = a.cb_M * G;
+  float4 v[kCbStage];
+#pragma unroll
+  for (int r = 0; r < kCbStage; ++r) {
+    const int i = min((int)threadIdx.x + r * kCbThreads, npc - 1);
+    const int m = i / G, col = 4 * (tile * G + (i % G));
+    const int b = col / a.cb_D, d = col % a.cb_D;
+    v[r] = *reinterpret_cast<const float4*>(a.cbe + b * a.cb_bstride + (int64_t)m * a.cb_ldw + d);
+  }
+  // (unconditional writes: a piece past the image rewrites the last one with
+  // its own value -- a branch here would let the compiler sink each load
+  // into it, one wait per piece again)
+#pragma unroll
+  for (int r = 0; r < kCbStage; ++r) {
+    const int i = min((int)threadIdx.x + r * kCbThreads, npc - 1);
+    *reinterpret_cast<float4*>(cb_smem + (size_t)i * 16) = v[r];
   }
   __syncthreads();
   const int wave = threadIdx.x >> 6;
