@@ -97,3 +97,13 @@ def test_codebook_reads_bounded_by_its_branch_count():
     assert h.vqgnn_spmm_task_cb_supported(100, 5_000_000, 128, 128, 128, 1000, 32, 32, 256,
                                           4) == 0          # X past the 2 GiB near range
     assert h.vqgnn_spmm_task_cb_supported(100, 50, 128, 40, 128, 1000, 16, 16, 256, 4) == 0
+
+
+def test_codebook_source_preferred_only_at_full_width():
+    """The host layer takes the codebook source only where the whole 128-column
+    tile's image fits (M <= 320); narrower tiles lose to the gather (DESIGN
+    4.2d, profiles/r05_cb_m1024_probe.txt)."""
+    from vq_gnn_amd import kernels
+    assert kernels.codebook_source_preferred(256) and kernels.codebook_source_preferred(320)
+    assert not kernels.codebook_source_preferred(321)
+    assert not kernels.codebook_source_preferred(1024)
