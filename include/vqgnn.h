@@ -334,7 +334,11 @@ int vqgnn_spmm_task(const int32_t* rowptr, int32_t n_rows, int32_t n_cols, int64
  *      vqgnn_spmm_task, which has a 64-bit path).
  *    vqgnn_spmm_task_cb_supported: 1 iff vqgnn_spmm_task_cb accepts this
  *      shape (the same checks, no launch), so a host falls back before the
- *      call instead of catching its error.                                   */
+ *      call instead of catching its error.
+ *    Speed: each column tile walks every edge once, so the narrow tiles (G <
+ *      32) are slower than gather + vqgnn_spmm_task on arxiv-like batches;
+ *      the package's host layer uses this entry only when
+ *      vqgnn_spmm_task_cb_lds(M) == M * 512 (the 128-column tile fits).      */
 int vqgnn_spmm_task_records_cb(int64_t* records, int64_t nnz, int32_t B, const int64_t* subset,
                                int32_t n_cols, int64_t n_nodes, vqgnn_stream_t stream);
 size_t vqgnn_spmm_task_cb_lds(int32_t M);
