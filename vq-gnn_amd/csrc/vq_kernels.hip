@@ -2681,6 +2681,11 @@ extern "C" size_t vqgnn_vq_assign_workspace(int32_t B, int32_t nb, int32_t M, in
 // launch is issued with hipExtLaunchKernelGGL and a start/stop event pair, so
 // its duration is the kernel's own (no gap before the launch, unlike events
 // recorded around it on the stream).  Library-owned events, one mutex.
+// The events skip the system-scope fence (hipEventDisableSystemFence): they
+// only time, and are read after the caller's full synchronisation; a fenced
+// event pair costs each step a cache write-back and invalidate before the
+// assign and again before the next kernel (≈ 11 µs of idle GPU per arxiv
+// step, profiles/r05r_event_fence_ab.txt).
 static std::mutex g_timing_mu;
 static bool g_timing_on = false;
 static std::vector<std::pair<hipEvent_t, hipEvent_t>> g_timing_ev;
@@ -2689,7 +2694,8 @@ static void timing_events(hipEvent_t* a, hipEvent_t* b) {
   *a = *b = nullptr;
   std::lock_guard<std::mutex> lk(g_timing_mu);
   if (!g_timing_on) return;
-  if (hipEventCreate(a) != hipSuccess || hipEventCreate(b) != hipSuccess) {
+  if (hipEventCreateWithFlags(a, hipEventDisableSystemFence) != hipSuccess ||
+      hipEventCreateWithFlags(b, hipEventDisableSystemFence) != hipSuccess) {
     (void)hipGetLastError();
     *a = *b = nullptr;
     return;
