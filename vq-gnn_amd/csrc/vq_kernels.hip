@@ -798,7 +798,7 @@ static size_t flt_lds_bytes(int chunk) {
 // and the fused slab): [16 rows][12 dwords], one row group at a time
 
 // filtered assignment for W <= 8 (section 3b)
-template <bool FUSED, int WM, int WV>
+template <bool FUSED, int WM, int WV, bool CO>
 __global__ void __launch_bounds__(WV * 64)
 vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restrict__ Gr,
                  int64_t ldg, int B, int nb, int D, int M, int W,
@@ -808,7 +808,7 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
                  const int64_t* __restrict__ batch_idx, int* __restrict__ idx32,
                  unsigned long long* __restrict__ partial, int* __restrict__ flags,
                  int rows_per_part, int chunk, int shift_f, int shift_g, int m_sweep, int elds,
-                 BnFold fold, unsigned long long* __restrict__ co_state);
+                 BnFold fold, unsigned long long* __restrict__ co_state, int co_pass);
 
 // the filter's row-load mode: 2 -> W = 8 = 2D, D = 4; 1 -> W = D = 4 (float4
 // rows, aligned); 0 -> general
@@ -821,16 +821,19 @@ static int flt_mode(int W, int D, int64_t ldx, int64_t ldg, const void* X, const
 }
 
 template <int WV>
-static const void* flt_fn_wv(bool fused, int wm) {
-  if (fused) return wm == 1 ? (const void*)vq_filter_kernel<true, 1, WV>
-                  : wm == 2 ? (const void*)vq_filter_kernel<true, 2, WV>
-                            : (const void*)vq_filter_kernel<true, 0, WV>;
-  return wm == 1 ? (const void*)vq_filter_kernel<false, 1, WV>
-       : wm == 2 ? (const void*)vq_filter_kernel<false, 2, WV>
-                 : (const void*)vq_filter_kernel<false, 0, WV>;
+static const void* flt_fn_wv(bool fused, int wm, bool co) {
+  if (fused) return wm == 1 ? (const void*)vq_filter_kernel<true, 1, WV, false>
+                  : wm == 2 ? (const void*)vq_filter_kernel<true, 2, WV, false>
+                            : (const void*)vq_filter_kernel<true, 0, WV, false>;
+  if (co) return wm == 1 ? (const void*)vq_filter_kernel<false, 1, WV, true>
+                 : wm == 2 ? (const void*)vq_filter_kernel<false, 2, WV, true>
+                           : (const void*)vq_filter_kernel<false, 0, WV, true>;
+  return wm == 1 ? (const void*)vq_filter_kernel<false, 1, WV, false>
+       : wm == 2 ? (const void*)vq_filter_kernel<false, 2, WV, false>
+                 : (const void*)vq_filter_kernel<false, 0, WV, false>;
 }
-static const void* flt_fn(bool fused, int wm, int wv) {
-  return wv == 16 ? flt_fn_wv<16>(fused, wm) : flt_fn_wv<8>(fused, wm);
+static const void* flt_fn(bool fused, int wm, int wv, bool co) {
+  return wv == 16 ? flt_fn_wv<16>(fused, wm, co) : flt_fn_wv<8>(fused, wm, co);
 }
 
 // the filtered path serves W <= 8 (VQGNN_ASSIGN_EXACT=1: the exact f32 sweep
@@ -864,7 +867,8 @@ static const void* assign_fn(bool fused, int wm, int wv) {
 // Workgroups of the assign kernel the current device holds at once (register
 // and LDS limited), cached per configuration.  Without a device (host-only
 // queries) a static estimate is returned; the value only sizes the grid.
-static int assign_capacity(int kc, bool fused, int wm, size_t lds, int wv, bool flt) {
+static int assign_capacity(int kc, bool fused, int wm, size_t lds, int wv, bool flt,
+                           bool co = false) {
   const int fallback = 512 * 8 / wv;
   int dev = 0, cus = 0, per_cu = 0;
   if (hipGetDevice(&dev) != hipSuccess) {
@@ -873,11 +877,12 @@ static int assign_capacity(int kc, bool fused, int wm, size_t lds, int wv, bool 
   }
   static std::mutex mu;
   static std::map<std::tuple<int, int, bool, size_t>, int> cache;
-  const auto key = std::make_tuple(dev, ((flt ? 8 : 0) + kc) * 128 + wm * 32 + wv, fused, lds);
+  const auto key = std::make_tuple(dev, (((co ? 16 : 0) + (flt ? 8 : 0) + kc) * 128 + wm * 32 + wv),
+                                   fused, lds);
   std::lock_guard<std::mutex> lk(mu);
   auto it = cache.find(key);
   if (it != cache.end()) return it->second;
-  const void* fn = flt ? flt_fn(fused, wm, wv)
+  const void* fn = flt ? flt_fn(fused, wm, wv, co)
                  : kc == 1 ? assign_fn<1>(fused, wm, wv)
                  : kc == 2 ? assign_fn<2>(fused, wm, wv) : assign_fn<4>(fused, wm, wv);
   if (lds > 64 * 1024)
@@ -927,12 +932,16 @@ static AssignGeom assign_geom(int B, int nb, int M, int W) {
   if (g.fused) lds += acc;
   const size_t scr8 = 0;   // (the filter hands fragments over by permlane swaps: no scratch)
   const int wm = g.filter ? (W == 8 ? 2 : (W == 4 ? 1 : 0)) : (W == 4 * g.kc ? 2 : 0);
+  // several chunks: chunk-outer passes, one launch per chunk, unless
+  // VQGNN_ASG_CO=0 (chunk-inner: every chunk restaged for every 1,024-row
+  // iteration).  A fused launch holds its whole codebook in one chunk.
+  g.co = g.filter && !g.fused && g.chunk < M && env_int_vq("VQGNN_ASG_CO", 1) != 0;
   // waves per workgroup: the choice with more resident waves per CU (ties: 8).
   // (10-wave filter workgroups -- 20 resident waves at 5 per SIMD instead of
   // 16 -- measured 1.9x slower at arxiv update, 188 vs 98 us, and 1.4x at
   // feature_update: profiles/r04d_assign_waves_ab.txt)
-  const int cap8 = assign_capacity(g.kc, g.fused, wm, lds + scr8, 8, g.filter);
-  const int cap16 = assign_capacity(g.kc, g.fused, wm, lds + 2 * scr8, 16, g.filter);
+  const int cap8 = assign_capacity(g.kc, g.fused, wm, lds + scr8, 8, g.filter, g.co);
+  const int cap16 = assign_capacity(g.kc, g.fused, wm, lds + 2 * scr8, 16, g.filter, g.co);
   const int wenv = env_int_vq("VQGNN_ASG_WAVES", 0);
   g.wv = cap16 * 16 > cap8 * 8 ? 16 : 8;
   if (wenv == 8 || wenv == 16) g.wv = wenv;
@@ -951,14 +960,11 @@ static AssignGeom assign_geom(int B, int nb, int M, int W) {
     const int env = env_int_vq("VQGNN_FLT_ELDS", -1);
     if (g.lds + ef <= kLdsBudget && env != 0 &&
         (env == 1 || (g.chunk <= 512 &&
-                      assign_capacity(g.kc, g.fused, wmv, g.lds + ef, g.wv, true) >= cap))) {
+                      assign_capacity(g.kc, g.fused, wmv, g.lds + ef, g.wv, true, g.co) >= cap))) {
       g.elds = 1;
       g.lds += ef;
     }
   }
-  // several chunks: chunk-outer passes unless VQGNN_ASG_CO=0 (chunk-inner:
-  // every chunk restaged for every 1,024-row iteration)
-  g.co = g.filter && g.chunk < M && env_int_vq("VQGNN_ASG_CO", 1) != 0;
   // rows per workgroup iteration: the filter's lanes own one row each
   const int rows_per_iter = g.filter ? g.wv * 64 : g.wv * 16 * kAsgGroups;
   const int row_blocks = (B + rows_per_iter - 1) / rows_per_iter;
@@ -1508,7 +1514,7 @@ __device__ __forceinline__ void transpose_quads(uint32_t (&r)[4]) {
 // keeps, for each group g, the running minimum over its quad's codewords
 // 4q .. 4q+3 of every tile; a 4 x 4 transpose over the quads (permlane
 // swaps, VALU) hands the owner lane the four quads' minima of its row.
-template <bool FUSED, int WM, int WV>
+template <bool FUSED, int WM, int WV, bool CO>
 __global__ void __launch_bounds__(WV * 64)
 vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restrict__ Gr,
                  int64_t ldg, int B, int nb, int D_, int M, int W_,
@@ -1518,7 +1524,7 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
                  const int64_t* __restrict__ batch_idx, int* __restrict__ idx32,
                  unsigned long long* __restrict__ partial, int* __restrict__ flags,
                  int rows_per_part, int chunk, int shift_f, int shift_g, int m_sweep, int elds,
-                 BnFold fold, unsigned long long* __restrict__ co_state) {
+                 BnFold fold, unsigned long long* __restrict__ co_state, int co_pass) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int NT = WV * 64;
   const int W = WM == 2 ? 8 : (WM == 1 ? 4 : W_);          // compile-time in the row modes
@@ -1616,7 +1622,11 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
   }
   int* const flist = flags + (int64_t)wg * rows_per_part;
   __syncthreads();
-  if (nchunks == 1) stage_filter<NT>(E, ldw, W, 0, M, chunk, lds, tid, &s_bigmin, ef);
+  if (CO)                     // chunk-outer launch: this pass's chunk, once
+    stage_filter<NT>(E, ldw, W, co_pass * chunk, min(chunk, M - co_pass * chunk), chunk, lds,
+                     tid, &s_bigmin, ef);
+  else if (nchunks == 1)
+    stage_filter<NT>(E, ldw, W, 0, M, chunk, lds, tid, &s_bigmin, ef);
 
   const int part_begin = part * rows_per_part;
   const int part_end = min(B, part_begin + rows_per_part);
@@ -1625,7 +1635,7 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
   // A-fragment byte offset of this lane: plane (q: 0 -> hi, 1 -> lo, 2 -> hi,
   // 3 -> |e|^2 parts), codeword j of tile 0
   const uint32_t a_lane = (uint32_t)(((q == 1) ? 1 : (q == 3 ? 2 : 0)) * cs + j) * 16u;
-  if (nchunks == 1) __syncthreads();
+  if (CO || nchunks == 1) __syncthreads();
 
   // the owner lane's raw row (k-slot order: features, then gradients)
   auto load_raw = [&](int rowi, float (&raw)[8]) {
@@ -1682,23 +1692,15 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
   // its node id for the code scatter too (a dependent load right before the
   // store would stall the wave on a memory round trip every iteration)
   int64_t nid = 0;
-  // chunk-outer (several chunks, co_state given): pass c stages chunk c once
-  // and runs every row against it, carrying each row's best exact distance,
-  // index and near-tie flag to the next pass in co_state; only the last pass
-  // writes the outputs.  Chunk-inner (one pass): every row iteration walks
-  // all chunks, restaging each.  Same comparisons in the same chunk order:
-  // the same indices.
-  // (a fused launch holds its whole codebook in one chunk: never chunk-outer,
-  // and its registers stay those of the one-pass loop)
-  const bool co = !FUSED && co_state != nullptr && nchunks > 1;
-  const int npass = co ? nchunks : 1;
-  for (int pass = 0; pass < npass; ++pass) {
-  if (co) {
-    __syncthreads();
-    stage_filter<NT>(E, ldw, W, pass * chunk, min(chunk, M - pass * chunk), chunk, lds, tid,
-                     &s_bigmin, ef);
-    __syncthreads();
-  }
+  // chunk-outer (CO: one launch per chunk, pass co_pass): the launch stages
+  // its chunk once and runs every row against it, carrying each row's best
+  // exact distance, index and near-tie flag to the next launch in co_state;
+  // only the last pass writes the outputs.  Chunk-inner (nchunks > 1, not
+  // CO): every row iteration walks all chunks, restaging each.  Same
+  // comparisons in the same chunk order: the same indices.  (One launch per
+  // pass, not a pass loop: the loop kept 20 more VGPRs live across the row
+  // loop -- 139 instead of 119 at 8 waves, spills at 16.)
+  const bool co = CO && co_state != nullptr;
   if (n_iters > 0) {
     const int r0 = min(part_begin + wave * 64 + lane, part_end - 1);
     load_raw(r0, raw);
@@ -1756,17 +1758,17 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
     float best = INFINITY;
     int bidx = 0;
     bool ntie = !(sx < 65536.f);
-    if (co && pass > 0 && live) {                     // the earlier chunks' result
+    if (co && co_pass > 0 && live) {                  // the earlier chunks' result
       const unsigned long long st = co_state[(int64_t)b * B + row0 + lane];
       best = __uint_as_float((uint32_t)(st >> 32));
       bidx = (int)((uint32_t)st & 0x7fffffffu);
       ntie = ((uint32_t)st >> 31) != 0;
     }
 
-    for (int ch = co ? pass : 0; ch < (co ? pass + 1 : nchunks); ++ch) {
+    for (int ch = CO ? co_pass : 0; ch < (CO ? co_pass + 1 : nchunks); ++ch) {
       const int mc0 = ch * chunk;
       const int mcount = min(chunk, M - mc0);
-      if (nchunks > 1 && !co) {
+      if (nchunks > 1 && !CO) {
         __syncthreads();
         stage_filter<NT>(E, ldw, W, mc0, mcount, chunk, lds, tid, &s_bigmin, ef);
         __syncthreads();
@@ -1972,7 +1974,7 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
       }
       ntie = ntie || (!exact_ok && m_sweep >= mcount);
     }
-    if (co && pass + 1 < npass) {                     // not the last chunk: carry the state
+    if (co && co_pass + 1 < nchunks) {                // not the last chunk: carry the state
       if (live)
         co_state[(int64_t)b * B + row0 + lane] =
             ((unsigned long long)__float_as_uint(best) << 32) | ((uint32_t)ntie << 31) |
@@ -2005,7 +2007,6 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
       }
     }
   }
-  }   // pass
 
   // ---- near-tie rows of this workgroup: one wave per row sweeps every
   // codeword in vq.py's arithmetic (BatchNorm apply, |x|^2 and |e|^2 summed
@@ -2845,16 +2846,29 @@ static int launch_filter(const float* X, int64_t ldx, const float* G, int64_t ld
   const int m_sweep = msw_env >= 0 ? msw_env : (1 << 30);
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   timing_events(&ev0, &ev1);
-#define FLT_LAUNCH(FU, WMV, WVV)                                                              \
+  // chunk-outer: one launch per chunk (pass), the assign's timing events on
+  // the first and the last; the BatchNorm fold only in the first (it
+  // updates the running statistics and writes coef, which the later passes
+  // read like an unfolded launch)
+  const int npass = g.co ? (M + g.chunk - 1) / g.chunk : 1;
+#define FLT_LAUNCH_CO(FU, WMV, WVV, COV)                                                      \
   do {                                                                                        \
-    const void* fn = (const void*)vq_filter_kernel<FU, WMV, WVV>;                             \
+    const void* fn = (const void*)vq_filter_kernel<FU, WMV, WVV, COV>;                        \
     if (lds > 64 * 1024)                                                                      \
       (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);    \
-    hipExtLaunchKernelGGL((vq_filter_kernel<FU, WMV, WVV>), dim3(wgs), dim3(WVV * 64),          \
-                          (uint32_t)lds, s, ev0, ev1, 0, X, ldx, G, ldg, B, nb, D, M, W,       \
-                          coef, grad_scale, emb, ldw, emb_bstride, idx_out, codes, ldc,        \
-                          batch_idx, idx32, parts, flags, g.rows_per_part, g.chunk, sh.f,      \
-                          sh.g, m_sweep, g.elds, fold, co_state);                              \
+    for (int pass = 0; pass < npass; ++pass)                                                  \
+      hipExtLaunchKernelGGL((vq_filter_kernel<FU, WMV, WVV, COV>), dim3(wgs), dim3(WVV * 64),   \
+                            (uint32_t)lds, s, pass == 0 ? ev0 : nullptr,                      \
+                            pass + 1 == npass ? ev1 : nullptr, 0, X, ldx, G, ldg, B, nb, D,   \
+                            M, W, coef, grad_scale, emb, ldw, emb_bstride, idx_out, codes,    \
+                            ldc, batch_idx, idx32, parts, flags, g.rows_per_part, g.chunk,    \
+                            sh.f, sh.g, m_sweep, g.elds, pass == 0 ? fold : BnFold{},         \
+                            co_state, pass);                                                  \
+  } while (0)
+#define FLT_LAUNCH(FU, WMV, WVV)                                                              \
+  do {                                                                                        \
+    if (!FU && g.co) FLT_LAUNCH_CO(false, WMV, WVV, true);                                    \
+    else FLT_LAUNCH_CO(FU, WMV, WVV, false);                                                  \
   } while (0)
 #define FLT_LAUNCH_WV(FU, WMV)                                                                \
   do {                                                                                        \
@@ -2871,6 +2885,7 @@ static int launch_filter(const float* X, int64_t ldx, const float* G, int64_t ld
 #undef FLT_LAUNCH_WM
 #undef FLT_LAUNCH_WV
 #undef FLT_LAUNCH
+#undef FLT_LAUNCH_CO
   const int rc = check_launch("vq_filter");
   if (rc || !want_ema || fused) return rc;
   return launch_ema_tail(X, ldx, G, ldg, B, nb, D, M, W, coef, grad_scale, idx32, parts, g, sh, s);
