@@ -57,7 +57,7 @@ fcb.argtypes = ([ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_int32
                                   ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
                                   ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
                                   ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int32,
-                                  ctypes.c_int32, ctypes.c_void_p, ctypes.c_int64,
+                                  ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int64,
                                   ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32,
                                   ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
                                   ctypes.c_void_p])
@@ -76,7 +76,7 @@ def ref():
 
 def cb():
     rc = fcb(p(adj.rowptr), n, nnz, B, p(X), F, F, p(codes), nb, N,
-                              p(emb_out), emb_out.stride(1), emb_out.stride(0), M, D,
+                              p(emb_out), emb_out.stride(1), emb_out.stride(0), nb, M, D,
                               p(out_cb), F, p(plan.plan), p(rec_cb), plan.K, plan.n_jobs,
                               plan.n_empty, p(ws), stream)
     assert rc == 0, L.vqgnn_last_error()
