@@ -57,6 +57,10 @@ def parse():
     # codebook (kernels.spmm_codebook) where the shape allows
     # it; --gather-rows: materialise x_first_order and run the two-source SpMM
     p.add_argument("--gather-rows", action="store_true")
+    # one process, codebook source: the update's EMA finalize runs inside the
+    # aggregation's fix-up launch (vqgnn_spmm_task_cb_fin);
+    # --separate-finalize: its own launch after the aggregation
+    p.add_argument("--separate-finalize", action="store_true")
     return p.parse_args()
 
 
@@ -204,12 +208,20 @@ def main():
             e[4].record()
             ev.append(e)
 
+    fin_fused = [False]
+
     def aggregate(record, e):
         if use_cb:          # no x_first_order: the SpMM reads the codebook
             if record:
                 e[2].record()
+            # the pending EMA finalize inside the SpMM's fix-up launch (one
+            # process; multi-GPU it waits for its all-reduce: finish_update)
+            fin = None if args.separate_finalize else bank.take_fused_finalize()
+            fin_fused[0] = fin is not None
             kernels.spmm_codebook(adj.rowptr, n, nnz, Xd, F, B, codes, bank.emb_out, D,
-                                  spmm_plan)
+                                  spmm_plan, finalize=fin[0] if fin else None)
+            if fin:
+                fin[1]()
             if record:
                 e[3].record()
             return
@@ -304,7 +316,9 @@ def main():
     ms_step = dt / args.steps * 1e3
     value = total_edges * args.steps / dt
 
-    # VQ update = BN + assign (e0 -> e1) + the deferred finalize (e3 -> e4)
+    # VQ update = BN + assign (e0 -> e1) + the deferred finalize (e3 -> e4;
+    # with the finalize fused into the aggregation's fix-up launch it is
+    # inside the aggregation phase, e2 -> e3)
     vq_ms = float(np.mean([e[0].elapsed_time(e[1]) + e[3].elapsed_time(e[4]) for e in ev]))
     gather_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in ev]))
     spmm_ms = float(np.mean([e[2].elapsed_time(e[3]) for e in ev]))
@@ -394,6 +408,8 @@ def main():
                                     "codeword gather, " +
                                     ("GAT attention aggregation)" if gat is not None else "SpMM)")),
                         aggregation=("codebook_source" if use_cb else "gathered_rows"),
+                        ema_finalize=("in the aggregation's fix-up launch" if fin_fused[0]
+                                      else "own launch"),
                         B=B, B_prime=n - B, nnz=nnz, F=F, M=M, D=D, W=W,
                         parallelism=f"dp{world}", world=world,
                         backend=(args.backend if comm is not None else None),

@@ -236,6 +236,30 @@ int vqgnn_vq_ema_finalize(int64_t* ema_parts, int32_t nparts, int32_t zero_after
                           const float* rm_g, const float* rv_g,
                           int32_t* bad_init, vqgnn_stream_t stream);
 
+/* 4b. The operands of vqgnn_vq_ema_finalize as one record, for the
+ *     aggregation entry that runs the finalize inside its own fix-up launch
+ *     (vqgnn_spmm_task_cb_fin, §6b).  Same meaning, same checks.            */
+typedef struct vqgnn_ema_finalize_args {
+  int64_t* ema_parts;
+  int32_t nparts, zero_after;
+  int64_t stat_count;
+  int32_t nb, M, D, W, ldw;
+  float decay;
+  int32_t laplace;
+  float grad_scale, epsilon;
+  float* cluster_size;
+  int64_t cs_bstride;
+  float* ema_w;
+  float* embedding;
+  float* embedding_output;
+  int64_t emb_bstride;
+  const float* rm_f;
+  const float* rv_f;
+  const float* rm_g;
+  const float* rv_g;
+  int32_t* bad_init;
+} vqgnn_ema_finalize_args;
+
 /* ------------------------------------------------------------------------ *
  * 5. Out-of-batch codeword gather (models.py:158, :168-173): for j in [0, n-B)
  *    and b < nb, with node = subset[B+j] and code = codes[node][b]:
@@ -338,7 +362,19 @@ int vqgnn_spmm_task(const int32_t* rowptr, int32_t n_rows, int32_t n_cols, int64
  *    Speed: each column tile walks every edge once, so the narrow tiles (G <
  *      32) are slower than gather + vqgnn_spmm_task on arxiv-like batches;
  *      the package's host layer uses this entry only when
- *      vqgnn_spmm_task_cb_lds(M) == M * 512 (the 128-column tile fits).      */
+ *      vqgnn_spmm_task_cb_lds(M) == M * 512 (the 128-column tile fits).
+ *    vqgnn_spmm_task_cb_fin: vqgnn_spmm_task_cb, then the EMA finalize of
+ *      *fin (§4, the update whose statistics the walk's codebook predates:
+ *      models.py:181-185 runs it after the aggregation) inside the fix-up
+ *      launch -- its first fin->nb workgroups finalize the branches beside
+ *      the cut-row sums, one launch and one kernel boundary fewer than the
+ *      two calls.  The finalize overwrites embedding_output, which the walk
+ *      has read by then (same stream order as the two calls).  Same outputs
+ *      and state, bit for bit, as vqgnn_spmm_task_cb followed by
+ *      vqgnn_vq_ema_finalize; fin == NULL is vqgnn_spmm_task_cb.  For
+ *      M >= 1,024 (the finalize's two-kernel form) the finalize runs as its
+ *      own launches after the fix-up.  Single process: a multi-GPU update
+ *      finalizes after its statistics' all-reduce instead.                  */
 int vqgnn_spmm_task_records_cb(int64_t* records, int64_t nnz, int32_t B, const int64_t* subset,
                                int32_t n_cols, int64_t n_nodes, vqgnn_stream_t stream);
 size_t vqgnn_spmm_task_cb_lds(int32_t M);
@@ -351,6 +387,13 @@ int vqgnn_spmm_task_cb(const int32_t* rowptr, int32_t n_rows, int64_t nnz, int32
                        int32_t n_branches, int32_t M, int32_t D, float* out, int64_t ldo,
                        const int32_t* plan, const int64_t* records_cb, int32_t K, int32_t n_jobs,
                        int32_t n_empty, void* workspace, vqgnn_stream_t stream);
+int vqgnn_spmm_task_cb_fin(const int32_t* rowptr, int32_t n_rows, int64_t nnz, int32_t B,
+                           const float* X, int64_t ldx, int32_t F, const int16_t* codes,
+                           int64_t ldc, int64_t n_nodes, const float* codewords, int64_t ldw,
+                           int64_t bstride, int32_t n_branches, int32_t M, int32_t D, float* out,
+                           int64_t ldo, const int32_t* plan, const int64_t* records_cb, int32_t K,
+                           int32_t n_jobs, int32_t n_empty, void* workspace,
+                           const vqgnn_ema_finalize_args* fin, vqgnn_stream_t stream);
 
 /* 7. CSR transpose (structure + values) for the backward product
  *    dX = A^T dOut (torch_sparse matmul autograd, convs.py:95).  Output CSR of

@@ -46,3 +46,59 @@ def test_deferred_finalize_same_state(monkeypatch):
     assert torch.equal(a.emb_out, b.emb_out)
     a.check_bad_init()
     b.check_bad_init()
+
+
+@pytest.mark.parametrize("semantics,M", [("update", 256), ("feature_update", 256),
+                                         ("update", 1024)])
+def test_finalize_fused_into_codebook_spmm(monkeypatch, semantics, M):
+    """The deferred EMA finalize run inside the codebook-source SpMM's fix-up
+    launch (VQBank.take_fused_finalize + spmm_codebook(finalize=...),
+    vqgnn_spmm_task_cb_fin) leaves the SpMM output and every piece of VQ
+    state bit-identical to the SpMM followed by finish_update(), step after
+    step (the SpMM reads the pre-update codebook in both).  M = 1,024: the
+    finalize's two-kernel form, launched after the fix-up by the same entry."""
+    from vq_gnn_amd import graph, kernels
+    monkeypatch.setattr(vqmod, "STRICT_BAD_INIT", False)
+    cfg = dict(graph.CONFIGS["arxiv_gcn"])
+    g, _, bt = graph.make_batch(cfg)
+    F, D = 128, 4
+    nb = F // D
+    bidx, subset, adj = graph.batch_to_device(bt, DEV)
+    gen = torch.Generator(device="cpu").manual_seed(5)
+    X = torch.randn(bt.B, F, generator=gen).to(DEV)
+    G = (torch.randn(bt.B, F, generator=gen) * 1e-3).to(DEV)
+    a, b = _bank(nb, M, D), _bank(nb, M, D)
+    ca = torch.randint(0, M, (cfg["N"], nb), dtype=torch.int16, generator=gen).to(DEV)
+    cb = ca.clone()
+    pcb = adj.plan_codebook(bt.B, subset, cfg["N"])
+    supported = kernels.codebook_source_ok(X, F, M, D, codes=ca, n_rows=bt.n, n_branches=nb)
+    assert supported
+    for step in range(3):
+        for bank, codes, fused in ((a, ca, False), (b, cb, True)):
+            if semantics == "update":
+                bank.update(X, G, 0, nb, True, codes=codes, batch_idx=bidx, defer=True)
+            else:
+                bank.feature_update(X, 0, nb, True, codes=codes, batch_idx=bidx)
+            fin = bank.take_fused_finalize() if fused else None
+            if semantics == "update":
+                assert (fin is not None) == fused
+            else:                   # feature_update finalizes at once: nothing pending
+                assert fin is None
+            out = kernels.spmm_codebook(adj.rowptr, bt.n, bt.nnz, X, F, bt.B, codes,
+                                        bank.emb_out, D, pcb,
+                                        finalize=fin[0] if fin else None)
+            if fin:
+                fin[1]()
+            bank.finish_update()
+            if fused:
+                out_b = out
+            else:
+                out_a = out
+        assert torch.equal(out_a, out_b), step
+        for name in ("emb", "emb_out", "ema_w", "cs", "rm_f", "rv_f", "rm_g", "rv_g",
+                     "bad_flag", "stats_u", "stats_f"):
+            assert torch.equal(getattr(a, name), getattr(b, name)), (step, name)
+        assert torch.equal(ca, cb)
+        X = X * 1.01
+    a.check_bad_init()
+    b.check_bad_init()

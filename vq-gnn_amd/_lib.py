@@ -25,6 +25,23 @@ _f32 = ctypes.c_float
 _f64 = ctypes.c_double
 _size = ctypes.c_size_t
 
+
+
+class EmaFinalizeArgs(ctypes.Structure):
+    """include/vqgnn.h §4b vqgnn_ema_finalize_args (C layout and order)."""
+    _fields_ = [
+        ("ema_parts", _c_void_p), ("nparts", _i32), ("zero_after", _i32),
+        ("stat_count", _i64),
+        ("nb", _i32), ("M", _i32), ("D", _i32), ("W", _i32), ("ldw", _i32),
+        ("decay", _f32), ("laplace", _i32), ("grad_scale", _f32), ("epsilon", _f32),
+        ("cluster_size", _c_void_p), ("cs_bstride", _i64),
+        ("ema_w", _c_void_p), ("embedding", _c_void_p), ("embedding_output", _c_void_p),
+        ("emb_bstride", _i64),
+        ("rm_f", _c_void_p), ("rv_f", _c_void_p), ("rm_g", _c_void_p), ("rv_g", _c_void_p),
+        ("bad_init", _c_void_p),
+    ]
+
+
 # name -> (restype, argtypes); mirrors include/vqgnn.h one to one.
 SIGNATURES = {
     "vqgnn_last_error": (ctypes.c_char_p, []),
@@ -84,6 +101,11 @@ SIGNATURES = {
                                           _c_void_p, _i64, _i64, _c_void_p, _i64, _i64, _i32,
                                           _i32, _i32, _c_void_p, _i64, _c_void_p, _c_void_p,
                                           _i32, _i32, _i32, _c_void_p, _c_void_p]),
+    "vqgnn_spmm_task_cb_fin": (ctypes.c_int, [_c_void_p, _i32, _i64, _i32, _c_void_p, _i64, _i32,
+                                              _c_void_p, _i64, _i64, _c_void_p, _i64, _i64, _i32,
+                                              _i32, _i32, _c_void_p, _i64, _c_void_p, _c_void_p,
+                                              _i32, _i32, _i32, _c_void_p,
+                                              ctypes.POINTER(EmaFinalizeArgs), _c_void_p]),
     "vqgnn_gat_att_grad_workspace": (_size, [_i32, _i32, _i32]),
     "vqgnn_gat_att_grad": (ctypes.c_int, [_c_void_p, _i64, _c_void_p, _i64, _i32, _i32, _i32,
                                           _i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p,

@@ -29,7 +29,9 @@
 // separate multiply and add.
 
 #include "common.h"
+#include "ema_finalize.h"
 
+#include <mutex>
 #include <utility>
 
 namespace vqgnn {
@@ -602,14 +604,13 @@ static int cb_lanes(int F, int M) {
 // An empty row: zeros.  Rows at or past n_rows (a call over leading rows)
 // are skipped.
 template <bool GAT>
-__global__ void __launch_bounds__(256)
-spmm_task_fixup_kernel(TaskArgs a) {
+__device__ __forceinline__ void task_fixup_thread(const TaskArgs& a, int gtid) {
   // L lanes per job: 32 when a row (plus the GAT slot) fits 32 float4 pieces,
   // so a wave finishes two rows
   const int F4 = a.F >> 2;
   const int L = F4 <= 32 ? 32 : 64;          // (GAT's slot column F4 is skipped below)
-  const int lane = threadIdx.x & (L - 1);
-  const int w = (blockIdx.x * 256 + threadIdx.x) / L;
+  const int lane = gtid & (L - 1);
+  const int w = gtid / L;
   const int C4 = a.cf >> 2;                 // carry row stride in float4
   if (w < a.n_jobs) {
     const int r = a.jobs[3 * w], ts = a.jobs[3 * w + 1], t = a.jobs[3 * w + 2];
@@ -672,6 +673,27 @@ spmm_task_fixup_kernel(TaskArgs a) {
     float4* o = reinterpret_cast<float4*>(a.out + (int64_t)r * a.ldo);
     for (int c = lane; c < F4; c += L) o[c] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
+}
+
+template <bool GAT>
+__global__ void __launch_bounds__(256)
+spmm_task_fixup_kernel(TaskArgs a) {
+  task_fixup_thread<GAT>(a, blockIdx.x * 256 + threadIdx.x);
+}
+
+// The fix-up launch with the EMA finalize beside it (vqgnn_spmm_task_cb_fin):
+// workgroups [0, nb) finalize branch blockIdx.x (ema_finalize.h, the body of
+// vq_ema_finalize_kernel), the rest take the fix-up jobs.  Disjoint data: the
+// finalize touches the slabs and the codebook state, the fix-up the carries
+// and the output rows; the walk that read the codebook has finished.
+__global__ void __launch_bounds__(kFinThreads)
+spmm_fixup_fin_kernel(TaskArgs a, EmaFin f, int nb) {
+  extern __shared__ float fin_cs[];          // [M]
+  if ((int)blockIdx.x < nb) {
+    ema_finalize_branch(f, blockIdx.x, threadIdx.x, fin_cs);
+    return;
+  }
+  task_fixup_thread<false>(a, ((int)blockIdx.x - nb) * kFinThreads + threadIdx.x);
 }
 
 static int task_env(const char* name, int dflt) {
@@ -861,6 +883,19 @@ static void task_fixup(const TaskArgs& a, hipStream_t s) {
   }
 }
 
+static void task_fixup_fin(const TaskArgs& a, const EmaFin& f, int nb, hipStream_t s) {
+  const int nfix = a.n_jobs + a.n_empty;
+  const int L = a.F / 4 <= 32 ? 32 : 64;     // lanes per fix-up job (task_fixup_thread)
+  const int per = kFinThreads / L;
+  const size_t lds = (size_t)f.M * sizeof(float);
+  if (lds > 48 * 1024) {
+    static std::once_flag once;
+    std::call_once(once, [] { ema_fin_lds_attr((const void*)spmm_fixup_fin_kernel); });
+  }
+  hipLaunchKernelGGL(spmm_fixup_fin_kernel, dim3(nb + (nfix + per - 1) / per), dim3(kFinThreads),
+                     lds, s, a, f, nb);
+}
+
 template <bool GAT>
 static void task_launch(const TaskArgs& a, bool near, hipStream_t s) {
   if (a.nnz > 0) {
@@ -961,14 +996,19 @@ extern "C" int32_t vqgnn_spmm_task_cb_supported(int32_t n_rows, int32_t B, int64
   return cb_unsupported(n_rows, B, ldx, F, ldo, n_nodes, ldc, n_branches, M, D) ? 0 : 1;
 }
 
-extern "C" int vqgnn_spmm_task_cb(const int32_t* rowptr, int32_t n_rows, int64_t nnz, int32_t B,
-                                  const float* X, int64_t ldx, int32_t F, const int16_t* codes,
-                                  int64_t ldc, int64_t n_nodes, const float* codewords,
-                                  int64_t ldw, int64_t bstride, int32_t n_branches, int32_t M,
-                                  int32_t D, float* out, int64_t ldo, const int32_t* plan,
-                                  const int64_t* records_cb, int32_t K, int32_t n_jobs,
-                                  int32_t n_empty, void* workspace, vqgnn_stream_t stream) {
+static int spmm_task_cb_impl(const int32_t* rowptr, int32_t n_rows, int64_t nnz, int32_t B,
+                             const float* X, int64_t ldx, int32_t F, const int16_t* codes,
+                             int64_t ldc, int64_t n_nodes, const float* codewords, int64_t ldw,
+                             int64_t bstride, int32_t n_branches, int32_t M, int32_t D, float* out,
+                             int64_t ldo, const int32_t* plan, const int64_t* records_cb,
+                             int32_t K, int32_t n_jobs, int32_t n_empty, void* workspace,
+                             const vqgnn_ema_finalize_args* fin, vqgnn_stream_t stream) {
   clear_error();
+  EmaFin ef{};
+  if (fin) {                                // checked before anything is launched
+    const int frc = ema_fin_prepare(fin, &ef);
+    if (frc != VQGNN_OK) return frc;
+  }
   const char* why = cb_unsupported(n_rows, B, ldx, F, ldo, n_nodes, ldc, n_branches, M, D);
   VQGNN_REQUIRE(!why, "spmm_task_cb: %s (n_rows=%d B=%d F=%d D=%d M=%d branches=%d codes "
                 "[%lld x %lld])", why ? why : "", n_rows, B, F, D, M, n_branches,
@@ -1020,8 +1060,42 @@ extern "C" int vqgnn_spmm_task_cb(const int32_t* rowptr, int32_t n_rows, int64_t
     else
       hipLaunchKernelGGL((spmm_task_cb_kernel<8, 8>), grid, dim3(kCbThreads), lds, s, a, nunits);
   }
-  task_fixup<false>(a, s);
+  if (!fin) {
+    task_fixup<false>(a, s);
+  } else if (!ef.split) {
+    task_fixup_fin(a, ef, fin->nb, s);      // one launch: fix-up + finalize
+  } else {                                  // the finalize's two-kernel form
+    task_fixup<false>(a, s);
+    const int frc = ema_fin_run(ef, fin->nb, s);
+    if (frc != VQGNN_OK) return frc;
+  }
   return check_launch("spmm_task_cb");
+}
+
+extern "C" int vqgnn_spmm_task_cb(const int32_t* rowptr, int32_t n_rows, int64_t nnz, int32_t B,
+                                  const float* X, int64_t ldx, int32_t F, const int16_t* codes,
+                                  int64_t ldc, int64_t n_nodes, const float* codewords,
+                                  int64_t ldw, int64_t bstride, int32_t n_branches, int32_t M,
+                                  int32_t D, float* out, int64_t ldo, const int32_t* plan,
+                                  const int64_t* records_cb, int32_t K, int32_t n_jobs,
+                                  int32_t n_empty, void* workspace, vqgnn_stream_t stream) {
+  return spmm_task_cb_impl(rowptr, n_rows, nnz, B, X, ldx, F, codes, ldc, n_nodes, codewords, ldw,
+                           bstride, n_branches, M, D, out, ldo, plan, records_cb, K, n_jobs,
+                           n_empty, workspace, nullptr, stream);
+}
+
+extern "C" int vqgnn_spmm_task_cb_fin(const int32_t* rowptr, int32_t n_rows, int64_t nnz,
+                                      int32_t B, const float* X, int64_t ldx, int32_t F,
+                                      const int16_t* codes, int64_t ldc, int64_t n_nodes,
+                                      const float* codewords, int64_t ldw, int64_t bstride,
+                                      int32_t n_branches, int32_t M, int32_t D, float* out,
+                                      int64_t ldo, const int32_t* plan, const int64_t* records_cb,
+                                      int32_t K, int32_t n_jobs, int32_t n_empty,
+                                      void* workspace, const vqgnn_ema_finalize_args* fin,
+                                      vqgnn_stream_t stream) {
+  return spmm_task_cb_impl(rowptr, n_rows, nnz, B, X, ldx, F, codes, ldc, n_nodes, codewords, ldw,
+                           bstride, n_branches, M, D, out, ldo, plan, records_cb, K, n_jobs,
+                           n_empty, workspace, fin, stream);
 }
 
 extern "C" int vqgnn_gat_spmm_task(const int32_t* rowptr, int32_t n_rows, int32_t n_cols,

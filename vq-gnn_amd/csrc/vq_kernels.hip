@@ -13,6 +13,7 @@
 // The library is compiled with -ffp-contract=off; every fma is explicit.
 
 #include "common.h"
+#include "ema_finalize.h"
 
 #include <hip/hip_ext.h>
 
@@ -2231,114 +2232,12 @@ __global__ void vq_ema_reduce_kernel(const long long* __restrict__ parts, int np
 // ---------------------------------------------------------------------------
 // 4. EMA finalize: one workgroup per branch.        vq.py:177-200, :242-277
 // ---------------------------------------------------------------------------
-constexpr int kFinThreads = 1024;
-constexpr int kFinWaves = kFinThreads / 64;
-
-// One workgroup per branch; cs lives in LDS (dynamic, M floats) between the
-// phases, so the only global traffic is the slab, the state and the outputs.
+// (kFinThreads, EmaFin and the body: ema_finalize.h, shared with the
+// aggregation's fix-up launch, vqgnn_spmm_task_cb_fin)
 __global__ void __launch_bounds__(kFinThreads)
-vq_ema_finalize_kernel(long long* __restrict__ stats, int nparts, int64_t part_stride,
-                       int zero_after, int shift_f, int shift_g, int M, int D, int W, int ldw,
-                       float decay, int laplace, float grad_scale, float epsilon,
-                       float* __restrict__ cluster_size, int64_t cs_bstride,
-                       float* __restrict__ ema_w, float* __restrict__ emb,
-                       float* __restrict__ emb_out, int64_t emb_bstride,
-                       const float* __restrict__ rm_f, const float* __restrict__ rv_f,
-                       const float* __restrict__ rm_g, const float* __restrict__ rv_g,
-                       int* __restrict__ bad_init, int split) {
+vq_ema_finalize_kernel(EmaFin f) {
   extern __shared__ float cs_s[];            // [M]
-  __shared__ float wred[kFinWaves];
-  __shared__ int bad;
-  const int b = blockIdx.x;
-  const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
-  long long* st = stats + (int64_t)b * M * (W + 1);
-  // statistic = integer sum of the per-part fixed-point slabs, decoded once:
-  // round(exact sum * 2^-shift) to fp32 (count column: shift 0).  Every entry
-  // is read by exactly one thread; zero_after clears it behind the read so
-  // the slab is zero for the next vqgnn_vq_assign (ema_zeroed = 1).
-  auto stat = [&](int64_t i, int shift) {
-    long long v = st[i];
-    if (zero_after) st[i] = 0;
-    for (int p = 1; p < nparts; ++p) {
-      v += st[(int64_t)p * part_stride + i];
-      if (zero_after) st[(int64_t)p * part_stride + i] = 0;
-    }
-    return (float)ldexp((double)v, -shift);
-  };
-  float* cs = cluster_size + (int64_t)b * cs_bstride;
-  float* ew = ema_w + (int64_t)b * emb_bstride;
-  float* e = emb + (int64_t)b * emb_bstride;
-  float* eo = emb_out + (int64_t)b * emb_bstride;
-  const float one_m_decay = (float)(1.0 - (double)decay);  // python (1 - decay) -> float scalar
-  if (tid == 0) bad = 0;
-
-  // cs = cs*decay + (1-decay)*counts  (vq.py:177-178; fp32 tensor ops)
-#pragma unroll 4
-  for (int m = tid; m < M; m += kFinThreads)
-    cs_s[m] = __fadd_rn(__fmul_rn(cs[m], decay), __fmul_rn(one_m_decay, stat((int64_t)m * (W + 1), 0)));
-  __syncthreads();
-
-  if (laplace) {  // vq.py:182-186
-    // n = torch.sum(cs): per-thread sequential partials over a strided slice,
-    // a fixed butterfly per wave, then the waves in order — deterministic
-    // (ATen's CPU cascade order differs by ulps)
-    float sum = 0.f;
-    for (int m = tid; m < M; m += kFinThreads) sum = __fadd_rn(sum, cs_s[m]);
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) sum = __fadd_rn(sum, __shfl_xor(sum, off));
-    if (lane == 0) wred[wave] = sum;
-    __syncthreads();
-    float n = wred[0];
-#pragma unroll
-    for (int w = 1; w < kFinWaves; ++w) n = __fadd_rn(n, wred[w]);
-    const float den = __fadd_rn(n, (float)((double)M * 1e-5));  // n + M*1e-5 (python float -> f32)
-    for (int m = tid; m < M; m += kFinThreads)
-      cs_s[m] = __fmul_rn(__fdiv_rn(__fadd_rn(cs_s[m], 1e-5f), den), n);
-    __syncthreads();
-  }
-
-  for (int m = tid; m < M; m += kFinThreads) {
-    const float c = cs_s[m];
-    cs[m] = c;
-    if (c == 0.f) bad = 1;  // vq.py:188 count_nonzero(cs) != M
-  }
-  __syncthreads();
-  if (bad) {  // reference raises before touching ema_w / embedding
-    if (tid == 0) atomicOr(bad_init, 1);
-    if (zero_after)
-      for (int i = tid; i < M * W; i += kFinThreads)
-        for (int p = 0; p < nparts; ++p)
-          st[(int64_t)p * part_stride + (int64_t)(i / W) * (W + 1) + 1 + i % W] = 0;
-    return;
-  }
-  if (split) return;                         // vq_ema_apply_kernel takes the rest
-
-  // ema_w = ema_w*decay + (1-decay)*dw ; embedding = ema_w / cs ; output
-  // (unrolled: the loads of four elements per thread in flight together)
-  const int nw = M * W;
-#pragma unroll 4
-  for (int i = tid; i < nw; i += kFinThreads) {
-    const int m = i / W, k = i % W;
-    const int64_t o = (int64_t)m * ldw + k;
-    const float dw = stat((int64_t)m * (W + 1) + 1 + k, k < D ? shift_f : shift_g);
-    const float w = __fadd_rn(__fmul_rn(ew[o], decay), __fmul_rn(one_m_decay, dw));
-    ew[o] = w;
-    const float ev = __fdiv_rn(w, cs_s[m]);
-    e[o] = ev;
-    float out;
-    if (k < D) {  // vq.py:198-200 / :267-272 feature half: emb*sqrt(rv+1e-5)+rm
-      const float sd = sqrtf(__fadd_rn(rv_f[b * D + k], 1e-5f));
-      out = __fadd_rn(__fmul_rn(ev, sd), rm_f[b * D + k]);
-    } else {      // vq.py:263 /= (scale + eps); :267 sqrt(rv_g + eps)
-      const int kg = k - D;
-      const float div = (float)((double)grad_scale + (double)epsilon);
-      const float sd = sqrtf(__fadd_rn(rv_g[b * D + kg], epsilon));
-      out = __fadd_rn(__fmul_rn(__fdiv_rn(ev, div), sd), rm_g[b * D + kg]);
-      if (grad_scale == 0.f) out = __fmul_rn(out, 0.f);  // vq.py:274-275
-    }
-    eo[o] = out;
-  }
+  ema_finalize_branch(f, blockIdx.x, threadIdx.x, cs_s);
 }
 
 // Large codebooks (M >= 1024): the per-codeword half of the finalize spread
@@ -3046,6 +2945,77 @@ extern "C" int vqgnn_vq_ema_reduce(const int64_t* parts, int32_t nparts, int64_t
   return check_launch("ema_reduce");
 }
 
+namespace vqgnn {
+
+int ema_fin_prepare(const vqgnn_ema_finalize_args* a, EmaFin* f) {
+  VQGNN_REQUIRE(a, "ema_finalize: null arguments");
+  VQGNN_REQUIRE(a->ema_parts && a->cluster_size && a->ema_w && a->embedding &&
+                    a->embedding_output && a->bad_init,
+                "ema_finalize: null pointer");
+  VQGNN_REQUIRE(a->rm_f && a->rv_f, "ema_finalize: feature running stats required");
+  VQGNN_REQUIRE(a->W == a->D || (a->W == 2 * a->D && a->rm_g && a->rv_g),
+                "ema_finalize: W must be D or 2D");
+  VQGNN_REQUIRE(a->nb > 0 && a->M > 0 && a->ldw >= a->W && a->nparts > 0,
+                "ema_finalize: bad shape");
+  VQGNN_REQUIRE(a->stat_count > 0, "ema_finalize: stat_count must be > 0");
+  VQGNN_REQUIRE((size_t)a->M * 4 <= 136 * 1024, "ema_finalize: M=%d too large for the LDS", a->M);
+  const StatShift sh = stat_shift(a->stat_count, a->grad_scale);
+  EmaFin& e = *f;
+  e.stats = reinterpret_cast<long long*>(a->ema_parts);
+  e.nparts = a->nparts;
+  e.part_stride = (int64_t)a->nb * a->M * (a->W + 1);
+  e.zero_after = a->zero_after;
+  e.shift_f = sh.f;
+  e.shift_g = sh.g;
+  e.M = a->M;
+  e.D = a->D;
+  e.W = a->W;
+  e.ldw = a->ldw;
+  e.decay = a->decay;
+  e.laplace = a->laplace;
+  e.grad_scale = a->grad_scale;
+  e.epsilon = a->epsilon;
+  e.cluster_size = a->cluster_size;
+  e.cs_bstride = a->cs_bstride;
+  e.ema_w = a->ema_w;
+  e.emb = a->embedding;
+  e.emb_out = a->embedding_output;
+  e.emb_bstride = a->emb_bstride;
+  e.rm_f = a->rm_f;
+  e.rv_f = a->rv_f;
+  e.rm_g = a->rm_g;
+  e.rv_g = a->rv_g;
+  e.bad_init = a->bad_init;
+  // M >= 1024: the per-codeword half runs in a second, wider launch
+  e.split = a->M >= 1024 && !env_int_vq("VQGNN_EMA_FIN_ONE", 0);
+  return VQGNN_OK;
+}
+
+void ema_fin_lds_attr(const void* kernel) {
+  (void)hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 136 * 1024);
+}
+
+// the finalize's own launches (and the apply half when split)
+static int ema_fin_launch(const EmaFin& f, int nb, hipStream_t s) {
+  const size_t lds = (size_t)f.M * sizeof(float);
+  if (lds > 48 * 1024) {
+    static std::once_flag once;
+    std::call_once(once, [] { ema_fin_lds_attr((const void*)vq_ema_finalize_kernel); });
+  }
+  hipLaunchKernelGGL(vq_ema_finalize_kernel, dim3(nb), dim3(kFinThreads), lds, s, f);
+  if (f.split)
+    hipLaunchKernelGGL(vq_ema_apply_kernel, dim3((f.M + kApplySlice - 1) / kApplySlice, nb),
+                       dim3(kApplyThreads), 0, s, f.stats, f.nparts, f.part_stride,
+                       f.zero_after, f.shift_f, f.shift_g, f.M, f.D, f.W, f.ldw, f.decay,
+                       f.grad_scale, f.epsilon, f.cluster_size, f.cs_bstride, f.ema_w, f.emb,
+                       f.emb_out, f.emb_bstride, f.rm_f, f.rv_f, f.rm_g, f.rv_g);
+  return check_launch("ema_finalize");
+}
+
+int ema_fin_run(const EmaFin& f, int nb, hipStream_t s) { return ema_fin_launch(f, nb, s); }
+
+}  // namespace vqgnn
+
 extern "C" int vqgnn_vq_ema_finalize(int64_t* ema_parts, int32_t nparts, int32_t zero_after,
                                      int64_t stat_count, int32_t nb,
                                      int32_t M, int32_t D, int32_t W, int32_t ldw, float decay,
@@ -3056,38 +3026,35 @@ extern "C" int vqgnn_vq_ema_finalize(int64_t* ema_parts, int32_t nparts, int32_t
                                      const float* rm_g, const float* rv_g, int32_t* bad_init,
                                      vqgnn_stream_t stream) {
   clear_error();
-  VQGNN_REQUIRE(ema_parts && cluster_size && ema_w && embedding && embedding_output && bad_init,
-                "ema_finalize: null pointer");
-  VQGNN_REQUIRE(rm_f && rv_f, "ema_finalize: feature running stats required");
-  VQGNN_REQUIRE(W == D || (W == 2 * D && rm_g && rv_g), "ema_finalize: W must be D or 2D");
-  VQGNN_REQUIRE(nb > 0 && M > 0 && ldw >= W && nparts > 0, "ema_finalize: bad shape");
-  VQGNN_REQUIRE(stat_count > 0, "ema_finalize: stat_count must be > 0");
-  VQGNN_REQUIRE((size_t)M * 4 <= 136 * 1024, "ema_finalize: M=%d too large for the LDS", M);
-  const StatShift sh = stat_shift(stat_count, grad_scale);
-  const size_t lds = (size_t)M * sizeof(float);
-  if (lds > 48 * 1024) {
-    static std::once_flag once;
-    std::call_once(once, [] {
-      (void)hipFuncSetAttribute((const void*)vq_ema_finalize_kernel,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 136 * 1024);
-    });
-  }
-  // M >= 1024: the per-codeword half runs in a second, wider launch
-  const int split = M >= 1024 && !env_int_vq("VQGNN_EMA_FIN_ONE", 0);
-  hipLaunchKernelGGL(vq_ema_finalize_kernel, dim3(nb), dim3(kFinThreads), lds, as_stream(stream),
-                     reinterpret_cast<long long*>(ema_parts), nparts,
-                     (int64_t)nb * M * (W + 1), zero_after, sh.f, sh.g, M, D, W, ldw, decay,
-                     laplace,
-                     grad_scale, epsilon, cluster_size, cs_bstride, ema_w, embedding,
-                     embedding_output, emb_bstride, rm_f, rv_f, rm_g, rv_g, bad_init, split);
-  if (split)
-    hipLaunchKernelGGL(vq_ema_apply_kernel, dim3((M + kApplySlice - 1) / kApplySlice, nb),
-                       dim3(kApplyThreads), 0, as_stream(stream),
-                       reinterpret_cast<long long*>(ema_parts), nparts, (int64_t)nb * M * (W + 1),
-                       zero_after, sh.f, sh.g, M, D, W, ldw, decay, grad_scale, epsilon,
-                       cluster_size, cs_bstride, ema_w, embedding, embedding_output, emb_bstride,
-                       rm_f, rv_f, rm_g, rv_g);
-  return check_launch("ema_finalize");
+  vqgnn_ema_finalize_args a{};
+  a.ema_parts = ema_parts;
+  a.nparts = nparts;
+  a.zero_after = zero_after;
+  a.stat_count = stat_count;
+  a.nb = nb;
+  a.M = M;
+  a.D = D;
+  a.W = W;
+  a.ldw = ldw;
+  a.decay = decay;
+  a.laplace = laplace;
+  a.grad_scale = grad_scale;
+  a.epsilon = epsilon;
+  a.cluster_size = cluster_size;
+  a.cs_bstride = cs_bstride;
+  a.ema_w = ema_w;
+  a.embedding = embedding;
+  a.embedding_output = embedding_output;
+  a.emb_bstride = emb_bstride;
+  a.rm_f = rm_f;
+  a.rv_f = rv_f;
+  a.rm_g = rm_g;
+  a.rv_g = rv_g;
+  a.bad_init = bad_init;
+  EmaFin f{};
+  const int rc = ema_fin_prepare(&a, &f);
+  if (rc != VQGNN_OK) return rc;
+  return ema_fin_run(f, nb, as_stream(stream));
 }
 
 extern "C" int vqgnn_assign_timing(int32_t enable) {

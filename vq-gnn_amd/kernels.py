@@ -256,6 +256,28 @@ def vq_ema_finalize(parts, D, W, decay, laplace, grad_scale, epsilon, cs, ema_w,
                                       ptr(bad_flag), stream_ptr()), "vq_ema_finalize")
 
 
+def ema_finalize_args(parts, D, W, decay, laplace, grad_scale, epsilon, cs, ema_w, emb, emb_out,
+                      rm_f, rv_f, rm_g, rv_g, bad_flag, stat_count, zero_after=False):
+    """vq_ema_finalize's operands as include/vqgnn.h §4b's record, for
+    spmm_codebook(finalize=...): the same checks; the tensors must outlive
+    the call that consumes the record."""
+    P, nb, M, _ = parts.shape
+    if not (ema_w.stride() == emb.stride() == emb_out.stride()):
+        raise ValueError("ema_w / embedding / output must share one layout")
+    if parts.dtype != torch.int64:
+        raise ValueError("EMA statistic slabs are int64 fixed point")
+    from ._lib import EmaFinalizeArgs
+    return EmaFinalizeArgs(
+        ema_parts=parts.data_ptr(), nparts=P, zero_after=int(bool(zero_after)),
+        stat_count=int(stat_count), nb=nb, M=M, D=D, W=W, ldw=emb.shape[2],
+        decay=float(decay), laplace=int(laplace), grad_scale=float(grad_scale),
+        epsilon=float(epsilon), cluster_size=cs.data_ptr(), cs_bstride=cs.stride(0),
+        ema_w=ema_w.data_ptr(), embedding=emb.data_ptr(), embedding_output=emb_out.data_ptr(),
+        emb_bstride=emb.stride(0), rm_f=rm_f.data_ptr(), rv_f=rv_f.data_ptr(),
+        rm_g=rm_g.data_ptr() if rm_g is not None else None,
+        rv_g=rv_g.data_ptr() if rv_g is not None else None, bad_init=bad_flag.data_ptr())
+
+
 def gather_codewords(subset, B, codes, emb_out, D, col_offset=0, want_x=True,
                      want_codes=False, nb=None):
     """models.py:168-173 for all branches: returns (xt [n-B, nb*D] or None,
@@ -458,12 +480,18 @@ def codebook_source_preferred(M):
     return int(lib().vqgnn_spmm_task_cb_lds(int(M))) == int(M) * 16 * 32
 
 
-def spmm_codebook(rowptr, n_rows, nnz, X, F, B, codes, emb_out, D, plan_cb, out=None):
+def spmm_codebook(rowptr, n_rows, nnz, X, F, B, codes, emb_out, D, plan_cb, out=None,
+                  finalize=None):
     """out = A @ [X[:B] ; x_first_order] with x_first_order's rows (the
     codeword feature halves of each out-of-batch node's codes, models.py:
     168-173) read from an LDS image of emb_out (vqgnn_spmm_task_cb); plan_cb
     from TaskPlan.with_codebook_source.  Equals spmm(..., X2=gather_codewords
-    (subset, B, codes, emb_out, D)[0], B=B)."""
+    (subset, B, codes, emb_out, D)[0], B=B).
+
+    finalize: an EMA finalize's operands (vq_ema_finalize's positional
+    arguments and keywords, as VQBank.take_fused_finalize returns them) run
+    inside the SpMM's fix-up launch (vqgnn_spmm_task_cb_fin): the same
+    results as this call followed by vq_ema_finalize, one launch fewer."""
     require_gpu(X, "spmm_codebook")
     if getattr(plan_cb, "cb_B", None) != int(B):
         raise ValueError("spmm_codebook: plan_cb must come from TaskPlan.with_codebook_source "
@@ -483,12 +511,18 @@ def spmm_codebook(rowptr, n_rows, nnz, X, F, B, codes, emb_out, D, plan_cb, out=
         out = torch.empty(n_rows, F, dtype=torch.float32, device=dev)
     L = lib()
     ws = workspace(L.vqgnn_spmm_task_workspace(int(nnz), plan_cb.K, F), dev)
-    check(L.vqgnn_spmm_task_cb(ptr(rowptr), int(n_rows), int(nnz), int(B), ptr(X), _ld(X), F,
-                               ptr(codes), codes.stride(0), codes.shape[0], ptr(emb_out),
-                               emb_out.stride(1), emb_out.stride(0), n_br, M, int(D), ptr(out),
-                               _ld(out), ptr(plan_cb.plan), ptr(plan_cb.records), plan_cb.K,
-                               plan_cb.n_jobs, plan_cb.n_empty, ptr(ws), stream_ptr()),
-          "spmm_task_cb")
+    args = (ptr(rowptr), int(n_rows), int(nnz), int(B), ptr(X), _ld(X), F,
+            ptr(codes), codes.stride(0), codes.shape[0], ptr(emb_out),
+            emb_out.stride(1), emb_out.stride(0), n_br, M, int(D), ptr(out),
+            _ld(out), ptr(plan_cb.plan), ptr(plan_cb.records), plan_cb.K,
+            plan_cb.n_jobs, plan_cb.n_empty, ptr(ws))
+    if finalize is None:
+        check(L.vqgnn_spmm_task_cb(*args, stream_ptr()), "spmm_task_cb")
+    else:
+        fin_args, fin_kw = finalize
+        rec = ema_finalize_args(*fin_args, **fin_kw)
+        check(L.vqgnn_spmm_task_cb_fin(*args, ctypes.byref(rec), stream_ptr()),
+              "spmm_task_cb_fin")
     return out
 
 

@@ -322,6 +322,24 @@ class VQBank(nn.Module):
         self._clean(*clean)
         self._finish()
 
+    def take_fused_finalize(self):
+        """Hand the pending finalize of an update(defer=True) to the caller's
+        next aggregation, which runs it inside its fix-up launch
+        (kernels.spmm_codebook(finalize=...), include/vqgnn.h §6b):
+        -> ((args, kw), done) -- call done() once that aggregation is queued
+        -- or None when nothing is pending, or when the finalize must wait for
+        the multi-GPU all-reduce of its statistics (finish_update() then)."""
+        p = self._pending_finalize
+        if p is None or p[0] is not None:
+            return None
+        self._pending_finalize = None
+        _, fin_args, fin_kw, clean = p
+
+        def done():
+            self._clean(*clean)
+            self._finish()
+        return (fin_args, fin_kw), done
+
     def update(self, X, G, b0, nbr, training, idx_out=None, codes=None, batch_idx=None,
                defer=False):
         """vq.py:204-279 for branches [b0, b0+nbr): X, G are [B, nbr*D] views.
