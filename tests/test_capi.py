@@ -107,3 +107,49 @@ def test_codebook_source_preferred_only_at_full_width():
     assert kernels.codebook_source_preferred(256) and kernels.codebook_source_preferred(320)
     assert not kernels.codebook_source_preferred(321)
     assert not kernels.codebook_source_preferred(1024)
+
+
+def test_ema_finalize_args_layout_matches_header(tmp_path):
+    """The ctypes record (vq_gnn_amd._lib.EmaFinalizeArgs) has the C layout of
+    include/vqgnn.h §4b's vqgnn_ema_finalize_args: every field's offset and
+    the size, as gcc lays the header's struct out."""
+    import ctypes
+    import shutil
+    import subprocess
+    import pytest
+    if shutil.which("gcc") is None:
+        pytest.skip("no gcc")
+    names = [f[0] for f in L.EmaFinalizeArgs._fields_]
+    src = tmp_path / "off.c"
+    src.write_text(
+        "#include <stdio.h>\n#include <stddef.h>\n#include \"vqgnn.h\"\n"
+        "int main(void) {\n"
+        + "".join(f'  printf("%zu\\n", offsetof(vqgnn_ema_finalize_args, {n}));\n' for n in names)
+        + '  printf("%zu\\n", sizeof(vqgnn_ema_finalize_args));\n  return 0;\n}\n')
+    exe = tmp_path / "off"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)],
+                   check=True)
+    got = [int(v) for v in subprocess.run([str(exe)], check=True, capture_output=True,
+                                          text=True).stdout.split()]
+    want = [getattr(L.EmaFinalizeArgs, n).offset for n in names] + \
+        [ctypes.sizeof(L.EmaFinalizeArgs)]
+    assert got == want
+
+
+def test_fused_finalize_entry_checks_the_finalize_first():
+    """vqgnn_spmm_task_cb_fin rejects a bad finalize record before any
+    launch (dummy device addresses are never dereferenced)."""
+    import ctypes
+    h = L.lib()
+    fin = L.EmaFinalizeArgs(ema_parts=16, nparts=1, zero_after=1, stat_count=100, nb=32, M=256,
+                            D=4, W=6, ldw=8, decay=0.99, laplace=1, grad_scale=1.0,
+                            epsilon=1e-5, cluster_size=16, cs_bstride=256, ema_w=16,
+                            embedding=16, embedding_output=16, emb_bstride=2048, rm_f=16,
+                            rv_f=16, rm_g=16, rv_g=16, bad_init=16)
+    args = (16, 100, 1000, 50, 16, 128, 128, 16, 32, 1000, 16, 8, 2048, 32, 256, 4, 16, 128,
+            16, 16, 64, 0, 0, 16)
+    rc = h.vqgnn_spmm_task_cb_fin(*args, ctypes.byref(fin), None)
+    assert rc == 1 and b"W must be D or 2D" in h.vqgnn_last_error()
+    fin.W, fin.stat_count = 8, 0
+    rc = h.vqgnn_spmm_task_cb_fin(*args, ctypes.byref(fin), None)
+    assert rc == 1 and b"stat_count" in h.vqgnn_last_error()

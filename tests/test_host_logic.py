@@ -218,3 +218,27 @@ def test_bn_fold_gating(monkeypatch):
     assert not bank._bn_fold(1000, 4, 8, F64, F64)        # all-FP64: the fp64-sum path
     monkeypatch.setattr(kernels, "bn_fold_supported", lambda *a: False)
     assert not bank._bn_fold(1000, 4, 8, S, S)
+
+
+def test_take_fused_finalize_hand_off():
+    """VQBank.take_fused_finalize: a pending single-process finalize goes to
+    the caller once (with a done() that clears the slab flags), nothing when
+    nothing is pending, and a multi-GPU one (an all-reduce to wait for) stays
+    with finish_update()."""
+    from vq_gnn_amd.vq import VQBank
+    bank = VQBank(2, 16, 4, warm_up_flag=True)
+    assert bank.take_fused_finalize() is None
+    calls = []
+    bank._clean = lambda *a: calls.append(("clean", a))
+    bank._finish = lambda: calls.append(("finish",))
+    bank._pending_finalize = (None, ("args",), {"zero_after": True}, (8, 0, 2))
+    got = bank.take_fused_finalize()
+    assert got is not None and got[0] == (("args",), {"zero_after": True})
+    assert bank._pending_finalize is None and calls == []
+    got[1]()
+    assert calls == [("clean", (8, 0, 2)), ("finish",)]
+    assert bank.take_fused_finalize() is None
+    work = object()
+    bank._pending_finalize = (work, ("args",), {}, (8, 0, 2))
+    assert bank.take_fused_finalize() is None
+    assert bank._pending_finalize[0] is work
