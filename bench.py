@@ -219,9 +219,7 @@ def main():
             fin = None if args.separate_finalize else bank.take_fused_finalize()
             fin_fused[0] = fin is not None
             kernels.spmm_codebook(adj.rowptr, n, nnz, Xd, F, B, codes, bank.emb_out, D,
-                                  spmm_plan, finalize=fin[0] if fin else None)
-            if fin:
-                fin[1]()
+                                  spmm_plan, finalize=fin)
             if record:
                 e[3].record()
             return
@@ -370,7 +368,7 @@ def main():
     roofline = dict(bound=dominant["bound"], achieved=dominant["achieved"], peak=dominant["peak"],
                     unit=dominant["unit"], frac=dominant["frac"], traffic=dominant["traffic"],
                     kernel=dominant["kernel"], traffic_source=pmc_note)
-    for k in ("limiter", "valu_issue_frac", "wait_frac", "effective_f32_frac"):
+    for k in ("limiter", "mfma_issue_frac", "valu_issue_frac", "wait_frac", "effective_f32_frac"):
         if k in dominant:
             roofline[k] = dominant[k]
 
@@ -475,17 +473,17 @@ F16_PEAK_TF, F32_PEAK_TF, SIMDS, CLOCK_HZ, VALU_CYCLES = 2500.0, 157.3, 1024, 2.
 
 
 def assign_roofline(name, assign_ms, B, M, W, nb, f32_flops, ctr):
-    """The assign's roofline on the resources it issues:
-    vq_filter_kernel scores every codeword with v_mfma_f32_16x16x32_f16
-    (16,384 flops per instruction) and recomputes the candidates on the VALU,
-    so it is priced against the dense f16 matrix peak, with the VALU issue
-    fraction and the share of wave cycles spent waiting beside it, from the
-    hash-stamped PMC counters of this build (SQ_INSTS_MFMA, SQ_INSTS_VALU,
-    SQ_WAIT_ANY / SQ_WAVE_CYCLES).  Without counters the MFMA count is the
-    analytic lower bound (64 MFMAs per 64-row wave iteration per 256
-    codewords).  The exact f32 path (vq_assign_kernel, W > 8) is priced
-    against the f32 matrix peak.  f32-equivalent distance work over the f32
-    peak is reported only as effective_f32_frac."""
+    """The assign's roofline by SURVEY §8(d): algorithmic flops (2*B*M*W*nb,
+    the distance contraction) / the kernel's own launch time / the dense peak
+    of the matrix pipe the kernel computes them on.  vq_filter_kernel scores
+    every codeword with v_mfma_f32_16x16x32_f16, so its peak is the dense f16
+    peak; the exact f32 path (vq_assign_kernel, W > 8) is
+    priced against the f32 matrix peak.  Beside it, from the hash-stamped PMC
+    counters of this build: mfma_issue_frac = f16 MFMA flops ISSUED
+    (SQ_INSTS_MFMA x 16,384: the hi/lo split issues ~4.3x the algorithmic
+    flops) over the same peak, the VALU issue fraction and the share of wave
+    cycles spent waiting.  effective_f32_frac = the algorithmic flops over the
+    f32 peak (what the exact path would need; not a roofline)."""
     t = assign_ms * 1e-3
     eff = f32_flops / t / 1e12 / F32_PEAK_TF
     if name != "vq_filter_kernel":
@@ -493,24 +491,28 @@ def assign_roofline(name, assign_ms, B, M, W, nb, f32_flops, ctr):
                     unit="TFLOP/s", frac=eff, flops_per_launch=f32_flops, ms_per_launch=assign_ms,
                     flops_note="2*B*M*W*nb f32 flops (exact sweep, v_mfma_f32_16x16x4_f32)",
                     effective_f32_frac=eff)
+    out = dict(kernel=name, bound="mfma", achieved=f32_flops / t / 1e12, peak=F16_PEAK_TF,
+               unit="TFLOP/s", flops_per_launch=f32_flops, ms_per_launch=assign_ms,
+               flops_note="2*B*M*W*nb algorithmic distance flops (SURVEY 8d) over the dense f16 "
+                          "peak of the pipe the filter scores on",
+               effective_f32_frac=eff,
+               effective_f32_note="the same flops / time / 157.3 TF/s (f32 peak): what the exact "
+                                  "path would need, not a roofline")
+    out["frac"] = out["achieved"] / out["peak"]
     if ctr and ctr.get("SQ_INSTS_MFMA"):
         mfma = ctr["SQ_INSTS_MFMA"]
         src = "SQ_INSTS_MFMA x 16384 (PMC, this build)"
     else:
         mfma = nb * -(-B // 64) * 4 * (M // 16)
         src = "analytic lower bound: nb * ceil(B/64) * 4 groups * M/16 tiles (no PMC for this build)"
-    f16 = mfma * 16384.0
-    out = dict(kernel=name, bound="mfma", achieved=f16 / t / 1e12, peak=F16_PEAK_TF,
-               unit="TFLOP/s", flops_per_launch=f16, ms_per_launch=assign_ms,
-               flops_note=f"f16 MFMA flops issued: {src}; dense f16 peak",
-               effective_f32_frac=eff,
-               effective_f32_note="2*B*M*W*nb f32 distance flops / time / 157.3 TF/s (f32 peak): "
-                                  "what the exact path would need, not a roofline")
-    out["frac"] = out["achieved"] / out["peak"]
+    issued = mfma * 16384.0
+    out["mfma_issue_frac"] = issued / t / 1e12 / F16_PEAK_TF
+    out["mfma_issued_flops"] = issued
+    out["mfma_issue_note"] = f"f16 MFMA flops issued: {src}, over the dense f16 peak"
     if ctr and ctr.get("SQ_INSTS_VALU") and ctr.get("SQ_WAVE_CYCLES"):
         out["valu_issue_frac"] = ctr["SQ_INSTS_VALU"] * VALU_CYCLES / SIMDS / CLOCK_HZ / t
         out["wait_frac"] = ctr.get("SQ_WAIT_ANY", 0.0) / ctr["SQ_WAVE_CYCLES"]
-        busiest = max(("f16 MFMA", out["frac"]), ("VALU issue", out["valu_issue_frac"]),
+        busiest = max(("f16 MFMA", out["mfma_issue_frac"]), ("VALU issue", out["valu_issue_frac"]),
                       key=lambda kv: kv[1])
         out["limiter"] = (f"latency: {out['wait_frac']:.0%} of wave cycles waiting; busiest issue "
                           f"port {busiest[0]} at {busiest[1]:.0%} (PMC)")

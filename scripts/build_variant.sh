@@ -2,7 +2,10 @@
 # Build a library variant with one source file replaced (A/B measurements):
 #   build_variant.sh <name> <replaced.hip> <replacement file>
 # -> vq-gnn_amd/lib/ab_<name>.so (travels to the GPU box; select it with
-#    VQGNN_LIB=vq-gnn_amd/lib/ab_<name>.so)
+#    VQGNN_LIB=vq-gnn_amd/lib/ab_<name>.so).  The replaced file is compiled
+#    with -DVQGNN_EXPERIMENTS: its measurement knobs (VQGNN_TASK_U/G,
+#    VQGNN_ASG_*, VQGNN_ASSIGN_MSWEEP, VQGNN_TASK_DBG, ...) read the
+#    environment there and only there -- the default library ignores them.
 set -e
 cd "$(dirname "$0")/../vq-gnn_amd/csrc"
 name=$1; src=$2; repl=$3
@@ -14,7 +17,7 @@ objs=""
 for f in $(sed -n 's/^SRCS := //p;s/^         //p' Makefile | tr ' ' '\n' | grep hip); do
   if [ "$f" = "$src" ]; then
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++20 -ffp-contract=off -Wall \
-      -Wno-unused-function -munsafe-fp-atomics -I$PWD -c $tmp/$src -o $tmp/${src%.hip}.o
+      -Wno-unused-function -munsafe-fp-atomics -DVQGNN_EXPERIMENTS -I$PWD -c $tmp/$src -o $tmp/${src%.hip}.o
     objs="$objs $tmp/${src%.hip}.o"
   else
     objs="$objs ../lib/obj/${f%.hip}.o"

@@ -27,10 +27,25 @@ for name, c in d.items():
     # wait fraction), per launch
     counters[key] = {k: v for k, v in c.items()
                      if k.startswith("SQ_") or k in ("GRBM_GUI_ACTIVE", "dur_ns_mean")}
+
+
+def git_head():
+    """The commit the counters belong to: $GIT_HEAD (the GPU box gets no .git
+    directory), else the local repository's HEAD, else null."""
+    if os.environ.get("GIT_HEAD"):
+        return os.environ["GIT_HEAD"]
+    try:
+        import subprocess
+        return subprocess.run(["git", "-C", ROOT, "rev-parse", "HEAD"], capture_output=True,
+                              text=True, check=True).stdout.strip() or None
+    except Exception:
+        return None
+
+
 h = hashlib.sha256(open(os.path.join(ROOT, "vq-gnn_amd", "lib", "libvqgnn.so"), "rb").read())
 json.dump({"config": config, "semantics": semantics, "hbm_bytes_per_launch": res,
            "counters_per_launch": counters,
-           "lib_sha256": h.hexdigest(), "git_head": os.environ.get("GIT_HEAD"),
+           "lib_sha256": h.hexdigest(), "git_head": git_head(),
            "rule": "2*FETCH_SIZE + WRITE_SIZE (KB->B), per launch, gfx950 wide-read correction",
            "source": summary}, open(out, "w"), indent=1)
 print(json.dumps(res, indent=1))

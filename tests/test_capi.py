@@ -153,3 +153,26 @@ def test_fused_finalize_entry_checks_the_finalize_first():
     fin.W, fin.stat_count = 8, 0
     rc = h.vqgnn_spmm_task_cb_fin(*args, ctypes.byref(fin), None)
     assert rc == 1 and b"stat_count" in h.vqgnn_last_error()
+
+
+def test_default_library_reads_no_measurement_knobs():
+    """The shipped library never reads the measurement knobs that cut work
+    short or drop stores (VQGNN_TASK_DBG, VQGNN_ASSIGN_MSWEEP, the schedule
+    and chunk knobs): they exist only in -DVQGNN_EXPERIMENTS builds
+    (scripts/build_variant.sh).  The environment names it can read are the
+    three alternative-implementation switches, whose results the suite checks
+    equal to the default path's."""
+    data = open(L._DEFAULT_LIB, "rb").read()
+    names = set(m.decode() for m in re.findall(rb"VQGNN_[A-Z0-9_]+", data))
+    assert names <= {"VQGNN_ASSIGN_EXACT", "VQGNN_EMA_GLOBAL", "VQGNN_SPMM_FAR"}, names
+    for knob in (b"VQGNN_TASK_DBG", b"VQGNN_ASSIGN_MSWEEP", b"VQGNN_TASK_U", b"VQGNN_ASG_CHUNK"):
+        assert knob not in data
+
+
+def test_bn_fold_refuses_chunked_codebooks():
+    """the BatchNorm fold is not offered for a codebook the assign
+    stages in chunks (chunk-outer passes, ppi's M = 4,096), a combination no
+    parity test pins; the single-chunk arxiv shape keeps it (host query)."""
+    h = L.lib()
+    assert h.vqgnn_vq_assign_bn_supported(30_000, 13, 4, 4096, 8) == 0
+    assert h.vqgnn_vq_assign_bn_supported(84_670, 32, 4, 256, 8) == 1

@@ -79,6 +79,7 @@ def test_fold_supported_bounds():
     assert not kernels.bn_fold_supported(1, 32, 4, 256, 8)          # B <= 1
     assert not kernels.bn_fold_supported(1000, 32, 4, 256, 16)      # W > 8: the exact kernel
     assert not kernels.bn_fold_supported((1 << 23) + 1, 1, 4, 64, 8)
+    assert not kernels.bn_fold_supported(30_000, 13, 4, 4096, 8)    # chunk-outer passes
 
 
 def test_fold_is_single_use():

@@ -85,10 +85,7 @@ def test_finalize_fused_into_codebook_spmm(monkeypatch, semantics, M):
             else:                   # feature_update finalizes at once: nothing pending
                 assert fin is None
             out = kernels.spmm_codebook(adj.rowptr, bt.n, bt.nnz, X, F, bt.B, codes,
-                                        bank.emb_out, D, pcb,
-                                        finalize=fin[0] if fin else None)
-            if fin:
-                fin[1]()
+                                        bank.emb_out, D, pcb, finalize=fin)
             bank.finish_update()
             if fused:
                 out_b = out

@@ -89,6 +89,39 @@ def test_assign_repeat_launches_identical(M, B):
     assert not bad, f"(launch, mismatching rows): {bad}"
 
 
+@pytest.mark.parametrize("M,nb", [(256, 32), (1024, 32), (4096, 13)])
+def test_assign_repeat_launches_many_branches(M, nb):
+    """The shapes where round 5's packed-f32 resolve variant returned different
+    indices on repeated launches (13-32 branches x 30,000 rows, M = 256 /
+    1,024 / 4,096; profiles/r05_pipe_packed_determinism.txt, DESIGN.md 4.1
+    "Nondeterminism"): every one of 4 launches of the shipped assign equals
+    the oracle, branch by branch."""
+    D, W, B = 4, 8, 30_000
+    g = torch.Generator().manual_seed(M + nb)
+    X = torch.randn(B, nb * D, generator=g)
+    G = torch.randn(B, nb * D, generator=g) * 1e-3
+    emb = torch.rand(nb, M, 2 * D, generator=g) * 2 - 1
+    af, bf = torch.ones(nb * D), torch.zeros(nb * D)
+    ag, bg = torch.full((nb * D,), 1000.0), torch.zeros(nb * D)
+    ref = torch.empty(nb, B, dtype=torch.long)
+    for b in range(nb):
+        cs = slice(b * D, (b + 1) * D)
+        for r0 in range(0, B, 5000):
+            rs = slice(r0, r0 + 5000)
+            ref[b, rs], _ = vq_ref.assign_with_coef(X[rs, cs], G[rs, cs], af[cs], bf[cs], ag[cs],
+                                                    bg[cs], 0.75, emb[b])
+    coef = _coef_tensor(af, bf, ag, bg)
+    Xd, Gd, Ed = X.to(DEV), G.to(DEV), emb.to(DEV)
+    bad = []
+    for rep in range(4):
+        idx = torch.empty(nb, B, dtype=torch.long, device=DEV)
+        kernels.vq_assign(Xd, Gd, coef, 0.75, Ed, D, W, idx_out=idx)
+        diff = idx.cpu() != ref
+        if diff.any():
+            bad.append((rep, int(diff.sum()), diff.any(0).nonzero().flatten()[:6].tolist()))
+    assert not bad, f"(launch, mismatching entries, first rows): {bad}"
+
+
 @pytest.mark.parametrize("M,W", [(256, 8), (256, 4), (1024, 8), (4096, 8), (40, 8)])
 def test_assign_near_ties_resolved_exactly(M, W):
     """The filtered sweep (f16-split scores on the MFMA) sends rows whose

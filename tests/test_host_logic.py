@@ -222,23 +222,47 @@ def test_bn_fold_gating(monkeypatch):
 
 def test_take_fused_finalize_hand_off():
     """VQBank.take_fused_finalize: a pending single-process finalize goes to
-    the caller once (with a done() that clears the slab flags), nothing when
-    nothing is pending, and a multi-GPU one (an all-reduce to wait for) stays
-    with finish_update()."""
+    the caller as a handle whose done() retires it (once) and clears the slab
+    flags; nothing when nothing is pending; a multi-GPU one (an all-reduce to
+    wait for) stays with finish_update()."""
     from vq_gnn_amd.vq import VQBank
     bank = VQBank(2, 16, 4, warm_up_flag=True)
     assert bank.take_fused_finalize() is None
     calls = []
     bank._clean = lambda *a: calls.append(("clean", a))
     bank._finish = lambda: calls.append(("finish",))
-    bank._pending_finalize = (None, ("args",), {"zero_after": True}, (8, 0, 2))
+    entry = (None, ("args",), {"zero_after": True}, (8, 0, 2))
+    bank._pending_finalize = entry
     got = bank.take_fused_finalize()
-    assert got is not None and got[0] == (("args",), {"zero_after": True})
-    assert bank._pending_finalize is None and calls == []
-    got[1]()
+    assert got is not None and got.operands == (("args",), {"zero_after": True})
+    assert bank._pending_finalize is entry and calls == []    # pending until queued
+    got.done()
+    assert calls == [("clean", (8, 0, 2)), ("finish",)]
+    assert bank._pending_finalize is None
+    got.done()                                                 # idempotent
     assert calls == [("clean", (8, 0, 2)), ("finish",)]
     assert bank.take_fused_finalize() is None
     work = object()
     bank._pending_finalize = (work, ("args",), {}, (8, 0, 2))
     assert bank.take_fused_finalize() is None
     assert bank._pending_finalize[0] is work
+
+
+def test_fused_finalize_survives_a_failed_aggregation():
+    """an aggregation that raises after the hand-off (here: the
+    no-CPU-fallback guard of spmm_codebook) leaves the finalize pending, so
+    the next finish_update() still runs the codebook update."""
+    import pytest
+    from vq_gnn_amd import kernels
+    from vq_gnn_amd.vq import VQBank
+    bank = VQBank(2, 16, 4, warm_up_flag=True)
+    calls = []
+    bank._clean = lambda *a: calls.append(("clean", a))
+    bank._finish = lambda: calls.append(("finish",))
+    entry = (None, ("args",), {"zero_after": True}, (8, 0, 2))
+    bank._pending_finalize = entry
+    fin = bank.take_fused_finalize()
+    X = torch.zeros(4, 32)
+    with pytest.raises(Exception):
+        kernels.spmm_codebook(None, 4, 0, X, 32, 4, None, bank.emb_out, 4, None, finalize=fin)
+    assert bank._pending_finalize is entry and calls == []

@@ -6,6 +6,7 @@
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 
 #include "../../include/vqgnn.h"
 
@@ -35,7 +36,25 @@ __device__ __forceinline__ int xcd_remap(int orig, int n) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + local;
 }
 
+// Environment of the alternative-implementation knobs the test suite drives
+// (VQGNN_SPMM_FAR, VQGNN_EMA_GLOBAL, VQGNN_ASSIGN_EXACT): each selects another
+// kernel whose results are identical to the default's (tested both ways).
+inline int path_env(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v && *v ? atoi(v) : dflt;
+}
+
 }  // namespace vqgnn
+
+// Measurement knobs (other schedules, chunk sizes, work cut short for timing)
+// exist only in builds compiled with -DVQGNN_EXPERIMENTS
+// (scripts/build_variant.sh); the default library never reads them, so no
+// environment variable can truncate or drop its work.
+#ifdef VQGNN_EXPERIMENTS
+#define VQGNN_KNOB(name, dflt) (::vqgnn::path_env(name, dflt))
+#else
+#define VQGNN_KNOB(name, dflt) (dflt)
+#endif
 
 #define VQGNN_REQUIRE(cond, ...)                    \
   do {                                              \

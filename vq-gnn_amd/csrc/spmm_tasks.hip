@@ -66,7 +66,8 @@ struct TaskArgs {
   const char* ubase;
   uint32_t span, offx, ldxb, offx2, ldx2b;
   uint32_t ldob;            // near path: ldo in bytes (rows addressed with a 24-bit multiply)
-  int dbg;                  // experiments: 1 = no row stores (results invalid)
+  int dbg;                  // VQGNN_TASK_DBG (experiments builds only): 1 = no row
+                            // stores, results invalid; 0 in the default library
   // GAT mode (OurGATConv + the layer's ones-column normalisation): edge
   // weight = exp(leaky(al[j] + ar[i])) * w with al, ar = alpha / s per node,
   // rows < norm_B divided by their coefficient sum + 1e-16
@@ -696,11 +697,6 @@ spmm_fixup_fin_kernel(TaskArgs a, EmaFin f, int nb) {
   task_fixup_thread<false>(a, ((int)blockIdx.x - nb) * kFinThreads + threadIdx.x);
 }
 
-static int task_env(const char* name, int dflt) {
-  const char* v = getenv(name);
-  return v ? atoi(v) : dflt;
-}
-
 template <int G, int NC, int U, bool FAR, bool GAT, bool PART = false>
 static void launch_task(const TaskArgs& a, int tiles, hipStream_t s) {
   const int waves = (a.ntasks + 64 / G - 1) / (64 / G);
@@ -788,7 +784,7 @@ extern "C" int vqgnn_spmm_task_plan(const int32_t* rowptr, const int32_t* col, c
     return check_launch("spmm_task_plan memset");
   task_records(rowptr, col, val, n_rows, nnz, reinterpret_cast<int2*>(records), s);
   hipLaunchKernelGGL(task_first_row_kernel, dim3((ntasks + 256) / 256), dim3(256), 0, s, rowptr,
-                     n_rows, (int)nnz, K, task_env("VQGNN_TASK_SNAP", 1) ? K / 2 : 0, ntasks,
+                     n_rows, (int)nnz, K, VQGNN_KNOB("VQGNN_TASK_SNAP", 1) ? K / 2 : 0, ntasks,
                      task_start, task_row);
   const int nx = ntasks > n_rows ? ntasks : n_rows;
   if (nx > 0)
@@ -859,7 +855,7 @@ static int task_setup(TaskArgs& a, const int32_t* rowptr, int32_t n_rows, int32_
   *near = hi - lo < 0x7FFFFFF0ull && (int64_t)ldx * 4 < (1 << 24) &&
           (int64_t)a.ldx2 * 4 < (1 << 24) && (int64_t)ldo * 4 < (1 << 24) &&
           n_cols < (1 << 24) && n_rows < (1 << 24) &&
-          (int64_t)n_rows * ldo * 4 < ((int64_t)1 << 32) && !task_env("VQGNN_SPMM_FAR", 0);
+          (int64_t)n_rows * ldo * 4 < ((int64_t)1 << 32) && !path_env("VQGNN_SPMM_FAR", 0);
   if (*near) {
     a.ubase = reinterpret_cast<const char*>(lo);
     a.span = (uint32_t)(hi - lo);
@@ -869,7 +865,7 @@ static int task_setup(TaskArgs& a, const int32_t* rowptr, int32_t n_rows, int32_
     a.ldx2b = (uint32_t)(a.ldx2 * 4);
     a.ldob = (uint32_t)(ldo * 4);
   }
-  a.dbg = task_env("VQGNN_TASK_DBG", 0);
+  a.dbg = VQGNN_KNOB("VQGNN_TASK_DBG", 0);
   return VQGNN_OK;
 }
 
@@ -902,12 +898,12 @@ static void task_launch(const TaskArgs& a, bool near, hipStream_t s) {
     const int F4 = a.F / 4;
     // lanes per task: VQGNN_TASK_G (8, 16 or 32; default 32); pieces per lane
     // so that one column tile covers min(F, 128) floats
-    int G = task_env("VQGNN_TASK_G", 32);
+    int G = VQGNN_KNOB("VQGNN_TASK_G", 32);
     G = G >= 32 ? 32 : (G >= 16 ? 16 : 8);
     int nc = 1;
     while (nc * G < F4 && nc * G * 4 < 128) nc *= 2;      // 4*G*nc floats <= 128
     const int tiles = (F4 + nc * G - 1) / (nc * G);
-    const int Ue = task_env("VQGNN_TASK_U", 16);
+    const int Ue = VQGNN_KNOB("VQGNN_TASK_U", 16);
     const int U = Ue >= 16 ? 16 : (Ue >= 8 ? 8 : (Ue >= 4 ? 4 : 2));
     if (G == 8) {
       if (nc == 1) launch_task_u<8, 1, GAT>(a, tiles, U, near, s);

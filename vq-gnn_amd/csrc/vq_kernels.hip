@@ -764,11 +764,6 @@ __device__ __forceinline__ unsigned long long to_fixed(float v, int shift) {
   return (unsigned long long)(long long)t;
 }
 
-static int env_int_vq(const char* name, int dflt) {
-  const char* v = getenv(name);
-  return v && *v ? atoi(v) : dflt;
-}
-
 // Waves per workgroup: 8, or 16 where the LDS footprint (a large codebook,
 // or the fused EMA slab of M = 1024) leaves one workgroup per CU — the
 // choice with more resident waves per CU (assign_geom).
@@ -840,7 +835,7 @@ static const void* flt_fn(bool fused, int wm, int wv, bool co) {
 // the filtered path serves W <= 8 (VQGNN_ASSIGN_EXACT=1: the exact f32 sweep
 // for every W, a measurement and cross-check knob)
 static bool use_filter(int W) {
-  static const int exact_env = env_int_vq("VQGNN_ASSIGN_EXACT", 0);
+  static const int exact_env = path_env("VQGNN_ASSIGN_EXACT", 0);
   return W <= 8 && !exact_env;
 }
 
@@ -912,7 +907,7 @@ static AssignGeom assign_geom(int B, int nb, int M, int W) {
     if (!g.fused)
       while (c > 32 && flt_lds_bytes(c) > kLdsBudget) c = (c / 2 + 31) / 32 * 32;
     // measurement knob: a smaller staged chunk of the filter (multiple of 32)
-    const int fenv = env_int_vq("VQGNN_FLT_CHUNK", 0);
+    const int fenv = VQGNN_KNOB("VQGNN_FLT_CHUNK", 0);
     if (!g.fused && fenv >= 32 && fenv < c) c = fenv / 32 * 32;
     g.chunk = c;
   } else if (cb_lds_bytes(g.kc, g.mpad) + acc <= kLdsBudget) {
@@ -925,7 +920,7 @@ static AssignGeom assign_geom(int B, int nb, int M, int W) {
     while (c > 16 && cb_lds_bytes(g.kc, c) > kLdsBudget) c = (c / 2 + 15) / 16 * 16;
     // measurement knob: a smaller staged chunk (more resident workgroups,
     // the codebook restaged once per chunk and row block)
-    const int cenv = env_int_vq("VQGNN_ASG_CHUNK", 0);
+    const int cenv = VQGNN_KNOB("VQGNN_ASG_CHUNK", 0);
     if (cenv >= 32 && cenv < c) c = cenv / 32 * 32;
     g.chunk = c;
   }
@@ -936,14 +931,14 @@ static AssignGeom assign_geom(int B, int nb, int M, int W) {
   // several chunks: chunk-outer passes, one launch per chunk, unless
   // VQGNN_ASG_CO=0 (chunk-inner: every chunk restaged for every 1,024-row
   // iteration).  A fused launch holds its whole codebook in one chunk.
-  g.co = g.filter && !g.fused && g.chunk < M && env_int_vq("VQGNN_ASG_CO", 1) != 0;
+  g.co = g.filter && !g.fused && g.chunk < M && VQGNN_KNOB("VQGNN_ASG_CO", 1) != 0;
   // waves per workgroup: the choice with more resident waves per CU (ties: 8).
   // (10-wave filter workgroups -- 20 resident waves at 5 per SIMD instead of
   // 16 -- measured 1.9x slower at arxiv update, 188 vs 98 us, and 1.4x at
   // feature_update: profiles/r04d_assign_waves_ab.txt)
   const int cap8 = assign_capacity(g.kc, g.fused, wm, lds + scr8, 8, g.filter, g.co);
   const int cap16 = assign_capacity(g.kc, g.fused, wm, lds + 2 * scr8, 16, g.filter, g.co);
-  const int wenv = env_int_vq("VQGNN_ASG_WAVES", 0);
+  const int wenv = VQGNN_KNOB("VQGNN_ASG_WAVES", 0);
   g.wv = cap16 * 16 > cap8 * 8 ? 16 : 8;
   if (wenv == 8 || wenv == 16) g.wv = wenv;
   g.lds = lds + (g.wv == 16 ? 2 * scr8 : scr8);
@@ -958,7 +953,7 @@ static AssignGeom assign_geom(int B, int nb, int M, int W) {
     const size_t ef = (size_t)(g.chunk + kFltSlack) * 32;
     const int wmv = wm;
     const int cap = g.wv == 16 ? cap16 : cap8;
-    const int env = env_int_vq("VQGNN_FLT_ELDS", -1);
+    const int env = VQGNN_KNOB("VQGNN_FLT_ELDS", -1);
     if (g.lds + ef <= kLdsBudget && env != 0 &&
         (env == 1 || (g.chunk <= 512 &&
                       assign_capacity(g.kc, g.fused, wmv, g.lds + ef, g.wv, true, g.co) >= cap))) {
@@ -971,7 +966,7 @@ static AssignGeom assign_geom(int B, int nb, int M, int W) {
   const int row_blocks = (B + rows_per_iter - 1) / rows_per_iter;
   // one full round of resident workgroups: parts x nb <= what the device
   // holds at once (every part has the same row count, so no tail round)
-  const int target = env_int_vq("VQGNN_ASG_TARGET", g.wv == 16 ? cap16 : cap8);
+  const int target = VQGNN_KNOB("VQGNN_ASG_TARGET", g.wv == 16 ? cap16 : cap8);
   int parts = target / nb;
   if (parts < 1) parts = 1;
   if (parts > row_blocks) parts = row_blocks;
@@ -2653,9 +2648,9 @@ static int launch_assign(const float* X, int64_t ldx, const float* G, int64_t ld
     else if (wm == 2) VQ_LAUNCH_WV(FU, 2);                                                    \
     else VQ_LAUNCH_WV(FU, 0);                                                                 \
   } while (0)
-  // codewords swept per chunk: all (VQGNN_ASSIGN_MSWEEP: a profiling knob that
-  // shortens the sweep and breaks the results; never set outside measurements)
-  static const int msw_env = env_int_vq("VQGNN_ASSIGN_MSWEEP", -1);
+  // codewords swept per chunk: all (VQGNN_ASSIGN_MSWEEP, experiments builds
+  // only: a profiling knob that shortens the sweep and breaks the results)
+  static const int msw_env = VQGNN_KNOB("VQGNN_ASSIGN_MSWEEP", -1);
   const int m_sweep = msw_env >= 0 ? msw_env : (1 << 30);
   if (fused) VQ_LAUNCH_WM(true); else VQ_LAUNCH_WM(false);
 #undef VQ_LAUNCH_WM
@@ -2682,7 +2677,7 @@ static int launch_ema_tail(const float* X, int64_t ldx, const float* G, int64_t 
     hipLaunchKernelGGL(vq_ema_partial_kernel, dim3(wgs), dim3(kAssignThreads), acc_bytes, s, X,
                        ldx, G, ldg, B, nb, D, M, W, coef, grad_scale, idx32, parts,
                        g.rows_per_part, 1, sh.f, sh.g);
-  } else if (!env_int_vq("VQGNN_EMA_GLOBAL", 0)) {
+  } else if (!path_env("VQGNN_EMA_GLOBAL", 0)) {
     // codeword ranges whose slab fits kSplitSlab; enough row parts for
     // about two workgroups per CU
     const size_t slot_bytes = (size_t)(W + 1) * sizeof(unsigned long long);
@@ -2741,7 +2736,7 @@ static int launch_filter(const float* X, int64_t ldx, const float* G, int64_t ld
   const int wm = flt_mode(W, D, ldx, ldg, X, G);
   if (want_ema && !ema_zeroed)
     (void)hipMemsetAsync(parts, 0, (size_t)nb * M * (W + 1) * sizeof(unsigned long long), s);
-  static const int msw_env = env_int_vq("VQGNN_ASSIGN_MSWEEP", -1);
+  static const int msw_env = VQGNN_KNOB("VQGNN_ASSIGN_MSWEEP", -1);
   const int m_sweep = msw_env >= 0 ? msw_env : (1 << 30);
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   timing_events(&ev0, &ev1);
@@ -2834,6 +2829,10 @@ extern "C" int32_t vqgnn_vq_assign_bn_supported(int32_t B, int32_t nb, int32_t D
       !use_filter(W))
     return 0;
   const AssignGeom g = assign_geom(B, nb, M, W);
+  // a chunked codebook (chunk-outer passes, one launch each) is not folded:
+  // its later passes would read the coef the first pass wrote, a combination
+  // no parity test pins; the separate finalize serves it
+  if (g.co) return 0;
   const CascadeGeom cg = cascade_geom(B);
   // the fold's scratch lives in the codebook planes' LDS before they are staged
   return bn_fold_scratch(cg.nsb, cg.lp, W) <= (size_t)kFltBytesPerCode * (g.chunk + kFltSlack)
@@ -2987,7 +2986,7 @@ int ema_fin_prepare(const vqgnn_ema_finalize_args* a, EmaFin* f) {
   e.rv_g = a->rv_g;
   e.bad_init = a->bad_init;
   // M >= 1024: the per-codeword half runs in a second, wider launch
-  e.split = a->M >= 1024 && !env_int_vq("VQGNN_EMA_FIN_ONE", 0);
+  e.split = a->M >= 1024 && !VQGNN_KNOB("VQGNN_EMA_FIN_ONE", 0);
   return VQGNN_OK;
 }
 

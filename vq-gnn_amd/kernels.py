@@ -488,10 +488,12 @@ def spmm_codebook(rowptr, n_rows, nnz, X, F, B, codes, emb_out, D, plan_cb, out=
     from TaskPlan.with_codebook_source.  Equals spmm(..., X2=gather_codewords
     (subset, B, codes, emb_out, D)[0], B=B).
 
-    finalize: an EMA finalize's operands (vq_ema_finalize's positional
-    arguments and keywords, as VQBank.take_fused_finalize returns them) run
-    inside the SpMM's fix-up launch (vqgnn_spmm_task_cb_fin): the same
-    results as this call followed by vq_ema_finalize, one launch fewer."""
+    finalize: a pending EMA finalize (VQBank.take_fused_finalize's handle, or
+    vq_ema_finalize's (args, kw)) run inside the SpMM's fix-up launch
+    (vqgnn_spmm_task_cb_fin): the same results as this call followed by
+    vq_ema_finalize, one launch fewer.  A handle is retired (done()) only
+    once the launch is queued: if this call raises, the bank keeps the
+    finalize pending for finish_update()."""
     require_gpu(X, "spmm_codebook")
     if getattr(plan_cb, "cb_B", None) != int(B):
         raise ValueError("spmm_codebook: plan_cb must come from TaskPlan.with_codebook_source "
@@ -519,10 +521,12 @@ def spmm_codebook(rowptr, n_rows, nnz, X, F, B, codes, emb_out, D, plan_cb, out=
     if finalize is None:
         check(L.vqgnn_spmm_task_cb(*args, stream_ptr()), "spmm_task_cb")
     else:
-        fin_args, fin_kw = finalize
+        fin_args, fin_kw = getattr(finalize, "operands", finalize)
         rec = ema_finalize_args(*fin_args, **fin_kw)
         check(L.vqgnn_spmm_task_cb_fin(*args, ctypes.byref(rec), stream_ptr()),
               "spmm_task_cb_fin")
+        if hasattr(finalize, "done"):
+            finalize.done()
     return out
 
 

@@ -40,6 +40,25 @@ from .kernels import (BN_CONTIG, BN_EVAL, BN_EVAL_INIT, BN_FP64, BN_TRAIN, BN_TR
 STRICT_BAD_INIT = os.environ.get("VQGNN_DEFER_BAD_INIT", "0") != "1"
 
 
+class FusedFinalize:
+    """A pending EMA finalize handed to an aggregation
+    (VQBank.take_fused_finalize): ``operands`` = (args, kw) of
+    kernels.vq_ema_finalize for the fused fix-up launch; done() -- called by
+    kernels.spmm_codebook once that launch is queued, idempotent -- retires it
+    from the bank.  Until then the bank keeps it pending."""
+
+    def __init__(self, bank, entry):
+        self._bank, self._entry = bank, entry
+        self.operands = (entry[1], entry[2])
+
+    def done(self):
+        bank = self._bank
+        if bank._pending_finalize is self._entry:
+            bank._pending_finalize = None
+            bank._clean(*self._entry[3])
+            bank._finish()
+
+
 class VQBank(nn.Module):
     """Packed EMA-VQ state of ``nb`` branches.  Buffers are non-persistent: the
     per-branch ``VectorQuantizerEMA`` modules own the state_dict entries."""
@@ -325,20 +344,16 @@ class VQBank(nn.Module):
     def take_fused_finalize(self):
         """Hand the pending finalize of an update(defer=True) to the caller's
         next aggregation, which runs it inside its fix-up launch
-        (kernels.spmm_codebook(finalize=...), include/vqgnn.h §6b):
-        -> ((args, kw), done) -- call done() once that aggregation is queued
-        -- or None when nothing is pending, or when the finalize must wait for
-        the multi-GPU all-reduce of its statistics (finish_update() then)."""
+        (kernels.spmm_codebook(finalize=handle), include/vqgnn.h §6b)
+        -> a FusedFinalize handle, or None when nothing is pending or when the
+        finalize must wait for the multi-GPU all-reduce of its statistics
+        (finish_update() then).  The finalize stays pending until the
+        aggregation has queued it (handle.done(), which spmm_codebook calls):
+        an aggregation that raises first leaves it to finish_update()."""
         p = self._pending_finalize
         if p is None or p[0] is not None:
             return None
-        self._pending_finalize = None
-        _, fin_args, fin_kw, clean = p
-
-        def done():
-            self._clean(*clean)
-            self._finish()
-        return (fin_args, fin_kw), done
+        return FusedFinalize(self, p)
 
     def update(self, X, G, b0, nbr, training, idx_out=None, codes=None, batch_idx=None,
                defer=False):
