@@ -345,15 +345,20 @@ int vqgnn_spmm_task(const int32_t* rowptr, int32_t n_rows, int32_t n_cols, int64
  *    vqgnn_spmm_task over [X ; gather_codewords(...)]: the same output.
  *    vqgnn_spmm_task_records_cb: copy of a plan's records (vqgnn_spmm_task_plan)
  *      rewritten in place: a column j >= B becomes B + subset[j] (the node
- *      whose codes give the row); requires B + n_nodes <= 2^26.
+ *      whose codes give the row); requires B + n_nodes <= 2^26.  A column
+ *      past the subset or a node outside [0, n_nodes) gets weight 0 (its
+ *      code reads as 0): it adds 0 x codeword 0 -- the zero row
+ *      vqgnn_gather_codewords writes for it, for a finite codebook.
  *    vqgnn_spmm_task_cb: out = A @ x_in for the rewritten records; codes
- *      [n_nodes][ldc] int16 (c_indices, every code in [0, M)), codewords =
+ *      [n_nodes][ldc] int16 (c_indices; a code outside [0, M) reads the
+ *      image's zero row, gather's zero row), codewords =
  *      emb_out [n_branches][M][ldw] (branch stride bstride, 16-byte aligned
  *      rows); the F / D code columns read must not exceed n_branches; D a
- *      multiple of 4; the image of a column tile of 4G columns is M x 16G
- *      bytes <= 160 KiB with 4G dividing F (G = 32: M <= 320 at F % 128 ==
- *      0; G = 16: M <= 640 at F % 64 == 0; G = 8: M <= 1,280 at F % 32 ==
- *      0), vqgnn_spmm_task_cb_lds; X and out on the 32-bit near path.  Any
+ *      multiple of 4; the image of a column tile of 4G columns is (M + 1) x
+ *      16G bytes (the codewords and a zero row) <= 160 KiB with 4G dividing
+ *      F (G = 32: M <= 319 at F % 128 == 0; G = 16: M <= 639 at F % 64 ==
+ *      0; G = 8: M <= 1,279 at F % 32 == 0), vqgnn_spmm_task_cb_lds; X and
+ *      out on the 32-bit near path.  Any
  *      other shape: VQGNN_ERR_INVALID (use vqgnn_gather_codewords +
  *      vqgnn_spmm_task, which has a 64-bit path).
  *    vqgnn_spmm_task_cb_supported: 1 iff vqgnn_spmm_task_cb accepts this
@@ -362,7 +367,7 @@ int vqgnn_spmm_task(const int32_t* rowptr, int32_t n_rows, int32_t n_cols, int64
  *    Speed: each column tile walks every edge once, so the narrow tiles (G <
  *      32) are slower than gather + vqgnn_spmm_task on arxiv-like batches;
  *      the package's host layer uses this entry only when
- *      vqgnn_spmm_task_cb_lds(M) == M * 512 (the 128-column tile fits).
+ *      vqgnn_spmm_task_cb_lds(M) == (M + 1) * 512 (the 128-column tile fits).
  *    vqgnn_spmm_task_cb_fin: vqgnn_spmm_task_cb, then the EMA finalize of
  *      *fin (§4, the update whose statistics the walk's codebook predates:
  *      models.py:181-185 runs it after the aggregation) inside the fix-up

@@ -6,6 +6,7 @@
 #    with -DVQGNN_EXPERIMENTS: its measurement knobs (VQGNN_TASK_U/G,
 #    VQGNN_ASG_*, VQGNN_ASSIGN_MSWEEP, VQGNN_TASK_DBG, ...) read the
 #    environment there and only there -- the default library ignores them.
+#    EXTRA_FLAGS: more hipcc flags for the replaced file.
 set -e
 cd "$(dirname "$0")/../vq-gnn_amd/csrc"
 name=$1; src=$2; repl=$3
@@ -17,7 +18,7 @@ objs=""
 for f in $(sed -n 's/^SRCS := //p;s/^         //p' Makefile | tr ' ' '\n' | grep hip); do
   if [ "$f" = "$src" ]; then
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++20 -ffp-contract=off -Wall \
-      -Wno-unused-function -munsafe-fp-atomics -DVQGNN_EXPERIMENTS -I$PWD -c $tmp/$src -o $tmp/${src%.hip}.o
+      -Wno-unused-function -munsafe-fp-atomics -DVQGNN_EXPERIMENTS $EXTRA_FLAGS -I$PWD -c $tmp/$src -o $tmp/${src%.hip}.o
     objs="$objs $tmp/${src%.hip}.o"
   else
     objs="$objs ../lib/obj/${f%.hip}.o"

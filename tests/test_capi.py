@@ -92,7 +92,8 @@ def test_codebook_reads_bounded_by_its_branch_count():
     assert h.vqgnn_spmm_task_cb_supported(100, 50, 128, 128, 128, 1000, 32, 32, 1281, 4) == 0
     assert h.vqgnn_spmm_task_cb_supported(100, 50, 128, 128, 128, 1000, 32, 32, 1024, 4) == 1
     assert h.vqgnn_spmm_task_cb_supported(100, 50, 96, 96, 96, 1000, 24, 24, 640, 4) == 1  # G = 8
-    assert h.vqgnn_spmm_task_cb_lds(256) == 256 * 512 and h.vqgnn_spmm_task_cb_lds(1024) == 1024 * 128
+    # M codeword rows + the zero row (codes >= M read it)
+    assert h.vqgnn_spmm_task_cb_lds(256) == 257 * 512 and h.vqgnn_spmm_task_cb_lds(1024) == 1025 * 128
     assert h.vqgnn_spmm_task_cb_supported(1 << 24, 50, 128, 128, 128, 1000, 32, 32, 256, 4) == 0
     assert h.vqgnn_spmm_task_cb_supported(100, 5_000_000, 128, 128, 128, 1000, 32, 32, 256,
                                           4) == 0          # X past the 2 GiB near range
@@ -101,11 +102,11 @@ def test_codebook_reads_bounded_by_its_branch_count():
 
 def test_codebook_source_preferred_only_at_full_width():
     """The host layer takes the codebook source only where the whole 128-column
-    tile's image fits (M <= 320); narrower tiles lose to the gather (DESIGN
+    tile's image fits (M <= 319 with its zero row); narrower tiles lose to the gather (DESIGN
     4.2d, profiles/r05_cb_m1024_probe.txt)."""
     from vq_gnn_amd import kernels
-    assert kernels.codebook_source_preferred(256) and kernels.codebook_source_preferred(320)
-    assert not kernels.codebook_source_preferred(321)
+    assert kernels.codebook_source_preferred(256) and kernels.codebook_source_preferred(319)
+    assert not kernels.codebook_source_preferred(320)
     assert not kernels.codebook_source_preferred(1024)
 
 
@@ -176,3 +177,53 @@ def test_bn_fold_refuses_chunked_codebooks():
     h = L.lib()
     assert h.vqgnn_vq_assign_bn_supported(30_000, 13, 4, 4096, 8) == 0
     assert h.vqgnn_vq_assign_bn_supported(84_670, 32, 4, 256, 8) == 1
+
+
+def test_codebook_source_query_agrees_with_the_entry(monkeypatch):
+    """the supported query refuses what the entry would refuse --
+    VQGNN_SPMM_FAR (the entry needs the near path) -- and codebook_source_ok
+    checks the codeword rows' layout the entry checks."""
+    import torch
+    from vq_gnn_amd import kernels
+    h = L.lib()
+    args = (100, 50, 128, 128, 128, 1000, 32, 32, 256, 4)
+    assert h.vqgnn_spmm_task_cb_supported(*args) == 1
+    monkeypatch.setenv("VQGNN_SPMM_FAR", "1")
+    assert h.vqgnn_spmm_task_cb_supported(*args) == 0
+    monkeypatch.delenv("VQGNN_SPMM_FAR")
+    X = torch.zeros(50, 128)
+    good = torch.zeros(32, 256, 8)
+    assert kernels.codebook_source_ok(X, 128, 256, 4, n_rows=100, emb_out=good)
+    odd = torch.zeros(32, 256, 10)[:, :, :6]          # ldw = 10: not a multiple of 4
+    assert not kernels.codebook_source_ok(X, 128, 256, 4, n_rows=100, emb_out=odd)
+
+
+def test_assign_kernels_have_no_packed_fp32():
+    """The assign kernels are built without SLP vectorization (csrc/Makefile):
+    no packed FP32 instruction in any vq_filter_kernel / vq_assign_kernel
+    instance, so the resolve's exact candidate chains are v_fma_f32 chains in
+    every instance (round 5's nondeterministic variant ran them packed;
+    DESIGN.md 4.1).  Reads the gfx950 code object of the built library."""
+    import subprocess
+    import tempfile
+    import pytest
+    llvm = "/opt/rocm/lib/llvm/bin"
+    obj = os.path.join(ROOT, "vq-gnn_amd", "lib", "obj", "vq_kernels.o")
+    if not (os.path.exists(obj) and os.path.exists(os.path.join(llvm, "llvm-objdump"))):
+        pytest.skip("needs the built object and the ROCm LLVM tools")
+    with tempfile.TemporaryDirectory() as d:
+        fat, dev = os.path.join(d, "fat.bin"), os.path.join(d, "dev.o")
+        subprocess.run([f"{llvm}/llvm-objcopy", "--dump-section", f".hip_fatbin={fat}", obj,
+                        os.path.join(d, "host.o")], check=True)
+        subprocess.run([f"{llvm}/clang-offload-bundler", "--unbundle", "--type=o",
+                        "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--input={fat}",
+                        f"--output={dev}"], check=True)
+        asm = subprocess.run([f"{llvm}/llvm-objdump", "-d", dev], check=True,
+                             capture_output=True, text=True).stdout
+    funcs = re.split(r"\n(?=[0-9a-f]+ <)", asm)
+    assign = [f for f in funcs if "vq_filter_kernel" in f.split("\n", 1)[0] or
+              "vq_assign_kernel" in f.split("\n", 1)[0]]
+    assert len(assign) >= 18
+    for f in assign:
+        packed = re.findall(r"\bv_pk_(?:fma|mul|add)_f32\b", f)
+        assert not packed, (f.split("\n", 1)[0][:80], len(packed))

@@ -233,10 +233,10 @@ def test_codebook_source_arxiv_batch_and_strides():
     _check(out, b.rowptr, b.col, b.val, xin)
 
 
-@pytest.mark.parametrize("F,M,G", [(128, 512, 16), (128, 1024, 8), (64, 640, 16), (96, 1280, 8),
+@pytest.mark.parametrize("F,M,G", [(128, 512, 16), (128, 1024, 8), (64, 639, 16), (96, 1279, 8),
                                    (32, 300, 8)])
 def test_codebook_source_narrow_tiles(F, M, G):
-    """Codebooks too large for a 128-column image (M > 320) walk narrower
+    """Codebooks too large for a 128-column image (M > 319) walk narrower
     column tiles of 4G columns (include/vqgnn.h §6b; reddit / arxiv-GAT use M =
     1,024): bit-identical to gather + two-source SpMM and within 1e-5 of the
     fp64 sum, hub rows and empty rows included."""
@@ -244,8 +244,8 @@ def test_codebook_source_narrow_tiles(F, M, G):
     B, n, N, D = 600, 1500, 4000, 4
     a, rowptr, col, val, subset, codes, emb_out, X, plan = _cb_case(rng, B, n, N, F, M, D)
     assert kernels.codebook_source_ok(X, F, M, D, codes=codes, n_rows=n, n_branches=F // D)
-    if F % 128 == 0 or M > 320:        # (the query gives the widest tile M alone allows)
-        assert kernels.lib().vqgnn_spmm_task_cb_lds(M) == M * 16 * G
+    if F % 128 == 0 or M > 319:        # (the query gives the widest tile M alone allows)
+        assert kernels.lib().vqgnn_spmm_task_cb_lds(M) == (M + 1) * 16 * G   # + the zero row
     xf, _ = kernels.gather_codewords(subset, B, codes, emb_out, D)
     ref = kernels.spmm(a.rowptr, a.col, a.value, n, a.nnz(), X, F, X2=xf, B=B, plan=plan)
     out = kernels.spmm_codebook(a.rowptr, n, a.nnz(), X, F, B, codes, emb_out, D,
@@ -311,6 +311,27 @@ def test_gather_bad_nodes_and_codes_read_nothing():
                 assert torch.equal(seg, e[br, c, :D])
             else:
                 assert torch.count_nonzero(seg) == 0
+
+
+def test_codebook_source_bad_nodes_and_codes_add_nothing():
+    """through spmm_codebook an out-of-range node (weight 0 in the
+    rewritten records) and a code outside [0, M) (the LDS image's zero row)
+    contribute nothing -- the same output as gather_codewords (zero rows for
+    both) + the two-source SpMM."""
+    rng = np.random.default_rng(77)
+    F, M, D, N, B, n = 128, 256, 4, 3000, 300, 800
+    a, rowptr, col, val, subset, codes, emb_out, X, plan = _cb_case(rng, B, n, N, F, M, D)
+    subset[B + 3] = N + 7                 # a node past the codes
+    subset[B + 11] = -5                   # a negative node
+    used = subset[B + 20:B + 40]
+    codes[used[:10], 2] = M + 9           # codes past the codebook
+    codes[used[10:], 5] = -3
+    xf, _ = kernels.gather_codewords(subset, B, codes, emb_out, D)
+    ref = kernels.spmm(a.rowptr, a.col, a.value, n, a.nnz(), X, F, X2=xf, B=B, plan=plan)
+    got = kernels.spmm_codebook(a.rowptr, n, a.nnz(), X, F, B, codes, emb_out, D,
+                                a.plan_codebook(B, subset, N))
+    assert torch.equal(ref, got)
+    assert torch.isfinite(got).all()
 
 
 def test_codebook_plan_cache_follows_the_subset():

@@ -89,14 +89,17 @@ def test_assign_repeat_launches_identical(M, B):
     assert not bad, f"(launch, mismatching rows): {bad}"
 
 
-@pytest.mark.parametrize("M,nb", [(256, 32), (1024, 32), (4096, 13)])
-def test_assign_repeat_launches_many_branches(M, nb):
+@pytest.mark.parametrize("M,nb,D", [(256, 32, 4), (1024, 32, 4), (4096, 13, 4), (1024, 32, 2),
+                                    (256, 32, 2)])
+def test_assign_repeat_launches_many_branches(M, nb, D):
     """The shapes where round 5's packed-f32 resolve variant returned different
     indices on repeated launches (13-32 branches x 30,000 rows, M = 256 /
     1,024 / 4,096; profiles/r05_pipe_packed_determinism.txt, DESIGN.md 4.1
     "Nondeterminism"): every one of 4 launches of the shipped assign equals
-    the oracle, branch by branch."""
-    D, W, B = 4, 8, 30_000
+    the oracle, branch by branch.  D = 2 runs the general filter instance
+    (WM 0), whose resolve the compiler used to pack (v_pk_fma_f32 over two
+    candidates) until the library was built without SLP vectorization."""
+    W, B = 2 * D, 30_000
     g = torch.Generator().manual_seed(M + nb)
     X = torch.randn(B, nb * D, generator=g)
     G = torch.randn(B, nb * D, generator=g) * 1e-3

@@ -60,7 +60,8 @@ class CodebookInput(NamedTuple):
                                            codes=self.codes,
                                            n_rows=n_rows if n_rows is not None
                                            else self.subset.numel(),
-                                           n_branches=self.emb_out.shape[0]))
+                                           n_branches=self.emb_out.shape[0],
+                                           emb_out=self.emb_out))
 
     def gathered(self):
         """The GatheredInput form (x_first_order materialised by the gather)."""

@@ -41,11 +41,14 @@ constexpr uint32_t kColMask = (1u << 26) - 1;
 constexpr uint32_t kEndBit = 1u << 31;
 constexpr int kSkipShift = 26;
 constexpr uint32_t kSkipEsc = 31;
+constexpr uint32_t kHeadBit = 1u << 31;   // task_row: the first row began in an earlier task
+constexpr int kRowMask = 0x7fffffff;
 
 struct TaskArgs {
   const int2* rec;          // [nnz] (col | skip << 26 | end << 31, weight bits)
   const int32_t* task_start;  // [ntasks + 1] first edge of each task (row-aligned unless split)
-  const int32_t* task_row;    // [ntasks] row containing the task's first edge
+  const int32_t* task_row;    // [ntasks] row containing the task's first edge (| kHeadBit:
+                              // that row began in an earlier task)
   const int32_t* jobs;        // fixup: [ntasks][3] slots, n_jobs used (row, first task,
                               // last task), then [n_rows] slots, n_empty used (empty rows)
   int n_jobs, n_empty;
@@ -111,7 +114,8 @@ __global__ void task_records_kernel(const int32_t* __restrict__ col, const float
 // codebook-source records: a column j >= B becomes B + nodes[j] (the node
 // whose codes give the row); flags and weight kept.  A column past the subset
 // or a node outside [0, n_nodes) becomes B + n_nodes, past the codes' buffer
-// range: its code reads as 0 with no memory access (invalid input, bounded)
+// range (its code reads as 0 with no memory access), with weight 0: it adds
+// 0 x codeword 0, the zero row gather_codewords writes for it (invalid input)
 __global__ void task_remap_cb_kernel(int2* __restrict__ rec, int nnz, int B, int n_cols,
                                      const int64_t* __restrict__ nodes, int64_t n_nodes) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
@@ -120,7 +124,10 @@ __global__ void task_remap_cb_kernel(int2* __restrict__ rec, int nnz, int B, int
   const uint32_t j = x & kColMask;
   if ((int)j >= B) {
     int64_t node = (int)j < n_cols ? nodes[j] : n_nodes;
-    if (node < 0 || node > n_nodes) node = n_nodes;
+    if (node < 0 || node >= n_nodes) {      // invalid: no contribution (gather_codewords' zero row)
+      node = n_nodes;
+      rec[e].y = 0;
+    }
     rec[e].x = (int)((x & ~kColMask) | ((uint32_t)B + (uint32_t)node));
   }
 }
@@ -154,7 +161,17 @@ __global__ void task_first_row_kernel(const int32_t* __restrict__ rowptr, int n_
     if (rs < st && re - rs <= snap) st = re;
   }
   task_start[t] = st;
-  if (t < ntasks) task_row[t] = st < nnz ? upper_bound_i32(rowptr, n_rows, st) - 1 : n_rows - 1;
+  if (t < ntasks) {
+    // bit 31: the task's first row began in an earlier task (its partial is a
+    // head for the fix-up), decided here so the walk needs no rowptr read
+    int r = n_rows - 1;
+    uint32_t head = 0;
+    if (st < nnz) {
+      r = upper_bound_i32(rowptr, n_rows, st) - 1;
+      head = rowptr[r] < st ? kHeadBit : 0u;
+    }
+    task_row[t] = (int32_t)((uint32_t)r | head);
+  }
 }
 
 // Fix-up jobs: a row cut by task boundaries (its first edge in task ts, its
@@ -168,7 +185,7 @@ __global__ void task_jobs_kernel(const int32_t* __restrict__ rowptr, int n_rows,
   const int nnz = task_start[ntasks];
   if (x < ntasks && task_start[x] < nnz) {
     const int e0 = task_start[x];
-    const int r = task_row[x];
+    const int r = task_row[x] & kRowMask;
     const int rs = rowptr[r], re = rowptr[r + 1];
     if (rs < e0 && re <= task_start[x + 1]) {
       const int ts = upper_bound_i32(task_start, ntasks, rs) - 1;
@@ -208,9 +225,6 @@ __device__ __forceinline__ void group_bcast(int x, int (&out)[sizeof...(Us)],
   ((out[Us] = __builtin_amdgcn_ds_swizzle(x, AND | (Us << 5))), ...);
 }
 
-// G lanes per task (64 / G tasks per wave), NC float4 pieces per lane (piece
-// i of lane k is float4 column G*i + k: a column tile of 4*G*NC floats), U
-// edges per block
 // GAT coefficient of one edge (convs.py:209-264, vq_softmax.py:33-57, the
 // op order of gat_coef_kernel): exp(leaky(al[j] + ar[i])) * w, al / ar
 // already divided by s per node as the reference does (convs.py:209-211)
@@ -220,28 +234,58 @@ __device__ __forceinline__ float gat_edge_coef(const TaskArgs& a, int e, uint32_
   return __fmul_rn(expf(x), w);
 }
 
-// PART (near path): the last column tile is partial (F/4 not a multiple of
-// G*NC): its lanes past F load nothing (an offset past the buffer range
-// returns 0 without a memory access) instead of reading the next row
+// The four plan words a wave's walk starts from (its first task's first edge,
+// and this lane's task's first / end edge and first row), read together --
+// independent loads, one memory round trip -- and, by the persistent kernel,
+// one unit ahead of the walk that uses them
+struct UnitInfo {
+  int wbase, e0, e1, row;
+};
+
+template <int G>
+__device__ __forceinline__ UnitInfo unit_info(const TaskArgs& a, int wv, int nnz) {
+  constexpr int TPW = 64 / G;
+  const int t = wv * TPW + (int)((threadIdx.x & 63) / G);
+  const int tw = min(wv * TPW, a.ntasks);           // task_start has ntasks + 1 entries
+  const int tc = min(t, a.ntasks - 1);
+  UnitInfo u;
+  u.wbase = a.task_start[tw];
+  const int s0 = a.task_start[max(tc, 0)], s1 = a.task_start[max(tc, 0) + 1];
+  const int rw = a.task_row[max(tc, 0)];
+  const bool tv = t < a.ntasks;
+  u.e0 = tv ? s0 : nnz;
+  u.e1 = tv ? s1 : nnz;
+  u.row = tv ? rw : 0;
+  return u;
+}
+
+// the edges a call covers: a call over the first n_rows rows of a larger CSR
+// (the backward's transpose restricted to batch rows) covers [0, rowptr[n_rows])
+__device__ __forceinline__ int call_nnz(const TaskArgs& a) { return min(a.nnz, a.rowptr[a.n_rows]); }
+
+// G lanes per task (64 / G tasks per wave), NC float4 pieces per lane (piece
+// i of lane k is float4 column G*i + k: a column tile of 4*G*NC floats), U
+// edges per block.  PART (near path): the last column tile is partial (F/4
+// not a multiple of G*NC): its lanes past F load nothing (an offset past the
+// buffer range returns 0 without a memory access) instead of reading the
+// next row
 template <int G, int NC, int U, bool FAR, bool GAT, bool PART, bool CB = false>
-__device__ __forceinline__ void task_walk(const TaskArgs& a, int wv, int nwaves) {
+__device__ __forceinline__ void task_walk(const TaskArgs& a, int wv, int nwaves, const UnitInfo& ui,
+                                          int nnz) {
   static_assert(!CB || (NC == 1 && !FAR && !GAT && !PART), "CB: the near shape, one piece per lane");
   constexpr int TPW = 64 / G;
   const int lane = threadIdx.x & 63;
   const int g = lane / G, k = lane % G;
   const int t = wv * TPW + g;
-  // a call over the first n_rows rows of a larger CSR (the backward's
-  // transpose restricted to batch rows) covers edges [0, rowptr[n_rows])
-  const int nnz = min(a.nnz, a.rowptr[a.n_rows]);
   if (wv >= nwaves || wv * TPW >= a.ntasks) return;
   // the wave's records are addressed from its first task's first edge: 32-bit
   // buffer offsets cover any nnz < 2^31 (a wave spans at most 64 tasks)
-  const int wbase = a.task_start[wv * TPW];
+  const int wbase = __builtin_amdgcn_readfirstlane(ui.wbase);
   if (wbase >= nnz) return;
   const bool tv = t < a.ntasks;
-  const int e0 = tv ? min(a.task_start[t], nnz) : nnz;
+  const int e0 = tv ? min(ui.e0, nnz) : nnz;
   const bool valid = e0 < nnz;
-  const int e1 = valid ? min(nnz, a.task_start[t + 1]) : e0;
+  const int e1 = valid ? min(nnz, ui.e1) : e0;
 
   const int F4 = a.F >> 2;
   const int c4base = (int)blockIdx.y * NC * G + k;   // this lane's first float4 column
@@ -255,8 +299,8 @@ __device__ __forceinline__ void task_walk(const TaskArgs& a, int wv, int nwaves)
   const uint32_t b1 = a.offx + lane_off;
   const uint32_t b2 = a.offx2 - (uint32_t)a.B * a.ldx2b + lane_off;
 
-  int r = valid ? a.task_row[t] : 0;
-  bool head = valid && a.rowptr[r] < e0;    // first row began in an earlier task
+  int r = valid ? (ui.row & kRowMask) : 0;
+  bool head = valid && ((uint32_t)ui.row & kHeadBit);   // first row began in an earlier task
 
   const __amdgpu_buffer_rsrc_t rsx =
       __builtin_amdgcn_make_buffer_rsrc((void*)a.ubase, 0, FAR ? 0 : (int)a.span, 0x00020000);
@@ -266,9 +310,10 @@ __device__ __forceinline__ void task_walk(const TaskArgs& a, int wv, int nwaves)
   // CB: the codes' buffer, this lane's branch code offset, its LDS column
   const __amdgpu_buffer_rsrc_t rsc = __builtin_amdgcn_make_buffer_rsrc(
       CB ? (void*)a.codes : (void*)a.rec, 0, CB ? (int)a.codes_bytes : 0, 0x00020000);
-  uint32_t lane_boff = 0, lane16 = 0;
+  uint32_t lane_boff = 0, lane16 = 0, cb_m = 0;
   const char* cb_img = nullptr;
   if constexpr (CB) {
+    cb_m = (uint32_t)a.cb_M;              // a code >= M reads the image's zero row M
     extern __shared__ __attribute__((aligned(16))) char cb_smem[];
     lane_boff = (uint32_t)((4 * c4base) / a.cb_D) * 2u;
     lane16 = (uint32_t)k * 16u;
@@ -359,7 +404,8 @@ __device__ __forceinline__ void task_walk(const TaskArgs& a, int wv, int nwaves)
 #pragma unroll
       for (int u = 0; u < U; ++u)
         if (bk.co[u] < 0)
-          v[u][0] = *reinterpret_cast<const float4*>(cb_img + (cd[u] & 0xffffu) * (16u * G) + lane16);
+          v[u][0] = *reinterpret_cast<const float4*>(cb_img + min(cd[u] & 0xffffu, cb_m) * (16u * G) +
+                                                     lane16);
       return;
     }
 #pragma unroll
@@ -538,7 +584,8 @@ spmm_task_kernel(TaskArgs a) {
   // scalar (a VGPR-derived resource costs a readfirstlane loop per block)
   const int wv = __builtin_amdgcn_readfirstlane(
       xcd_remap(blockIdx.x, gridDim.x) * (kTaskThreads / 64) + (threadIdx.x >> 6));
-  task_walk<G, NC, U, FAR, GAT, PART>(a, wv, nwaves);
+  const int nnz = call_nnz(a);
+  task_walk<G, NC, U, FAR, GAT, PART>(a, wv, nwaves, unit_info<G>(a, wv, nnz), nnz);
 }
 
 // Codebook-source task kernel: persistent 16-wave workgroups (the LDS
@@ -546,9 +593,10 @@ spmm_task_kernel(TaskArgs a) {
 // its tile's codeword features -- image row m = the 4G columns of codeword
 // m's branches (G float4 pieces: 512 B at G = 32), so lane k always reads
 // banks 4k..4k+3 of its row: conflict-free within a task whatever the codes
-// -- and its waves walk task groups round-robin.  G = 32 (128-column tiles)
-// serves M <= 320; G = 16 (64 columns) M <= 640, G = 8 (32 columns) M <=
-// 1,280: narrower tiles fit larger codebooks, each tile walking every edge.
+// -- and its waves walk task groups round-robin.  Row M of the image is
+// zeros (a code >= M reads it).  G = 32 (128-column tiles) serves M <= 319;
+// G = 16 (64 columns) M <= 639, G = 8 (32 columns) M <= 1,279: narrower
+// tiles fit larger codebooks, each tile walking every edge.
 constexpr int kCbThreads = 1024;
 constexpr size_t kCbLdsMax = 160 * 1024;
 constexpr int kCbStage = (int)(kCbLdsMax / 16 / kCbThreads);   // image pieces per thread (10)
@@ -563,15 +611,18 @@ spmm_task_cb_kernel(TaskArgs a, int nunits) {
   // a load-then-write loop waited one memory round trip per piece, eight of
   // them at M = 256 before any wave could walk.  Loads past the image repeat
   // its last piece.
-  // (the tile's columns lie inside F: cb_lanes needs F % 4G == 0)
-  const int npc = a.cb_M * G;
+  // (the tile's columns lie inside F: cb_lanes needs F % 4G == 0).  Image
+  // row M is zeros: the walk reads a code >= M (invalid input) there.
+  const int npc = (a.cb_M + 1) * G;
   float4 v[kCbStage];
 #pragma unroll
   for (int r = 0; r < kCbStage; ++r) {
     const int i = min((int)threadIdx.x + r * kCbThreads, npc - 1);
     const int m = i / G, col = 4 * (tile * G + (i % G));
     const int b = col / a.cb_D, d = col % a.cb_D;
-    v[r] = *reinterpret_cast<const float4*>(a.cbe + b * a.cb_bstride + (int64_t)m * a.cb_ldw + d);
+    v[r] = m < a.cb_M ? *reinterpret_cast<const float4*>(a.cbe + b * a.cb_bstride +
+                                                          (int64_t)min(m, a.cb_M - 1) * a.cb_ldw + d)
+                      : make_float4(0.f, 0.f, 0.f, 0.f);
   }
   // (unconditional writes: a piece past the image rewrites the last one with
   // its own value -- a branch here would let the compiler sink each load
@@ -585,9 +636,15 @@ spmm_task_cb_kernel(TaskArgs a, int nunits) {
   const int wave = threadIdx.x >> 6;
   const int g = xcd_remap(blockIdx.x, gridDim.x);
   const int stride = (int)gridDim.x * (kCbThreads / 64);
-  for (int u0 = g * (kCbThreads / 64); u0 < nunits; u0 += stride) {
+  const int nnz = call_nnz(a);
+  // the next unit's plan words are read while this unit is walked
+  int u0 = g * (kCbThreads / 64);
+  UnitInfo cur = unit_info<G>(a, __builtin_amdgcn_readfirstlane(u0 + wave), nnz);
+  for (; u0 < nunits; u0 += stride) {
     const int wv = __builtin_amdgcn_readfirstlane(u0 + wave);
-    task_walk<G, 1, U, false, false, false, true>(a, wv, nunits);
+    const UnitInfo nxt = unit_info<G>(a, wv + stride, nnz);
+    task_walk<G, 1, U, false, false, false, true>(a, wv, nunits, cur, nnz);
+    cur = nxt;
   }
 }
 
@@ -595,7 +652,7 @@ spmm_task_cb_kernel(TaskArgs a, int nunits) {
 // over F columns: the widest tile whose LDS image fits (0: none)
 static int cb_lanes(int F, int M) {
   for (int G = 32; G >= 8; G >>= 1)
-    if (F % (4 * G) == 0 && (size_t)M * G * 16 <= kCbLdsMax) return G;
+    if (F % (4 * G) == 0 && (size_t)(M + 1) * G * 16 <= kCbLdsMax) return G;
   return 0;
 }
 
@@ -956,8 +1013,8 @@ extern "C" size_t vqgnn_spmm_task_cb_lds(int32_t M) {
   // bytes of the LDS image per column tile at the tile width M allows (any F
   // the width divides); 0 when no tile fits
   if (M <= 0) return 0;
-  for (int G = 32; G >= 8; G >>= 1)
-    if ((size_t)M * G * 16 <= kCbLdsMax) return (size_t)M * G * 16;
+  for (int G = 32; G >= 8; G >>= 1)       // M codeword rows + the zero row
+    if ((size_t)(M + 1) * G * 16 <= kCbLdsMax) return (size_t)(M + 1) * G * 16;
   return 0;
 }
 
@@ -971,8 +1028,8 @@ static const char* cb_unsupported(int32_t n_rows, int32_t B, int64_t ldx, int32_
   if (D <= 0 || D % 4 != 0 || F % D != 0) return "D must be a multiple of 4 dividing F";
   if (F / D > n_branches) return "F / D code columns exceed the codebook's branches";
   if (M <= 0 || cb_lanes(F, M) == 0)
-    return "M above the LDS image (M x 16G bytes <= 160 KiB with 4G | F: M <= 320 at F % 128 "
-           "== 0, 640 at F % 64 == 0, 1280)";
+    return "M above the LDS image ((M + 1) x 16G bytes <= 160 KiB with 4G | F: M <= 319 at F % "
+           "128 == 0, 639 at F % 64 == 0, 1279)";
   if (ldc < F / D || n_nodes < 0 || n_nodes >= (1 << 24) ||
       n_nodes * ldc * 2 >= ((int64_t)1 << 31) || ldc * 2 >= (1 << 24) ||
       (int64_t)B + n_nodes > (int64_t)kColMask)
@@ -983,6 +1040,7 @@ static const char* cb_unsupported(int32_t n_rows, int32_t B, int64_t ldx, int32_
   if ((int64_t)(B > 0 ? B - 1 : 0) * ldx * 4 + (int64_t)F * 4 >= 0x7FFFFFF0ll)
     return "X above the 2 GiB near range";
   if ((int64_t)n_rows * ldo * 4 >= ((int64_t)1 << 32)) return "out above 4 GiB";
+  if (path_env("VQGNN_SPMM_FAR", 0)) return "VQGNN_SPMM_FAR forces the 64-bit far path";
   return nullptr;
 }
 
@@ -1029,7 +1087,7 @@ static int spmm_task_cb_impl(const int32_t* rowptr, int32_t n_rows, int64_t nnz,
   hipStream_t s = as_stream(stream);
   if (nnz > 0) {
     const int G = cb_lanes(F, M);
-    const size_t lds = (size_t)M * G * 16;
+    const size_t lds = (size_t)(M + 1) * G * 16;
     // U = 8 edges per block (96 VGPRs at G = 32); U = 12 measured the same
     // (77.6 against 77.7 us on the arxiv batch), U = 16 spills
     static const bool attr_set = [] {

@@ -450,14 +450,22 @@ def spmm(rowptr, col, val, n_rows, nnz, X, F, X2=None, B=None, out=None, plan=No
     raise TypeError(f"spmm: plan must be a TaskPlan (CSR.plan), got {type(plan)}")
 
 
-def codebook_source_ok(X, F, M, D, out=None, codes=None, n_rows=None, n_branches=None):
+def codebook_source_ok(X, F, M, D, out=None, codes=None, n_rows=None, n_branches=None,
+                       emb_out=None):
     """Whether spmm_codebook serves this layer shape (include/vqgnn.h §6b):
     the kernel's own checks (vqgnn_spmm_task_cb_supported) plus the host-side
-    alignment of X.  codes / n_rows / n_branches default to shapes that pass
+    alignment of X, out and the codeword rows of emb_out (the entry's own
+    layout check: ldw >= D, ldw and the branch stride multiples of 4, 16-byte
+    aligned base).  codes / n_rows / n_branches default to shapes that pass
     their checks; out defaults to a dense [n_rows, F]."""
     if not (X.dim() == 2 and X.stride(1) == 1 and X.stride(0) % 4 == 0 and
             X.data_ptr() % 16 == 0):
         return False
+    if emb_out is not None:
+        if not (emb_out.dim() == 3 and emb_out.stride(2) == 1 and emb_out.stride(1) >= D and
+                emb_out.stride(1) % 4 == 0 and emb_out.stride(0) % 4 == 0 and
+                emb_out.data_ptr() % 16 == 0):
+            return False
     if out is not None and not (out.stride(1) == 1 and out.stride(0) % 4 == 0 and
                                 out.data_ptr() % 16 == 0):
         return False
@@ -474,10 +482,10 @@ def codebook_source_ok(X, F, M, D, out=None, codes=None, n_rows=None, n_branches
 def codebook_source_preferred(M):
     """Whether the codebook source is the faster aggregation for a codebook of
     M codewords: only where its LDS image fits the full-width walk (32 lanes
-    per task, 128-column tiles: M <= 320).  At M = 1,024 the 32-column tiles
+    per task, 128-column tiles: M <= 319, the image's zero row beside it).  At M = 1,024 the 32-column tiles
     walk every edge four times: 129 us against 103 us for gather + two-source
     SpMM on the arxiv GAT batch (profiles/r05_cb_m1024_probe.txt)."""
-    return int(lib().vqgnn_spmm_task_cb_lds(int(M))) == int(M) * 16 * 32
+    return int(lib().vqgnn_spmm_task_cb_lds(int(M))) == (int(M) + 1) * 16 * 32
 
 
 def spmm_codebook(rowptr, n_rows, nnz, X, F, B, codes, emb_out, D, plan_cb, out=None,
