@@ -61,6 +61,9 @@ def parse():
     # aggregation's fix-up launch (vqgnn_spmm_task_cb_fin);
     # --separate-finalize: its own launch after the aggregation
     p.add_argument("--separate-finalize", action="store_true")
+    # the aggregation on a side stream beside BN statistics + assign (they are
+    # data-independent; the EMA finalize joins both): overlap study
+    p.add_argument("--overlap", action="store_true")
     return p.parse_args()
 
 
@@ -191,10 +194,37 @@ def main():
         else:
             bank.feature_update(Xd, 0, nb, True, codes=codes, batch_idx=bidx)
 
+    side = torch.cuda.Stream() if args.overlap else None
+
     def step(record):
         e = [torch.cuda.Event(enable_timing=True) for _ in range(5)] if record else None
         if record:
             e[0].record()
+        if side is not None and not record:
+            # the aggregation's walk first, on the side stream (it reads X,
+            # the out-of-batch nodes' codes and the codebook from before this
+            # step's update; the assign writes only batch nodes' codes), then
+            # BN statistics + assign on this stream; the fix-up -- with the
+            # update's EMA finalize -- after both
+            side.wait_stream(torch.cuda.current_stream())
+            if use_cb:
+                with torch.cuda.stream(side):
+                    wk = kernels.spmm_codebook_walk(adj.rowptr, n, nnz, Xd, F, B, codes,
+                                                    bank.emb_out, D, spmm_plan)
+                vq_update()
+                torch.cuda.current_stream().wait_stream(side)
+                fin = None if args.separate_finalize else bank.take_fused_finalize()
+                fin_fused[0] = fin is not None
+                kernels.spmm_codebook_fixup(wk, finalize=fin)
+            else:
+                with torch.cuda.stream(side):
+                    aggregate(False, None, fuse=False)
+                vq_update()
+                torch.cuda.current_stream().wait_stream(side)
+            bank.finish_update()
+            if args.graph:
+                bank.sync_codes()
+            return
         vq_update()
         if record:
             e[1].record()
@@ -210,13 +240,13 @@ def main():
 
     fin_fused = [False]
 
-    def aggregate(record, e):
+    def aggregate(record, e, fuse=True):
         if use_cb:          # no x_first_order: the SpMM reads the codebook
             if record:
                 e[2].record()
             # the pending EMA finalize inside the SpMM's fix-up launch (one
             # process; multi-GPU it waits for its all-reduce: finish_update)
-            fin = None if args.separate_finalize else bank.take_fused_finalize()
+            fin = None if args.separate_finalize or not fuse else bank.take_fused_finalize()
             fin_fused[0] = fin is not None
             kernels.spmm_codebook(adj.rowptr, n, nnz, Xd, F, B, codes, bank.emb_out, D,
                                   spmm_plan, finalize=fin)

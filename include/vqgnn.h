@@ -379,7 +379,17 @@ int vqgnn_spmm_task(const int32_t* rowptr, int32_t n_rows, int32_t n_cols, int64
  *      vqgnn_vq_ema_finalize; fin == NULL is vqgnn_spmm_task_cb.  For
  *      M >= 1,024 (the finalize's two-kernel form) the finalize runs as its
  *      own launches after the fix-up.  Single process: a multi-GPU update
- *      finalizes after its statistics' all-reduce instead.                  */
+ *      finalizes after its statistics' all-reduce instead.
+ *    vqgnn_spmm_task_cb_walk + vqgnn_spmm_task_cb_fixup: vqgnn_spmm_task_cb_fin
+ *      as two calls with the same arguments (the same workspace): the walk
+ *      (every row that ends inside a task, and the cut rows' partials) and
+ *      the fix-up (cut and empty rows, plus *fin's finalize when fin is not
+ *      NULL).  The caller orders them: the fix-up after the walk (same
+ *      stream, or an event).  Between them the walk may share the GPU with
+ *      work that does not write what it reads (X, the out-of-batch nodes'
+ *      codes, the codewords) -- the VQ update of the batch rows: its assign
+ *      writes only the batch nodes' codes, its finalize runs in the fix-up.
+ *      Same outputs, bit for bit, as the one-call entries.                 */
 int vqgnn_spmm_task_records_cb(int64_t* records, int64_t nnz, int32_t B, const int64_t* subset,
                                int32_t n_cols, int64_t n_nodes, vqgnn_stream_t stream);
 size_t vqgnn_spmm_task_cb_lds(int32_t M);
@@ -399,6 +409,20 @@ int vqgnn_spmm_task_cb_fin(const int32_t* rowptr, int32_t n_rows, int64_t nnz, i
                            int64_t ldo, const int32_t* plan, const int64_t* records_cb, int32_t K,
                            int32_t n_jobs, int32_t n_empty, void* workspace,
                            const vqgnn_ema_finalize_args* fin, vqgnn_stream_t stream);
+int vqgnn_spmm_task_cb_walk(const int32_t* rowptr, int32_t n_rows, int64_t nnz, int32_t B,
+                            const float* X, int64_t ldx, int32_t F, const int16_t* codes,
+                            int64_t ldc, int64_t n_nodes, const float* codewords, int64_t ldw,
+                            int64_t bstride, int32_t n_branches, int32_t M, int32_t D, float* out,
+                            int64_t ldo, const int32_t* plan, const int64_t* records_cb, int32_t K,
+                            int32_t n_jobs, int32_t n_empty, void* workspace,
+                            vqgnn_stream_t stream);
+int vqgnn_spmm_task_cb_fixup(const int32_t* rowptr, int32_t n_rows, int64_t nnz, int32_t B,
+                             const float* X, int64_t ldx, int32_t F, const int16_t* codes,
+                             int64_t ldc, int64_t n_nodes, const float* codewords, int64_t ldw,
+                             int64_t bstride, int32_t n_branches, int32_t M, int32_t D, float* out,
+                             int64_t ldo, const int32_t* plan, const int64_t* records_cb, int32_t K,
+                             int32_t n_jobs, int32_t n_empty, void* workspace,
+                             const vqgnn_ema_finalize_args* fin, vqgnn_stream_t stream);
 
 /* 7. CSR transpose (structure + values) for the backward product
  *    dX = A^T dOut (torch_sparse matmul autograd, convs.py:95).  Output CSR of

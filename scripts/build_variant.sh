@@ -6,7 +6,8 @@
 #    with -DVQGNN_EXPERIMENTS: its measurement knobs (VQGNN_TASK_U/G,
 #    VQGNN_ASG_*, VQGNN_ASSIGN_MSWEEP, VQGNN_TASK_DBG, ...) read the
 #    environment there and only there -- the default library ignores them.
-#    EXTRA_FLAGS: more hipcc flags for the replaced file.
+#    EXTRA_FLAGS: more hipcc flags for the replaced file.  EXP_ALSO: more
+#    in-tree sources (space separated) compiled with -DVQGNN_EXPERIMENTS too.
 set -e
 cd "$(dirname "$0")/../vq-gnn_amd/csrc"
 name=$1; src=$2; repl=$3
@@ -20,6 +21,11 @@ for f in $(sed -n 's/^SRCS := //p;s/^         //p' Makefile | tr ' ' '\n' | grep
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++20 -ffp-contract=off -Wall \
       -Wno-unused-function -munsafe-fp-atomics -DVQGNN_EXPERIMENTS $EXTRA_FLAGS -I$PWD -c $tmp/$src -o $tmp/${src%.hip}.o
     objs="$objs $tmp/${src%.hip}.o"
+  elif [[ " $EXP_ALSO " == *" $f "* ]]; then
+    /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++20 -ffp-contract=off -Wall \
+      -Wno-unused-function -munsafe-fp-atomics -DVQGNN_EXPERIMENTS $(test $f = vq_kernels.hip && echo -fno-slp-vectorize) \
+      -I$PWD -c $f -o $tmp/${f%.hip}.o
+    objs="$objs $tmp/${f%.hip}.o"
   else
     objs="$objs ../lib/obj/${f%.hip}.o"
   fi

@@ -99,3 +99,55 @@ def test_finalize_fused_into_codebook_spmm(monkeypatch, semantics, M):
         X = X * 1.01
     a.check_bad_init()
     b.check_bad_init()
+
+
+@pytest.mark.parametrize("M", [256, 1024])
+def test_walk_beside_update_then_fixup(monkeypatch, M):
+    """The overlapped step (bench.py's default): the codebook-source walk on a
+    side stream (vqgnn_spmm_task_cb_walk) beside the VQ update on the main
+    stream, then the fix-up with the update's EMA finalize
+    (vqgnn_spmm_task_cb_fixup) after both -- the SpMM output and every piece
+    of VQ state bit-identical to the serial update + spmm_codebook(finalize)
+    form, step after step.  M = 1,024: the finalize's two-kernel form."""
+    from vq_gnn_amd import graph, kernels
+    monkeypatch.setattr(vqmod, "STRICT_BAD_INIT", False)
+    cfg = dict(graph.CONFIGS["arxiv_gcn"])
+    g, _, bt = graph.make_batch(cfg)
+    F, D = 128, 4
+    nb = F // D
+    bidx, subset, adj = graph.batch_to_device(bt, DEV)
+    gen = torch.Generator(device="cpu").manual_seed(6)
+    X = torch.randn(bt.B, F, generator=gen).to(DEV)
+    G = (torch.randn(bt.B, F, generator=gen) * 1e-3).to(DEV)
+    a, b = _bank(nb, M, D), _bank(nb, M, D)
+    ca = torch.randint(0, M, (cfg["N"], nb), dtype=torch.int16, generator=gen).to(DEV)
+    cb = ca.clone()
+    pcb = adj.plan_codebook(bt.B, subset, cfg["N"])
+    side = torch.cuda.Stream()
+    main = torch.cuda.current_stream()
+    for step in range(3):
+        a.update(X, G, 0, nb, True, codes=ca, batch_idx=bidx, defer=True)
+        out_a = kernels.spmm_codebook(adj.rowptr, bt.n, bt.nnz, X, F, bt.B, ca, a.emb_out, D,
+                                      pcb, finalize=a.take_fused_finalize())
+        a.finish_update()
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            wk = kernels.spmm_codebook_walk(adj.rowptr, bt.n, bt.nnz, X, F, bt.B, cb, b.emb_out,
+                                            D, pcb)
+        b.update(X, G, 0, nb, True, codes=cb, batch_idx=bidx, defer=True)
+        main.wait_stream(side)
+        fin = b.take_fused_finalize()
+        assert fin is not None
+        out_b = kernels.spmm_codebook_fixup(wk, finalize=fin)
+        b.finish_update()
+        with pytest.raises(RuntimeError):
+            kernels.spmm_codebook_fixup(wk)
+        torch.cuda.synchronize()
+        assert torch.equal(out_a, out_b), step
+        for name in ("emb", "emb_out", "ema_w", "cs", "rm_f", "rv_f", "rm_g", "rv_g",
+                     "bad_flag", "stats_u", "stats_f"):
+            assert torch.equal(getattr(a, name), getattr(b, name)), (step, name)
+        assert torch.equal(ca, cb)
+        X = X * 1.01
+    a.check_bad_init()
+    b.check_bad_init()

@@ -106,6 +106,15 @@ SIGNATURES = {
                                               _i32, _i32, _c_void_p, _i64, _c_void_p, _c_void_p,
                                               _i32, _i32, _i32, _c_void_p,
                                               ctypes.POINTER(EmaFinalizeArgs), _c_void_p]),
+    "vqgnn_spmm_task_cb_walk": (ctypes.c_int, [_c_void_p, _i32, _i64, _i32, _c_void_p, _i64,
+                                               _i32, _c_void_p, _i64, _i64, _c_void_p, _i64, _i64,
+                                               _i32, _i32, _i32, _c_void_p, _i64, _c_void_p,
+                                               _c_void_p, _i32, _i32, _i32, _c_void_p, _c_void_p]),
+    "vqgnn_spmm_task_cb_fixup": (ctypes.c_int, [_c_void_p, _i32, _i64, _i32, _c_void_p, _i64,
+                                                _i32, _c_void_p, _i64, _i64, _c_void_p, _i64, _i64,
+                                                _i32, _i32, _i32, _c_void_p, _i64, _c_void_p,
+                                                _c_void_p, _i32, _i32, _i32, _c_void_p,
+                                                ctypes.POINTER(EmaFinalizeArgs), _c_void_p]),
     "vqgnn_gat_att_grad_workspace": (_size, [_i32, _i32, _i32]),
     "vqgnn_gat_att_grad": (ctypes.c_int, [_c_void_p, _i64, _c_void_p, _i64, _i32, _i32, _i32,
                                           _i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p,

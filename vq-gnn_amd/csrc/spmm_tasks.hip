@@ -69,6 +69,8 @@ struct TaskArgs {
   const char* ubase;
   uint32_t span, offx, ldxb, offx2, ldx2b;
   uint32_t ldob;            // near path: ldo in bytes (rows addressed with a 24-bit multiply)
+  int xcd;                  // 1: XCD-contiguous task ranges (VQGNN_TASK_XCD=0, experiments
+                            // builds only: the dispatcher's round-robin order)
   int dbg;                  // VQGNN_TASK_DBG (experiments builds only): 1 = no row
                             // stores, results invalid; 0 in the default library
   // GAT mode (OurGATConv + the layer's ones-column normalisation): edge
@@ -582,8 +584,12 @@ spmm_task_kernel(TaskArgs a) {
   const int nwaves = (int)gridDim.x * (kTaskThreads / 64);
   // wave-uniform in an SGPR: the record buffer resource built from it is then
   // scalar (a VGPR-derived resource costs a readfirstlane loop per block)
-  const int wv = __builtin_amdgcn_readfirstlane(
-      xcd_remap(blockIdx.x, gridDim.x) * (kTaskThreads / 64) + (threadIdx.x >> 6));
+#ifdef VQGNN_EXPERIMENTS
+  const int blk = a.xcd ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+#else
+  const int blk = xcd_remap(blockIdx.x, gridDim.x);
+#endif
+  const int wv = __builtin_amdgcn_readfirstlane(blk * (kTaskThreads / 64) + (threadIdx.x >> 6));
   const int nnz = call_nnz(a);
   task_walk<G, NC, U, FAR, GAT, PART>(a, wv, nwaves, unit_info<G>(a, wv, nnz), nnz);
 }
@@ -601,8 +607,8 @@ constexpr int kCbThreads = 1024;
 constexpr size_t kCbLdsMax = 160 * 1024;
 constexpr int kCbStage = (int)(kCbLdsMax / 16 / kCbThreads);   // image pieces per thread (10)
 
-template <int G, int U>
-__global__ void __launch_bounds__(kCbThreads) __attribute__((amdgpu_waves_per_eu(4)))
+template <int G, int U, int NT = kCbThreads>
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4)))
 spmm_task_cb_kernel(TaskArgs a, int nunits) {
   extern __shared__ __attribute__((aligned(16))) char cb_smem[];
   const int tile = blockIdx.y;
@@ -613,32 +619,36 @@ spmm_task_cb_kernel(TaskArgs a, int nunits) {
   // its last piece.
   // (the tile's columns lie inside F: cb_lanes needs F % 4G == 0).  Image
   // row M is zeros: the walk reads a code >= M (invalid input) there.
+  // (NT < kCbThreads, an experiments-build workgroup shape: several rounds)
   const int npc = (a.cb_M + 1) * G;
-  float4 v[kCbStage];
 #pragma unroll
-  for (int r = 0; r < kCbStage; ++r) {
-    const int i = min((int)threadIdx.x + r * kCbThreads, npc - 1);
-    const int m = i / G, col = 4 * (tile * G + (i % G));
-    const int b = col / a.cb_D, d = col % a.cb_D;
-    v[r] = m < a.cb_M ? *reinterpret_cast<const float4*>(a.cbe + b * a.cb_bstride +
-                                                          (int64_t)min(m, a.cb_M - 1) * a.cb_ldw + d)
-                      : make_float4(0.f, 0.f, 0.f, 0.f);
-  }
-  // (unconditional writes: a piece past the image rewrites the last one with
-  // its own value -- a branch here would let the compiler sink each load
-  // into it, one wait per piece again)
+  for (int base = 0; base < kCbThreads * kCbStage; base += NT * kCbStage) {
+    float4 v[kCbStage];
 #pragma unroll
-  for (int r = 0; r < kCbStage; ++r) {
-    const int i = min((int)threadIdx.x + r * kCbThreads, npc - 1);
-    *reinterpret_cast<float4*>(cb_smem + (size_t)i * 16) = v[r];
+    for (int r = 0; r < kCbStage; ++r) {
+      const int i = min(base + (int)threadIdx.x + r * NT, npc - 1);
+      const int m = i / G, col = 4 * (tile * G + (i % G));
+      const int b = col / a.cb_D, d = col % a.cb_D;
+      v[r] = m < a.cb_M ? *reinterpret_cast<const float4*>(a.cbe + b * a.cb_bstride +
+                                                            (int64_t)min(m, a.cb_M - 1) * a.cb_ldw + d)
+                        : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    // (unconditional writes: a piece past the image rewrites the last one with
+    // its own value -- a branch here would let the compiler sink each load
+    // into it, one wait per piece again)
+#pragma unroll
+    for (int r = 0; r < kCbStage; ++r) {
+      const int i = min(base + (int)threadIdx.x + r * NT, npc - 1);
+      *reinterpret_cast<float4*>(cb_smem + (size_t)i * 16) = v[r];
+    }
   }
   __syncthreads();
   const int wave = threadIdx.x >> 6;
   const int g = xcd_remap(blockIdx.x, gridDim.x);
-  const int stride = (int)gridDim.x * (kCbThreads / 64);
+  const int stride = (int)gridDim.x * (NT / 64);
   const int nnz = call_nnz(a);
   // the next unit's plan words are read while this unit is walked
-  int u0 = g * (kCbThreads / 64);
+  int u0 = g * (NT / 64);
   UnitInfo cur = unit_info<G>(a, __builtin_amdgcn_readfirstlane(u0 + wave), nnz);
   for (; u0 < nunits; u0 += stride) {
     const int wv = __builtin_amdgcn_readfirstlane(u0 + wave);
@@ -923,6 +933,7 @@ static int task_setup(TaskArgs& a, const int32_t* rowptr, int32_t n_rows, int32_
     a.ldob = (uint32_t)(ldo * 4);
   }
   a.dbg = VQGNN_KNOB("VQGNN_TASK_DBG", 0);
+  a.xcd = VQGNN_KNOB("VQGNN_TASK_XCD", 1);
   return VQGNN_OK;
 }
 
@@ -1056,7 +1067,9 @@ static int spmm_task_cb_impl(const int32_t* rowptr, int32_t n_rows, int64_t nnz,
                              int64_t bstride, int32_t n_branches, int32_t M, int32_t D, float* out,
                              int64_t ldo, const int32_t* plan, const int64_t* records_cb,
                              int32_t K, int32_t n_jobs, int32_t n_empty, void* workspace,
-                             const vqgnn_ema_finalize_args* fin, vqgnn_stream_t stream) {
+                             const vqgnn_ema_finalize_args* fin, vqgnn_stream_t stream,
+                             int phases = 3) {
+  // phases: 1 the walk, 2 the fix-up (+ finalize), 3 both (same checks either way)
   clear_error();
   EmaFin ef{};
   if (fin) {                                // checked before anything is launched
@@ -1085,8 +1098,8 @@ static int spmm_task_cb_impl(const int32_t* rowptr, int32_t n_rows, int64_t nnz,
   a.cb_M = M;
   a.cb_D = D;
   hipStream_t s = as_stream(stream);
-  if (nnz > 0) {
-    const int G = cb_lanes(F, M);
+  if (nnz > 0 && (phases & 1)) {
+    int G = cb_lanes(F, M);
     const size_t lds = (size_t)(M + 1) * G * 16;
     // U = 8 edges per block (96 VGPRs at G = 32); U = 12 measured the same
     // (77.6 against 77.7 us on the arxiv batch), U = 16 spills
@@ -1095,6 +1108,12 @@ static int spmm_task_cb_impl(const int32_t* rowptr, int32_t n_rows, int64_t nnz,
                             (const void*)spmm_task_cb_kernel<16, 8>,
                             (const void*)spmm_task_cb_kernel<8, 8>})
         (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kCbLdsMax);
+#ifdef VQGNN_EXPERIMENTS
+      for (const void* f : {(const void*)spmm_task_cb_kernel<32, 8, 512>,
+                            (const void*)spmm_task_cb_kernel<16, 8, 512>,
+                            (const void*)spmm_task_cb_kernel<8, 8, 512>})
+        (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kCbLdsMax);
+#endif
       return true;
     }();
     (void)attr_set;
@@ -1106,15 +1125,63 @@ static int spmm_task_cb_impl(const int32_t* rowptr, int32_t n_rows, int64_t nnz,
     const int nunits = (a.ntasks + tpw - 1) / tpw;
     int wgs = (nunits + kCbThreads / 64 - 1) / (kCbThreads / 64);
     wgs = wgs < cus ? wgs : cus;
-    const dim3 grid(wgs, F / (4 * G));
-    if (G == 32)
-      hipLaunchKernelGGL((spmm_task_cb_kernel<32, 8>), grid, dim3(kCbThreads), lds, s, a, nunits);
-    else if (G == 16)
-      hipLaunchKernelGGL((spmm_task_cb_kernel<16, 8>), grid, dim3(kCbThreads), lds, s, a, nunits);
-    else
-      hipLaunchKernelGGL((spmm_task_cb_kernel<8, 8>), grid, dim3(kCbThreads), lds, s, a, nunits);
+#ifdef VQGNN_EXPERIMENTS
+    // measurement knobs (overlap study): a narrower tile, 8-wave workgroups,
+    // fewer workgroups per column tile
+    const int g_env = path_env("VQGNN_CB_G", 0), nt_env = path_env("VQGNN_CB_NT", 0),
+              wg_env = path_env("VQGNN_CB_WGS", 0);
+    if (g_env && g_env < G && (g_env == 16 || g_env == 8)) G = g_env;
+    if (nt_env == 512 || wg_env > 0) {
+      const int nt = nt_env == 512 ? 512 : kCbThreads;
+      const int tpw2 = 64 / G;
+      const int nu = (a.ntasks + tpw2 - 1) / tpw2;
+      int w2 = (nu + nt / 64 - 1) / (nt / 64);
+      const int cap = wg_env > 0 ? wg_env : cus;
+      w2 = w2 < cap ? w2 : cap;
+      const size_t lds2 = (size_t)(M + 1) * G * 16;
+      const dim3 grid2(w2, F / (4 * G));
+#define CB_LAUNCH(GG, NN) \
+      hipLaunchKernelGGL((spmm_task_cb_kernel<GG, 8, NN>), grid2, dim3(NN), lds2, s, a, nu)
+      if (nt == 512) {
+        if (G == 32) CB_LAUNCH(32, 512); else if (G == 16) CB_LAUNCH(16, 512); else CB_LAUNCH(8, 512);
+      } else {
+        if (G == 32) CB_LAUNCH(32, 1024); else if (G == 16) CB_LAUNCH(16, 1024); else CB_LAUNCH(8, 1024);
+      }
+#undef CB_LAUNCH
+      goto walked;
+    }
+    {
+      const int tpw2 = 64 / G;
+      const int nu = (a.ntasks + tpw2 - 1) / tpw2;
+      wgs = (nu + kCbThreads / 64 - 1) / (kCbThreads / 64);
+      wgs = wgs < cus ? wgs : cus;
+      const size_t lds2 = (size_t)(M + 1) * G * 16;
+      const dim3 grid2(wgs, F / (4 * G));
+      if (G == 32)
+        hipLaunchKernelGGL((spmm_task_cb_kernel<32, 8>), grid2, dim3(kCbThreads), lds2, s, a, nu);
+      else if (G == 16)
+        hipLaunchKernelGGL((spmm_task_cb_kernel<16, 8>), grid2, dim3(kCbThreads), lds2, s, a, nu);
+      else
+        hipLaunchKernelGGL((spmm_task_cb_kernel<8, 8>), grid2, dim3(kCbThreads), lds2, s, a, nu);
+      goto walked;
+    }
+#endif
+    {
+      const dim3 grid(wgs, F / (4 * G));
+      if (G == 32)
+        hipLaunchKernelGGL((spmm_task_cb_kernel<32, 8>), grid, dim3(kCbThreads), lds, s, a, nunits);
+      else if (G == 16)
+        hipLaunchKernelGGL((spmm_task_cb_kernel<16, 8>), grid, dim3(kCbThreads), lds, s, a, nunits);
+      else
+        hipLaunchKernelGGL((spmm_task_cb_kernel<8, 8>), grid, dim3(kCbThreads), lds, s, a, nunits);
+    }
   }
-  if (!fin) {
+#ifdef VQGNN_EXPERIMENTS
+walked:
+#endif
+  if (!(phases & 2)) {
+    // the walk alone: its fix-up comes later (vqgnn_spmm_task_cb_fixup)
+  } else if (!fin) {
     task_fixup<false>(a, s);
   } else if (!ef.split) {
     task_fixup_fin(a, ef, fin->nb, s);      // one launch: fix-up + finalize
@@ -1150,6 +1217,37 @@ extern "C" int vqgnn_spmm_task_cb_fin(const int32_t* rowptr, int32_t n_rows, int
   return spmm_task_cb_impl(rowptr, n_rows, nnz, B, X, ldx, F, codes, ldc, n_nodes, codewords, ldw,
                            bstride, n_branches, M, D, out, ldo, plan, records_cb, K, n_jobs,
                            n_empty, workspace, fin, stream);
+}
+
+// The walk and the fix-up as two calls (include/vqgnn.h §6b): the walk can
+// run on a second stream beside the VQ update, the fix-up -- with the
+// update's EMA finalize -- after both.  The same arguments to both calls.
+extern "C" int vqgnn_spmm_task_cb_walk(const int32_t* rowptr, int32_t n_rows, int64_t nnz,
+                                       int32_t B, const float* X, int64_t ldx, int32_t F,
+                                       const int16_t* codes, int64_t ldc, int64_t n_nodes,
+                                       const float* codewords, int64_t ldw, int64_t bstride,
+                                       int32_t n_branches, int32_t M, int32_t D, float* out,
+                                       int64_t ldo, const int32_t* plan, const int64_t* records_cb,
+                                       int32_t K, int32_t n_jobs, int32_t n_empty,
+                                       void* workspace, vqgnn_stream_t stream) {
+  return spmm_task_cb_impl(rowptr, n_rows, nnz, B, X, ldx, F, codes, ldc, n_nodes, codewords, ldw,
+                           bstride, n_branches, M, D, out, ldo, plan, records_cb, K, n_jobs,
+                           n_empty, workspace, nullptr, stream, 1);
+}
+
+extern "C" int vqgnn_spmm_task_cb_fixup(const int32_t* rowptr, int32_t n_rows, int64_t nnz,
+                                        int32_t B, const float* X, int64_t ldx, int32_t F,
+                                        const int16_t* codes, int64_t ldc, int64_t n_nodes,
+                                        const float* codewords, int64_t ldw, int64_t bstride,
+                                        int32_t n_branches, int32_t M, int32_t D, float* out,
+                                        int64_t ldo, const int32_t* plan,
+                                        const int64_t* records_cb, int32_t K, int32_t n_jobs,
+                                        int32_t n_empty, void* workspace,
+                                        const vqgnn_ema_finalize_args* fin,
+                                        vqgnn_stream_t stream) {
+  return spmm_task_cb_impl(rowptr, n_rows, nnz, B, X, ldx, F, codes, ldc, n_nodes, codewords, ldw,
+                           bstride, n_branches, M, D, out, ldo, plan, records_cb, K, n_jobs,
+                           n_empty, workspace, fin, stream, 2);
 }
 
 extern "C" int vqgnn_gat_spmm_task(const int32_t* rowptr, int32_t n_rows, int32_t n_cols,

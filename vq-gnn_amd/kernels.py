@@ -488,6 +488,39 @@ def codebook_source_preferred(M):
     return int(lib().vqgnn_spmm_task_cb_lds(int(M))) == (int(M) + 1) * 16 * 32
 
 
+def _cb_prepare(rowptr, n_rows, nnz, X, F, B, codes, emb_out, D, plan_cb, out, what):
+    """Checks and the argument tuple shared by the codebook-source entries."""
+    require_gpu(X, what)
+    if getattr(plan_cb, "cb_B", None) != int(B):
+        raise ValueError(f"{what}: plan_cb must come from TaskPlan.with_codebook_source "
+                         f"for B={B}")
+    if plan_cb.nnz != int(nnz) or int(n_rows) > plan_cb.n_rows:
+        raise ValueError(f"{what}: task plan for nnz={plan_cb.nnz}, rows={plan_cb.n_rows}; "
+                         f"called with nnz={nnz}, n_rows={n_rows}")
+    if codes.dtype != torch.int16 or emb_out.dtype != torch.float32:
+        raise TypeError(f"{what}: codes must be int16 and emb_out float32")
+    if codes.dim() != 2 or codes.stride(1) != 1:
+        raise ValueError(f"{what}: codes must be an int16 [N, ldc] row-major view")
+    n_br, M, ldw = (int(v) for v in emb_out.shape)
+    if emb_out.stride(2) != 1 or emb_out.stride(1) != ldw:
+        raise ValueError(f"{what}: emb_out must be row-major per branch")
+    dev = X.device
+    if out is None:
+        out = torch.empty(n_rows, F, dtype=torch.float32, device=dev)
+    ws = workspace(lib().vqgnn_spmm_task_workspace(int(nnz), plan_cb.K, F), dev)
+    args = (ptr(rowptr), int(n_rows), int(nnz), int(B), ptr(X), _ld(X), F,
+            ptr(codes), codes.stride(0), codes.shape[0], ptr(emb_out),
+            emb_out.stride(1), emb_out.stride(0), n_br, M, int(D), ptr(out),
+            _ld(out), ptr(plan_cb.plan), ptr(plan_cb.records), plan_cb.K,
+            plan_cb.n_jobs, plan_cb.n_empty, ptr(ws))
+    return out, ws, args
+
+
+def _finalize_record(finalize):
+    fin_args, fin_kw = getattr(finalize, "operands", finalize)
+    return ema_finalize_args(*fin_args, **fin_kw)
+
+
 def spmm_codebook(rowptr, n_rows, nnz, X, F, B, codes, emb_out, D, plan_cb, out=None,
                   finalize=None):
     """out = A @ [X[:B] ; x_first_order] with x_first_order's rows (the
@@ -502,40 +535,62 @@ def spmm_codebook(rowptr, n_rows, nnz, X, F, B, codes, emb_out, D, plan_cb, out=
     vq_ema_finalize, one launch fewer.  A handle is retired (done()) only
     once the launch is queued: if this call raises, the bank keeps the
     finalize pending for finish_update()."""
-    require_gpu(X, "spmm_codebook")
-    if getattr(plan_cb, "cb_B", None) != int(B):
-        raise ValueError("spmm_codebook: plan_cb must come from TaskPlan.with_codebook_source "
-                         f"for B={B}")
-    if plan_cb.nnz != int(nnz) or int(n_rows) > plan_cb.n_rows:
-        raise ValueError(f"spmm_codebook: task plan for nnz={plan_cb.nnz}, rows={plan_cb.n_rows}; "
-                         f"called with nnz={nnz}, n_rows={n_rows}")
-    if codes.dtype != torch.int16 or emb_out.dtype != torch.float32:
-        raise TypeError("spmm_codebook: codes must be int16 and emb_out float32")
-    if codes.dim() != 2 or codes.stride(1) != 1:
-        raise ValueError("spmm_codebook: codes must be an int16 [N, ldc] row-major view")
-    n_br, M, ldw = (int(v) for v in emb_out.shape)
-    if emb_out.stride(2) != 1 or emb_out.stride(1) != ldw:
-        raise ValueError("spmm_codebook: emb_out must be row-major per branch")
-    dev = X.device
-    if out is None:
-        out = torch.empty(n_rows, F, dtype=torch.float32, device=dev)
+    out, ws, args = _cb_prepare(rowptr, n_rows, nnz, X, F, B, codes, emb_out, D, plan_cb, out,
+                                "spmm_codebook")
     L = lib()
-    ws = workspace(L.vqgnn_spmm_task_workspace(int(nnz), plan_cb.K, F), dev)
-    args = (ptr(rowptr), int(n_rows), int(nnz), int(B), ptr(X), _ld(X), F,
-            ptr(codes), codes.stride(0), codes.shape[0], ptr(emb_out),
-            emb_out.stride(1), emb_out.stride(0), n_br, M, int(D), ptr(out),
-            _ld(out), ptr(plan_cb.plan), ptr(plan_cb.records), plan_cb.K,
-            plan_cb.n_jobs, plan_cb.n_empty, ptr(ws))
     if finalize is None:
         check(L.vqgnn_spmm_task_cb(*args, stream_ptr()), "spmm_task_cb")
     else:
-        fin_args, fin_kw = getattr(finalize, "operands", finalize)
-        rec = ema_finalize_args(*fin_args, **fin_kw)
+        rec = _finalize_record(finalize)
         check(L.vqgnn_spmm_task_cb_fin(*args, ctypes.byref(rec), stream_ptr()),
               "spmm_task_cb_fin")
         if hasattr(finalize, "done"):
             finalize.done()
     return out
+
+
+class CodebookWalk:
+    """A codebook-source aggregation whose walk is queued and whose fix-up is
+    not (spmm_codebook_walk -> spmm_codebook_fixup)."""
+
+    def __init__(self, out, ws, args, stream):
+        self.out, self.ws, self.args, self.stream = out, ws, args, stream
+        self.fixed = False
+
+
+def spmm_codebook_walk(rowptr, n_rows, nnz, X, F, B, codes, emb_out, D, plan_cb, out=None):
+    """spmm_codebook's walk alone, on the current stream (vqgnn_spmm_task_cb_walk,
+    include/vqgnn.h §6b) -> CodebookWalk.  Meant for a second stream beside
+    the VQ update of the same batch (the assign writes only the batch nodes'
+    codes; the walk reads X, the out-of-batch nodes' codes and emb_out), with
+    spmm_codebook_fixup after both.  The rows that span tasks and the empty
+    rows of out are written only by the fix-up."""
+    out, ws, args = _cb_prepare(rowptr, n_rows, nnz, X, F, B, codes, emb_out, D, plan_cb, out,
+                                "spmm_codebook_walk")
+    check(lib().vqgnn_spmm_task_cb_walk(*args, stream_ptr()), "spmm_task_cb_walk")
+    return CodebookWalk(out, ws, args, torch.cuda.current_stream())
+
+
+def spmm_codebook_fixup(walk, finalize=None):
+    """The fix-up of a CodebookWalk on the current stream (which must already
+    wait for the walk's stream: torch's wait_stream), with the pending EMA
+    finalize inside it as in spmm_codebook -> out, equal bit for bit to
+    spmm_codebook's.  The walk's buffers are marked in use by this stream
+    for the caching allocator."""
+    if walk.fixed:
+        raise RuntimeError("spmm_codebook_fixup: this walk was fixed up already")
+    cur = torch.cuda.current_stream()
+    if cur != walk.stream:
+        walk.out.record_stream(cur)
+        walk.ws.record_stream(cur)
+    L = lib()
+    rec = None if finalize is None else _finalize_record(finalize)
+    check(L.vqgnn_spmm_task_cb_fixup(*walk.args, ctypes.byref(rec) if rec is not None else None,
+                                     stream_ptr()), "spmm_task_cb_fixup")
+    walk.fixed = True
+    if finalize is not None and hasattr(finalize, "done"):
+        finalize.done()
+    return walk.out
 
 
 def csr_transpose(rowptr, col, val, n_rows, n_cols, nnz, want_perm=False):
