@@ -5,12 +5,18 @@ One step = one layer step on a synthetic arxiv-shaped mini-batch (SURVEY.md §8d
         semantics (W = 2D: features and gradients), one launch sequence
         (BN stats -> BN finalize -> MFMA assign + fused EMA statistics ->
         EMA finalize), c_indices scattered in place;
-  (ii)  codeword gather for the B' out-of-batch rows (x_first_order);
-  (iii) two-source CSR SpMM over all nnz edges, all n rows.
-With update() semantics the EMA finalize is queued after (ii)+(iii): the
-gather reads the codebook from before this step's update, as the reference's
-forward does (its update runs in the backward hook, models.py:181-185), and
-with N > 1 the all-reduce of the EMA statistics overlaps (ii)+(iii).
+  (ii)  the aggregation over all nnz edges and all n rows: for GCN / SAGE with
+        M <= 319 the codebook-source SpMM (the B' out-of-batch rows read as
+        codewords from an LDS image, kernels.spmm_codebook), otherwise the
+        codeword gather (x_first_order) + two-source SpMM (GAT: the fused
+        attention aggregation).
+With update() semantics the EMA finalize is queued after (ii): the
+aggregation reads the codebook from before this step's update, as the
+reference's forward does (its update runs in the backward hook,
+models.py:181-185); one process runs it inside the aggregation's fix-up
+launch, and (--overlap auto) the aggregation's walk on a side stream beside
+(i)'s BN statistics and assign, the fix-up after both.  With N > 1 the
+all-reduce of the EMA statistics overlaps (ii).
 value = edges of all ranks / time.  Inputs are resident in HBM before timing.
 
 Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
@@ -61,9 +67,15 @@ def parse():
     # aggregation's fix-up launch (vqgnn_spmm_task_cb_fin);
     # --separate-finalize: its own launch after the aggregation
     p.add_argument("--separate-finalize", action="store_true")
-    # the aggregation on a side stream beside BN statistics + assign (they are
-    # data-independent; the EMA finalize joins both): overlap study
-    p.add_argument("--overlap", action="store_true")
+    # the codebook-source walk on a side stream beside BN statistics + assign
+    # (data-independent; the fix-up with the EMA finalize joins both):
+    # auto = on for one process with the codebook source,
+    # off = the serial step; on = also for N > 1 (the code exchange lands on
+    # the side stream, VQBank.land_codes_on)
+    p.add_argument("--overlap", default="auto", choices=["auto", "on", "off"])
+    # (study) the whole aggregation -- walk and fix-up -- on the side stream,
+    # the EMA finalize in its own launch after the join
+    p.add_argument("--overlap-whole", action="store_true")
     return p.parse_args()
 
 
@@ -194,7 +206,9 @@ def main():
         else:
             bank.feature_update(Xd, 0, nb, True, codes=codes, batch_idx=bidx)
 
-    side = torch.cuda.Stream() if args.overlap else None
+    overlap = (args.overlap == "on" or (args.overlap == "auto" and world == 1 and use_cb)) \
+        and not args.graph
+    side = torch.cuda.Stream() if (overlap or args.overlap_whole) else None
 
     def step(record):
         e = [torch.cuda.Event(enable_timing=True) for _ in range(5)] if record else None
@@ -206,17 +220,19 @@ def main():
             # step's update; the assign writes only batch nodes' codes), then
             # BN statistics + assign on this stream; the fix-up -- with the
             # update's EMA finalize -- after both
-            side.wait_stream(torch.cuda.current_stream())
-            if use_cb:
-                with torch.cuda.stream(side):
-                    wk = kernels.spmm_codebook_walk(adj.rowptr, n, nnz, Xd, F, B, codes,
-                                                    bank.emb_out, D, spmm_plan)
+            if use_cb and not args.overlap_whole:
+                # multi-GPU: the other ranks' previous codes land on the side
+                # stream ahead of the walk; the update's own codes wait for it
+                bank.land_codes_on(side)
+                wk = kernels.spmm_codebook_walk(adj.rowptr, n, nnz, Xd, F, B, codes,
+                                                bank.emb_out, D, spmm_plan, stream=side)
                 vq_update()
-                torch.cuda.current_stream().wait_stream(side)
                 fin = None if args.separate_finalize else bank.take_fused_finalize()
                 fin_fused[0] = fin is not None
-                kernels.spmm_codebook_fixup(wk, finalize=fin)
+                kernels.spmm_codebook_fixup(wk, finalize=fin)     # joins the walk
             else:
+                bank.land_codes_on(side)
+                side.wait_stream(torch.cuda.current_stream())
                 with torch.cuda.stream(side):
                     aggregate(False, None, fuse=False)
                 vq_update()
@@ -438,6 +454,11 @@ def main():
                         aggregation=("codebook_source" if use_cb else "gathered_rows"),
                         ema_finalize=("in the aggregation's fix-up launch" if fin_fused[0]
                                       else "own launch"),
+                        schedule=("aggregation walk on a side stream beside BN statistics + "
+                                  "assign, fix-up after both" if side is not None and use_cb
+                                  and not args.overlap_whole else
+                                  "whole aggregation on a side stream" if side is not None
+                                  else "serial"),
                         B=B, B_prime=n - B, nnz=nnz, F=F, M=M, D=D, W=W,
                         parallelism=f"dp{world}", world=world,
                         backend=(args.backend if comm is not None else None),

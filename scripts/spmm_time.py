@@ -20,7 +20,7 @@ cfg = dict(CONFIGS[name])
 F = cfg["F"]
 if cfg.get("device_build"):
     _, (bidx, subset, adj) = make_batch_device(cfg, device=dev)
-    B, n, nnz = int(bidx.numel()), int(subset.numel()), adj.nnz
+    B, n, nnz = int(bidx.numel()), int(subset.numel()), adj.nnz()
 else:
     g, _, b = make_batch(cfg)
     bidx, subset, adj = batch_to_device(b, dev)

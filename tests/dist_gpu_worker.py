@@ -127,6 +127,30 @@ def main(out_dir):
     sb.sync_codes()
     torch.cuda.synchronize()
     res["stale_final"] = sc.cpu().numpy()
+    # the overlapped step (bench.py --overlap on): the previous exchange lands
+    # on a side stream (VQBank.land_codes_on) where the aggregation's walk then
+    # reads the codes, beside the update on the compute stream; the codes
+    # after every step must equal the serial steps' above, and what the side
+    # stream reads must be the codes the serial step's aggregation reads
+    ob2 = fresh_bank()
+    ob2.comm = CodebookSync(count_group=sync.count_group, capacity=700)
+    oc2 = codes0.to(dev)
+    side = torch.cuda.Stream()
+    for k in range(3):
+        gk = torch.Generator().manual_seed(100 + 10 * k + rank)
+        nodes = sets[rank][k]
+        Xk = torch.randn(nodes.numel(), F, generator=gk).to(dev)
+        Gk = (torch.randn(nodes.numel(), F, generator=gk) * 1e-3).to(dev)
+        ob2.land_codes_on(side)
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            seen = oc2.clone()                     # the walk's view
+        ob2.update(Xk, Gk, 0, nb, True, codes=oc2, batch_idx=nodes.to(dev), defer=True)
+        torch.cuda.current_stream().wait_stream(side)
+        ob2.finish_update()
+        torch.cuda.synchronize()
+        res[f"ostale_{k}"] = oc2.cpu().numpy()
+        res[f"oseen_{k}"] = seen.cpu().numpy()
     res["stale_codes0"] = codes0.numpy()
     for r in range(world):
         for k in range(3):

@@ -124,18 +124,14 @@ def test_walk_beside_update_then_fixup(monkeypatch, M):
     cb = ca.clone()
     pcb = adj.plan_codebook(bt.B, subset, cfg["N"])
     side = torch.cuda.Stream()
-    main = torch.cuda.current_stream()
     for step in range(3):
         a.update(X, G, 0, nb, True, codes=ca, batch_idx=bidx, defer=True)
         out_a = kernels.spmm_codebook(adj.rowptr, bt.n, bt.nnz, X, F, bt.B, ca, a.emb_out, D,
                                       pcb, finalize=a.take_fused_finalize())
         a.finish_update()
-        side.wait_stream(main)
-        with torch.cuda.stream(side):
-            wk = kernels.spmm_codebook_walk(adj.rowptr, bt.n, bt.nnz, X, F, bt.B, cb, b.emb_out,
-                                            D, pcb)
+        wk = kernels.spmm_codebook_walk(adj.rowptr, bt.n, bt.nnz, X, F, bt.B, cb, b.emb_out,
+                                        D, pcb, stream=side)
         b.update(X, G, 0, nb, True, codes=cb, batch_idx=bidx, defer=True)
-        main.wait_stream(side)
         fin = b.take_fused_finalize()
         assert fin is not None
         out_b = kernels.spmm_codebook_fixup(wk, finalize=fin)

@@ -83,6 +83,17 @@ def test_two_ranks_match_union_batch(tmp_path):
             for kk in range(k):
                 np.testing.assert_array_equal(snap[sets[r][kk]], own[r][kk])
     np.testing.assert_array_equal(r0["stale_final"], r1["stale_final"])
+    # the overlapped step's landing: the same codes after every step, and the
+    # side stream saw the serial aggregation's codes on every node outside the
+    # rank's own step-k batch (the nodes an aggregation reads from codes)
+    for r in range(2):
+        for k in range(3):
+            np.testing.assert_array_equal(rs[r][f"ostale_{k}"], rs[r][f"stale_{k}"],
+                                          err_msg=f"rank {r} step {k}")
+            outside = np.setdiff1d(np.arange(codes0.shape[0]), sets[r][k])
+            np.testing.assert_array_equal(rs[r][f"oseen_{k}"][outside],
+                                          rs[r][f"stale_{k}"][outside],
+                                          err_msg=f"rank {r} step {k} (walk's view)")
     for r in range(2):
         for k in range(3):
             np.testing.assert_array_equal(r0["stale_final"][sets[r][k]], own[r][k])

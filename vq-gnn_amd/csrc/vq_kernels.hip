@@ -1542,7 +1542,11 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
                                               (FUSED ? (size_t)M * (W + 1) * 8 : 0))
                    : nullptr;
   const float* E = emb + (int64_t)b * emb_bstride;
-  const int nchunks = (M + chunk - 1) / chunk;
+  // a fused launch holds its whole codebook in one chunk (assign_geom): a
+  // static single pass drops the restaging loop's code and 21 of its 40 SGPR
+  // spills (arxiv update assign 92.5-93.0 against 94.1-96.3 us,
+  // profiles/r06f_assign_single_chunk_ab.txt)
+  const int nchunks = FUSED ? 1 : (M + chunk - 1) / chunk;
   const bool vec_rows = (ldw & 3) == 0 && (emb_bstride & 3) == 0 &&
                         (reinterpret_cast<uintptr_t>(emb) & 15) == 0;
   __shared__ int s_nflag;

@@ -558,31 +558,38 @@ class CodebookWalk:
         self.fixed = False
 
 
-def spmm_codebook_walk(rowptr, n_rows, nnz, X, F, B, codes, emb_out, D, plan_cb, out=None):
-    """spmm_codebook's walk alone, on the current stream (vqgnn_spmm_task_cb_walk,
-    include/vqgnn.h §6b) -> CodebookWalk.  Meant for a second stream beside
-    the VQ update of the same batch (the assign writes only the batch nodes'
-    codes; the walk reads X, the out-of-batch nodes' codes and emb_out), with
-    spmm_codebook_fixup after both.  The rows that span tasks and the empty
-    rows of out are written only by the fix-up."""
+def spmm_codebook_walk(rowptr, n_rows, nnz, X, F, B, codes, emb_out, D, plan_cb, out=None,
+                       stream=None):
+    """spmm_codebook's walk alone (vqgnn_spmm_task_cb_walk, include/vqgnn.h
+    §6b) -> CodebookWalk; spmm_codebook_fixup finishes it.  stream: a second
+    stream to walk on, beside what the caller queues next on its own stream --
+    the VQ update of the same batch (its assign writes only the batch nodes'
+    codes; the walk reads X, the out-of-batch nodes' codes and emb_out).  The
+    walk waits for the caller's stream first; out and the workspace are
+    allocated on the caller's stream, which joins the walk (fix-up) before
+    it can free them.  The rows that span tasks and the empty rows of out are
+    written only by the fix-up."""
     out, ws, args = _cb_prepare(rowptr, n_rows, nnz, X, F, B, codes, emb_out, D, plan_cb, out,
                                 "spmm_codebook_walk")
-    check(lib().vqgnn_spmm_task_cb_walk(*args, stream_ptr()), "spmm_task_cb_walk")
-    return CodebookWalk(out, ws, args, torch.cuda.current_stream())
+    cur = torch.cuda.current_stream()
+    s = cur if stream is None else stream
+    if s != cur:
+        s.wait_stream(cur)
+    with torch.cuda.stream(s):
+        check(lib().vqgnn_spmm_task_cb_walk(*args, stream_ptr()), "spmm_task_cb_walk")
+    return CodebookWalk(out, ws, args, s)
 
 
 def spmm_codebook_fixup(walk, finalize=None):
-    """The fix-up of a CodebookWalk on the current stream (which must already
-    wait for the walk's stream: torch's wait_stream), with the pending EMA
-    finalize inside it as in spmm_codebook -> out, equal bit for bit to
-    spmm_codebook's.  The walk's buffers are marked in use by this stream
-    for the caching allocator."""
+    """The fix-up of a CodebookWalk on the current stream, after the walk (the
+    current stream waits for the walk's), with the pending EMA finalize
+    inside it as in spmm_codebook -> out, equal bit for bit to
+    spmm_codebook's."""
     if walk.fixed:
         raise RuntimeError("spmm_codebook_fixup: this walk was fixed up already")
     cur = torch.cuda.current_stream()
-    if cur != walk.stream:
-        walk.out.record_stream(cur)
-        walk.ws.record_stream(cur)
+    if walk.stream != cur:
+        cur.wait_stream(walk.stream)
     L = lib()
     rec = None if finalize is None else _finalize_record(finalize)
     check(L.vqgnn_spmm_task_cb_fixup(*walk.args, ctypes.byref(rec) if rec is not None else None,

@@ -155,10 +155,34 @@ class VQBank(nn.Module):
     def sync_codes(self):
         """Land the other ranks' codes of the last update (multi-GPU); a no-op
         on one GPU.  Called before the next VQ call and by the layer after its
-        aggregation, so the exchange overlaps the gather + SpMM."""
+        aggregation, so the exchange overlaps the gather + SpMM.  After
+        land_codes_on(stream) the current stream waits for that landing."""
+        ev, self._codes_landed = self._codes_landed, None
+        if ev is not None:
+            torch.cuda.current_stream().wait_event(ev)
         p, self._pending_codes = self._pending_codes, None
         if p is not None:
             p.wait()
+
+    _codes_landed = None
+
+    def land_codes_on(self, stream):
+        """Multi-GPU, the overlapped step (an aggregation walk on `stream`
+        beside the next update): land the last update's code exchange on
+        `stream`, ahead of the walk that reads the codes there.  The next
+        sync_codes() -- the update's, before it scatters its own codes --
+        makes its stream wait for this landing, so the order of the code
+        writes (the other ranks' previous codes, then this rank's new ones)
+        is the serial step's.  A no-op when nothing is pending."""
+        if self._pending_codes is None:
+            return
+        stream.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(stream):
+            p, self._pending_codes = self._pending_codes, None
+            p.wait()
+            ev = torch.cuda.Event()
+            ev.record(stream)
+        self._codes_landed = ev
 
     def _exchange_codes(self, batch_idx, local, codes, max_B):
         """Own codes now (scattered by the pack kernel), everyone's
