@@ -76,6 +76,8 @@ def parse():
     # (study) the whole aggregation -- walk and fix-up -- on the side stream,
     # the EMA finalize in its own launch after the join
     p.add_argument("--overlap-whole", action="store_true")
+    # (study) the walk queued after the update's BatchNorm launches
+    p.add_argument("--walk-after-bn", action="store_true")
     return p.parse_args()
 
 
@@ -200,11 +202,13 @@ def main():
 
     ev = []
 
-    def vq_update():
+    def vq_update(before_assign=None):
         if W == 2 * D:
-            bank.update(Xd, Gd, 0, nb, True, codes=codes, batch_idx=bidx, defer=True)
+            bank.update(Xd, Gd, 0, nb, True, codes=codes, batch_idx=bidx, defer=True,
+                        before_assign=before_assign)
         else:
-            bank.feature_update(Xd, 0, nb, True, codes=codes, batch_idx=bidx)
+            bank.feature_update(Xd, 0, nb, True, codes=codes, batch_idx=bidx,
+                                before_assign=before_assign)
 
     overlap = (args.overlap == "on" or (args.overlap == "auto" and world == 1 and use_cb)) \
         and not args.graph
@@ -224,9 +228,13 @@ def main():
                 # multi-GPU: the other ranks' previous codes land on the side
                 # stream ahead of the walk; the update's own codes wait for it
                 bank.land_codes_on(side)
+                # the walk queued first (--walk-after-bn: from the update's
+                # before_assign hook, after its BatchNorm launches; measured
+                # 1.7 % slower)
                 wk = kernels.spmm_codebook_walk(adj.rowptr, n, nnz, Xd, F, B, codes,
-                                                bank.emb_out, D, spmm_plan, stream=side)
-                vq_update()
+                                                bank.emb_out, D, spmm_plan, stream=side,
+                                                deferred=args.walk_after_bn)
+                vq_update(before_assign=wk.launch)
                 fin = None if args.separate_finalize else bank.take_fused_finalize()
                 fin_fused[0] = fin is not None
                 kernels.spmm_codebook_fixup(wk, finalize=fin)     # joins the walk

@@ -32,7 +32,7 @@ log rocprof
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -T -d $O/prof -o run --output-format csv \
   -- python bench.py --steps 30 --warmup 5 --no-cpu-baseline --pmc-json $O/pmc_latest.json > $O/prof_bench.log 2>&1 || stop $?
 log variants
-for v in "--config arxiv_gcn --semantics feature_update" "--config arxiv_gat" "--config ppi_sage"; do
+for v in "--config arxiv_gcn --semantics feature_update" "--config arxiv_gat" "--config ppi_sage" "--config reddit_gcn"; do
   timeout -k 10 400 python -u bench.py --steps 20 --warmup 5 $v >> $O/bench_variants.jsonl.log 2>&1 || stop $?
 done
 grep -h '^{' $O/bench_variants.jsonl.log | cut -c1-300

@@ -101,14 +101,16 @@ def test_finalize_fused_into_codebook_spmm(monkeypatch, semantics, M):
     b.check_bad_init()
 
 
-@pytest.mark.parametrize("M", [256, 1024])
-def test_walk_beside_update_then_fixup(monkeypatch, M):
+@pytest.mark.parametrize("M,deferred", [(256, True), (256, False), (1024, True)])
+def test_walk_beside_update_then_fixup(monkeypatch, M, deferred):
     """The overlapped step (bench.py's default): the codebook-source walk on a
     side stream (vqgnn_spmm_task_cb_walk) beside the VQ update on the main
     stream, then the fix-up with the update's EMA finalize
     (vqgnn_spmm_task_cb_fixup) after both -- the SpMM output and every piece
     of VQ state bit-identical to the serial update + spmm_codebook(finalize)
-    form, step after step.  M = 1,024: the finalize's two-kernel form."""
+    form, step after step.  M = 1,024: the finalize's two-kernel form.
+    deferred: the walk queued from the update's before_assign hook, after the
+    BatchNorm launches (bench.py's order)."""
     from vq_gnn_amd import graph, kernels
     monkeypatch.setattr(vqmod, "STRICT_BAD_INIT", False)
     cfg = dict(graph.CONFIGS["arxiv_gcn"])
@@ -130,8 +132,10 @@ def test_walk_beside_update_then_fixup(monkeypatch, M):
                                       pcb, finalize=a.take_fused_finalize())
         a.finish_update()
         wk = kernels.spmm_codebook_walk(adj.rowptr, bt.n, bt.nnz, X, F, bt.B, cb, b.emb_out,
-                                        D, pcb, stream=side)
-        b.update(X, G, 0, nb, True, codes=cb, batch_idx=bidx, defer=True)
+                                        D, pcb, stream=side, deferred=deferred)
+        b.update(X, G, 0, nb, True, codes=cb, batch_idx=bidx, defer=True,
+                 before_assign=wk.launch if deferred else None)
+        assert wk.launched
         fin = b.take_fused_finalize()
         assert fin is not None
         out_b = kernels.spmm_codebook_fixup(wk, finalize=fin)

@@ -550,34 +550,52 @@ def spmm_codebook(rowptr, n_rows, nnz, X, F, B, codes, emb_out, D, plan_cb, out=
 
 
 class CodebookWalk:
-    """A codebook-source aggregation whose walk is queued and whose fix-up is
-    not (spmm_codebook_walk -> spmm_codebook_fixup)."""
+    """A codebook-source aggregation whose walk is queued (or ready to be) and
+    whose fix-up is not (spmm_codebook_walk -> spmm_codebook_fixup)."""
 
-    def __init__(self, out, ws, args, stream):
-        self.out, self.ws, self.args, self.stream = out, ws, args, stream
-        self.fixed = False
+    def __init__(self, out, ws, args, stream, fork):
+        self.out, self.ws, self.args, self.stream, self.fork = out, ws, args, stream, fork
+        self.launched = self.fixed = False
+
+    def launch(self):
+        """Queue the walk on its stream, after the caller's stream as it was
+        when the walk was created (the fork event): work queued on the
+        caller's stream since then runs beside it."""
+        if self.launched:
+            return
+        if self.fork is not None:
+            self.stream.wait_event(self.fork)
+        with torch.cuda.stream(self.stream):
+            check(lib().vqgnn_spmm_task_cb_walk(*self.args, stream_ptr()), "spmm_task_cb_walk")
+        self.launched = True
 
 
 def spmm_codebook_walk(rowptr, n_rows, nnz, X, F, B, codes, emb_out, D, plan_cb, out=None,
-                       stream=None):
+                       stream=None, deferred=False):
     """spmm_codebook's walk alone (vqgnn_spmm_task_cb_walk, include/vqgnn.h
     §6b) -> CodebookWalk; spmm_codebook_fixup finishes it.  stream: a second
     stream to walk on, beside what the caller queues next on its own stream --
     the VQ update of the same batch (its assign writes only the batch nodes'
     codes; the walk reads X, the out-of-batch nodes' codes and emb_out).  The
-    walk waits for the caller's stream first; out and the workspace are
-    allocated on the caller's stream, which joins the walk (fix-up) before
-    it can free them.  The rows that span tasks and the empty rows of out are
-    written only by the fix-up."""
+    walk runs after the caller's stream as it is now (an event); out and the
+    workspace are allocated on the caller's stream before that event, which
+    joins the walk (fix-up) before it can free them.  deferred: create the
+    walk now, queue it later with .launch() (e.g. VQBank.update's
+    before_assign, so the update's BatchNorm pass is queued first and runs
+    while the walk's launch crosses streams).  The rows that span tasks and
+    the empty rows of out are written only by the fix-up."""
     out, ws, args = _cb_prepare(rowptr, n_rows, nnz, X, F, B, codes, emb_out, D, plan_cb, out,
                                 "spmm_codebook_walk")
     cur = torch.cuda.current_stream()
     s = cur if stream is None else stream
+    fork = None
     if s != cur:
-        s.wait_stream(cur)
-    with torch.cuda.stream(s):
-        check(lib().vqgnn_spmm_task_cb_walk(*args, stream_ptr()), "spmm_task_cb_walk")
-    return CodebookWalk(out, ws, args, s)
+        fork = torch.cuda.Event()
+        fork.record(cur)
+    walk = CodebookWalk(out, ws, args, s, fork)
+    if not deferred:
+        walk.launch()
+    return walk
 
 
 def spmm_codebook_fixup(walk, finalize=None):
@@ -587,6 +605,7 @@ def spmm_codebook_fixup(walk, finalize=None):
     spmm_codebook's."""
     if walk.fixed:
         raise RuntimeError("spmm_codebook_fixup: this walk was fixed up already")
+    walk.launch()                           # (a deferred walk nobody launched)
     cur = torch.cuda.current_stream()
     if walk.stream != cur:
         cur.wait_stream(walk.stream)

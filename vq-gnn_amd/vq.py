@@ -292,8 +292,11 @@ class VQBank(nn.Module):
             return False
         return kernels.bn_fold_supported(B, nbr, self.D, self.M, W)
 
-    def feature_update(self, X, b0, nbr, training, idx_out=None, codes=None, batch_idx=None):
-        """vq.py:160-202 for branches [b0, b0+nbr): X is [B, nbr*D] (a row-major view)."""
+    def feature_update(self, X, b0, nbr, training, idx_out=None, codes=None, batch_idx=None,
+                       before_assign=None):
+        """vq.py:160-202 for branches [b0, b0+nbr): X is [B, nbr*D] (a row-major view).
+        before_assign: called after the BatchNorm launches, before the
+        assign's (update())."""
         self.finish_update()
         exchanging = training and self.comm is not None and codes is not None
         if not exchanging:
@@ -330,6 +333,8 @@ class VQBank(nn.Module):
         slab = self._slab(D, b0, nbr) if training else None
         local = None
         cap = max_B if comm is not None else None
+        if before_assign is not None:
+            before_assign()
         if comm is not None and codes is not None:
             local = self._local_codes(B, nbr, X.device)
             stats = self._assign_capped(X, None, coef, 1.0, self.emb[sl], D, idx_out, local,
@@ -380,7 +385,7 @@ class VQBank(nn.Module):
         return FusedFinalize(self, p)
 
     def update(self, X, G, b0, nbr, training, idx_out=None, codes=None, batch_idx=None,
-               defer=False):
+               defer=False, before_assign=None):
         """vq.py:204-279 for branches [b0, b0+nbr): X, G are [B, nbr*D] views.
 
         defer=True (training): return after the assign with the finalize
@@ -393,7 +398,12 @@ class VQBank(nn.Module):
         Multi-GPU, the previous update's code exchange is landed after this
         update's assign, just before its own codes are scattered (the assign
         reads no codes): the all_gather then overlaps the caller's gather +
-        SpMM and this update's statistics and assign."""
+        SpMM and this update's statistics and assign.
+
+        before_assign: called after the BatchNorm launches, before the
+        assign's -- where bench.py queues the aggregation's walk on a side
+        stream (kernels.spmm_codebook_walk(deferred=True).launch), so the
+        BatchNorm pass runs while the walk's launch crosses streams."""
         self.finish_update()
         exchanging = training and self.comm is not None and codes is not None
         if not exchanging:
@@ -439,6 +449,8 @@ class VQBank(nn.Module):
         slab = self._slab(2 * D, b0, nbr) if training else None
         local = None
         cap = max_B if comm is not None else None
+        if before_assign is not None:
+            before_assign()
         if comm is not None and codes is not None:
             local = self._local_codes(B, nbr, X.device)
             stats = self._assign_capped(X, G, coef, scale, self.emb[sl], 2 * D, idx_out, local,
