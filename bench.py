@@ -14,8 +14,8 @@ With update() semantics the EMA finalize is queued after (ii): the
 aggregation reads the codebook from before this step's update, as the
 reference's forward does (its update runs in the backward hook,
 models.py:181-185); one process runs it inside the aggregation's fix-up
-launch, and (--overlap auto) the aggregation's walk on a side stream beside
-(i)'s BN statistics and assign, the fix-up after both.  With N > 1 the
+launch (--overlap on: the aggregation's walk on a side stream beside (i)'s
+BN statistics and assign, the fix-up after both).  With N > 1 the
 all-reduce of the EMA statistics overlaps (ii).
 value = edges of all ranks / time.  Inputs are resident in HBM before timing.
 
@@ -67,12 +67,13 @@ def parse():
     # aggregation's fix-up launch (vqgnn_spmm_task_cb_fin);
     # --separate-finalize: its own launch after the aggregation
     p.add_argument("--separate-finalize", action="store_true")
-    # the codebook-source walk on a side stream beside BN statistics + assign
-    # (data-independent; the fix-up with the EMA finalize joins both):
-    # auto = on for one process with the codebook source,
-    # off = the serial step; on = also for N > 1 (the code exchange lands on
-    # the side stream, VQBank.land_codes_on)
-    p.add_argument("--overlap", default="auto", choices=["auto", "on", "off"])
+    # on: the codebook-source walk on a side stream beside BN statistics +
+    # assign (data-independent; the fix-up with the EMA finalize joins both;
+    # N > 1: the code exchange lands on the side stream, VQBank.land_codes_on).
+    # 2 % faster at N = 1, but the assign then waits for CUs behind the walk
+    # and its event-timed duration (the roofline kernel's) grows from 87 to
+    # ~144 us, so the default is the serial step
+    p.add_argument("--overlap", default="off", choices=["on", "off"])
     # (study) the whole aggregation -- walk and fix-up -- on the side stream,
     # the EMA finalize in its own launch after the join
     p.add_argument("--overlap-whole", action="store_true")
@@ -210,8 +211,7 @@ def main():
             bank.feature_update(Xd, 0, nb, True, codes=codes, batch_idx=bidx,
                                 before_assign=before_assign)
 
-    overlap = (args.overlap == "on" or (args.overlap == "auto" and world == 1 and use_cb)) \
-        and not args.graph
+    overlap = args.overlap == "on" and use_cb and not args.graph
     side = torch.cuda.Stream() if (overlap or args.overlap_whole) else None
 
     def step(record):

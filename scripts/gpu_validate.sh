@@ -1,8 +1,8 @@
 #!/bin/bash
 # Full validation of the library on one box: smoke, every -m gpu test, then
 # (PART=measure) the PMC passes of the bench step (-> pmc_latest.json stamped
-# with this library), the bench line with them, its rocprofv3 kernel stats and
-# the config variants.  Every GPU step has its own time limit; a crash / abort /
+# with this library; PMC_JSON=<file>: reuse that stamp), the bench line with
+# them, its rocprofv3 kernel stats and the config variants.  Every GPU step has its own time limit; a crash / abort /
 # time-limit kill (exit > 1) ends the script.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -21,10 +21,14 @@ if [ "${PART:-tests}" = tests ]; then
   rc=$?; grep -E "passed|failed" $O/pytest_gpu.log | tail -1; grep -E "FAILED|Error" $O/pytest_gpu.log | head -5
   stop $rc
 fi
-log pmc
-TAG=${TAG}_pmc TARGET=step bash scripts/gpu_pmc.sh > $O/pmc.log 2>&1 || stop $?
-python scripts/pmc_summary.py gpurun_out/pmc_${TAG}_pmc > $O/pmc_summary.txt
-python scripts/pmc_to_json.py gpurun_out/pmc_${TAG}_pmc/summary.json $O/pmc_latest.json arxiv_gcn update > /dev/null
+if [ -n "$PMC_JSON" ]; then          # counters of this library collected already
+  cp "$PMC_JSON" $O/pmc_latest.json
+else
+  log pmc
+  TAG=${TAG}_pmc TARGET=step bash scripts/gpu_pmc.sh > $O/pmc.log 2>&1 || stop $?
+  python scripts/pmc_summary.py gpurun_out/pmc_${TAG}_pmc > $O/pmc_summary.txt
+  python scripts/pmc_to_json.py gpurun_out/pmc_${TAG}_pmc/summary.json $O/pmc_latest.json arxiv_gcn update > /dev/null
+fi
 log bench
 timeout -k 10 400 python -u bench.py --steps 30 --warmup 5 --pmc-json $O/pmc_latest.json > $O/bench.log 2>&1 || stop $?
 grep -h '^{' $O/bench.log | cut -c1-400
