@@ -37,6 +37,7 @@
 namespace vqgnn {
 
 constexpr int kTaskThreads = 256;             // 4 waves
+constexpr unsigned kRoundRobinGrid = 1u << 16; // task-kernel grids this large skip xcd_remap
 constexpr uint32_t kColMask = (1u << 26) - 1;
 constexpr uint32_t kEndBit = 1u << 31;
 constexpr int kSkipShift = 26;
@@ -585,9 +586,25 @@ spmm_task_kernel(TaskArgs a) {
   // wave-uniform in an SGPR: the record buffer resource built from it is then
   // scalar (a VGPR-derived resource costs a readfirstlane loop per block)
 #ifdef VQGNN_EXPERIMENTS
-  const int blk = a.xcd ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+  // VQGNN_TASK_XCD: 1 contiguous eighths, 0 round-robin, C > 1 chunks of C
+  // workgroups dealt to the XCDs in turn (XCD x: chunks x, x + 8, ...)
+  int blk;
+  if (a.xcd == 1) {
+    blk = xcd_remap(blockIdx.x, gridDim.x);
+  } else if (a.xcd > 1) {
+    const int p = blockIdx.x, C = a.xcd, full = (int)gridDim.x / (8 * C) * (8 * C);
+    const int local = p / 8;
+    blk = p < full ? ((local / C) * 8 + p % 8) * C + local % C : p;
+  } else {
+    blk = (int)blockIdx.x;
+  }
 #else
-  const int blk = xcd_remap(blockIdx.x, gridDim.x);
+  // XCD-contiguous eighths of the tasks (each XCD's L2 keeps its rows'
+  // cluster), except for grids of 2^16 workgroups and more (> 33 M edges),
+  // where the dispatcher's round-robin order balances the XCDs' mix of rows
+  // (reddit layer 2: 4,072-4,093 against 4,348-4,374 us; arxiv, contiguous:
+  // 74 against 106 us round-robin; profiles/r06n_task_xcd_chunks.txt)
+  const int blk = gridDim.x >= kRoundRobinGrid ? (int)blockIdx.x : xcd_remap(blockIdx.x, gridDim.x);
 #endif
   const int wv = __builtin_amdgcn_readfirstlane(blk * (kTaskThreads / 64) + (threadIdx.x >> 6));
   const int nnz = call_nnz(a);
