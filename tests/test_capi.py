@@ -156,6 +156,33 @@ def test_fused_finalize_entry_checks_the_finalize_first():
     assert rc == 1 and b"stat_count" in h.vqgnn_last_error()
 
 
+def test_split_walk_and_fixup_check_like_the_one_call_entry():
+    """vqgnn_spmm_task_cb_walk / _fixup (the walk beside the VQ update, its
+    fix-up after both) run the one-call entry's checks before any launch:
+    the branch bound, the tile limits, and (fix-up) the finalize record."""
+    import ctypes
+    h = L.lib()
+    # F / D = 32 code columns against 16 branches: both halves refuse
+    bad = (16, 100, 1000, 50, 16, 128, 128, 16, 32, 1000, 16, 8, 256 * 8, 16, 256, 4, 16, 128,
+           16, 16, 64, 0, 0, 16)
+    assert h.vqgnn_spmm_task_cb_walk(*bad, None) == 1
+    assert b"branches" in h.vqgnn_last_error()
+    assert h.vqgnn_spmm_task_cb_fixup(*bad, None, None) == 1
+    assert b"branches" in h.vqgnn_last_error()
+    # M past the widest image
+    big = bad[:13] + (32, 1281) + bad[15:]
+    assert h.vqgnn_spmm_task_cb_walk(*big, None) == 1 and b"image" in h.vqgnn_last_error()
+    # the fix-up checks the finalize record first, as vqgnn_spmm_task_cb_fin
+    fin = L.EmaFinalizeArgs(ema_parts=16, nparts=1, zero_after=1, stat_count=100, nb=32, M=256,
+                            D=4, W=6, ldw=8, decay=0.99, laplace=1, grad_scale=1.0,
+                            epsilon=1e-5, cluster_size=16, cs_bstride=256, ema_w=16,
+                            embedding=16, embedding_output=16, emb_bstride=2048, rm_f=16,
+                            rv_f=16, rm_g=16, rv_g=16, bad_init=16)
+    good = bad[:13] + (32,) + bad[14:]
+    assert h.vqgnn_spmm_task_cb_fixup(*good, ctypes.byref(fin), None) == 1
+    assert b"W must be D or 2D" in h.vqgnn_last_error()
+
+
 def test_default_library_reads_no_measurement_knobs():
     """The shipped library never reads the measurement knobs that cut work
     short or drop stores (VQGNN_TASK_DBG, VQGNN_ASSIGN_MSWEEP, the schedule
