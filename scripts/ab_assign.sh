@@ -8,7 +8,7 @@ O=gpurun_out/${TAG:-ab}
 mkdir -p $O
 VARS="$1"
 CFGS="${2:-arxiv_gcn:update}"
-for rep in 1 2; do
+for rep in ${REPS:-1 2}; do
   for cs in $CFGS; do
     cfg=${cs%%:*}; sem=${cs#*:}
     for n in $VARS; do

@@ -394,7 +394,11 @@ __device__ __forceinline__ void task_walk(const TaskArgs& a, int wv, int nwaves,
       // codes first (an X edge's offset is out of range: no access), then
       // the X rows, then -- once the codes are in -- the codewords from LDS;
       // lane k's float4 is column 4 (32 tile + k): branch (4 (32 tile + k)) / D
+      // the block's loads at raised wave priority, so they are in flight
+      // before other waves' fma chains take the issue port (codebook SpMM
+      // 79.8-80.9 against 81.1-82.8 us, profiles/r06t_setprio_ab.txt)
       uint32_t cd[U];
+      __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int u = 0; u < U; ++u)
         cd[u] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(
@@ -409,6 +413,7 @@ __device__ __forceinline__ void task_walk(const TaskArgs& a, int wv, int nwaves,
         if (bk.co[u] < 0)
           v[u][0] = *reinterpret_cast<const float4*>(cb_img + min(cd[u] & 0xffffu, cb_m) * (16u * G) +
                                                      lane16);
+      __builtin_amdgcn_s_setprio(0);
       return;
     }
 #pragma unroll

@@ -1803,6 +1803,13 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
           for (int g = 0; g < 4; ++g) d0[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, bop[g], zero, 0, 0, 0);
 #pragma unroll
           for (int g = 0; g < 4; ++g) d1[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, bop[g], zero, 0, 0, 0);
+          // the fold at raised wave priority: a wave whose MFMA results are
+          // in gets its VALU issued first and returns to the matrix pipe
+          // sooner (arxiv_gat assign 220-224 against 234-236 us, ppi 540-542
+          // against 562-566, arxiv 86-88 against 89.5-90;
+          // profiles/r06t_setprio_ab.txt; raised while issuing the MFMAs
+          // instead: no gain, r06s_assign_setprio_ab.txt)
+          __builtin_amdgcn_s_setprio(1);
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
             // by value: clang's __builtin_bit_cast of a vector-element
@@ -1817,6 +1824,7 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
           }
           __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);    // the 8 MFMAs first
           __builtin_amdgcn_sched_group_barrier(0x002, 40, 0);   // then the VALU
+          __builtin_amdgcn_s_setprio(0);
         } else {   // WM 0 (any W): one tile's accumulators at a time (> 128 VGPRs otherwise)
           uint32_t m4[4];
           {
