@@ -45,5 +45,6 @@ for _ in range(3):
     ts.append(e0.elapsed_time(e1) / reps * 1e3)
 alg = 4 * (n + 1) + 8 * nnz + 8 * n * F
 print(f"{name} {os.path.basename(os.environ.get('VQGNN_LIB', 'libvqgnn.so'))}: "
-      f"{min(ts):8.1f} us  frac {alg / min(ts) / 8e6:.3f}  ({', '.join(f'{t:.1f}' for t in ts)})",
+      f"{min(ts):8.1f} us  frac {alg / min(ts) / 8e6:.3f}  ({', '.join(f'{t:.1f}' for t in ts)})"
+      f"  checksum {float(out.double().sum()):.6e}",
       flush=True)

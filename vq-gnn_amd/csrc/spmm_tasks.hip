@@ -202,6 +202,16 @@ __global__ void task_jobs_kernel(const int32_t* __restrict__ rowptr, int n_rows,
 }
 
 // ---- main kernel ---------------------------------------------------------
+// Cache-policy bits (buffer instruction aux: 1 sc0, 2 nt, 16 sc1) of the
+// record loads and the output-row stores; 0 = the default policy
+#ifndef VQGNN_REC_AUX
+#define VQGNN_REC_AUX 0
+#endif
+#ifndef VQGNN_OUT_AUX
+#define VQGNN_OUT_AUX 0
+#endif
+typedef int v4i __attribute__((ext_vector_type(4)));
+
 // Source of record word x (column j = x & kColMask).  Near path: one 24-bit
 // multiply-add, j * ld + base, with (ld, base) = (ldxb, offx + lane_off) or
 // (ldx2b, offx2 - B * ldx2b + lane_off) (mod 2^32; task_setup guarantees
@@ -326,6 +336,10 @@ __device__ __forceinline__ void task_walk(const TaskArgs& a, int wv, int nwaves,
   float4 acc[NC];
 #pragma unroll
   for (int i = 0; i < NC; ++i) acc[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  // output rows through a buffer resource when a store cache policy is set
+  // (near path: row offsets below 4 GiB)
+  const __amdgpu_buffer_rsrc_t rso =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.out, 0, (int)0xFFFFFFFFu, 0x00020000);
 
   // Records: lane k < U of a group holds the record of edge e + k of the
   // current block (one coalesced 8-byte load per lane); step u reads edge
@@ -339,7 +353,7 @@ __device__ __forceinline__ void task_walk(const TaskArgs& a, int wv, int nwaves,
   // so no wait for it sits between a block's gathers and the next block's.
   auto load_rec = [&](int e) -> int2 {
     return __builtin_bit_cast(
-        int2, __builtin_amdgcn_raw_buffer_load_b64(rsr, (uint32_t)(e - wbase + k) * 8u, 0, 0));
+        int2, __builtin_amdgcn_raw_buffer_load_b64(rsr, (uint32_t)(e - wbase + k) * 8u, 0, VQGNN_REC_AUX));
   };
   auto mask_rec = [&](int2 q, int e) -> int2 {
     const int eu = e + k;
@@ -475,8 +489,20 @@ __device__ __forceinline__ void task_walk(const TaskArgs& a, int wv, int nwaves,
         }
 #pragma unroll
         for (int i = 0; i < NC; ++i) {
-          if (pv[i] && !(a.dbg & 1))
-            *reinterpret_cast<float4*>(dst + 4 * (c4base + G * i)) = acc[i];
+          if (pv[i] && !(a.dbg & 1)) {
+            if constexpr (VQGNN_OUT_AUX != 0 && !FAR) {
+              if (!head) {
+                __builtin_amdgcn_raw_buffer_store_b128(
+                    __builtin_bit_cast(v4i, acc[i]), rso,
+                    (uint32_t)__umul24((uint32_t)r, a.ldob) + 16u * (uint32_t)(c4base + G * i), 0,
+                    VQGNN_OUT_AUX);
+              } else {
+                *reinterpret_cast<float4*>(dst + 4 * (c4base + G * i)) = acc[i];
+              }
+            } else {
+              *reinterpret_cast<float4*>(dst + 4 * (c4base + G * i)) = acc[i];
+            }
+          }
           acc[i] = make_float4(0.f, 0.f, 0.f, 0.f);
         }
         const uint32_t skip = (x >> kSkipShift) & kSkipEsc;
