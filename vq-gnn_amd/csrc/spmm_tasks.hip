@@ -210,6 +210,11 @@ __global__ void task_jobs_kernel(const int32_t* __restrict__ rowptr, int n_rows,
 #ifndef VQGNN_OUT_AUX
 #define VQGNN_OUT_AUX 0
 #endif
+// 1: the two-source walk issues a block's gathers at raised wave priority
+// (as the codebook walk does); experiments builds only
+#ifndef VQGNN_TASK_PRIO
+#define VQGNN_TASK_PRIO 0
+#endif
 typedef int v4i __attribute__((ext_vector_type(4)));
 
 // Source of record word x (column j = x & kColMask).  Near path: one 24-bit
@@ -430,6 +435,7 @@ __device__ __forceinline__ void task_walk(const TaskArgs& a, int wv, int nwaves,
       __builtin_amdgcn_s_setprio(0);
       return;
     }
+    if constexpr (VQGNN_TASK_PRIO != 0) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
 #pragma unroll
@@ -447,6 +453,7 @@ __device__ __forceinline__ void task_walk(const TaskArgs& a, int wv, int nwaves,
         }
       }
     }
+    if constexpr (VQGNN_TASK_PRIO != 0) __builtin_amdgcn_s_setprio(0);
   };
   auto consume = [&](int e, const Blk& bk, const float4 (&v)[U][NC]) {
 #pragma unroll
