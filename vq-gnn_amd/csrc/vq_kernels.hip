@@ -1422,6 +1422,24 @@ __device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
 // 4 (t ^ (pair >> 1 & 1)) + quad: 16 slots over the 32 (pair, quad) sets of
 // a 256-codeword chunk instead of 8, fewer lanes of a 16-lane group on one
 // bank.  Runs of 4 stay contiguous; chunks are multiples of 32 codewords.
+// Wave priorities (s_setprio) of the filter's phases in the single-pass
+// instances: the sweep's fold at 2, the row phase (row loads, BatchNorm
+// apply, f16 split, B fragments) at 1, the resolve not raised -- arxiv
+// assign 87.0-88.0 against 89.9-91.4 us, arxiv_gat 216.0-219.3 against
+// 220.0-225.0 us (profiles/r06y2_assign_phase_prio_ab.txt).  The chunk-outer
+// (CO) instances keep the fold at 1 and the row phase at 0: ppi's assign
+// was 1 % slower with the raised row phase.  Compile-time; experiments
+// builds set them (VQGNN_ASG_FOLD_PRIO / _ROW_PRIO / _RES_PRIO).
+#ifndef VQGNN_ASG_FOLD_PRIO
+#define VQGNN_ASG_FOLD_PRIO 2
+#endif
+#ifndef VQGNN_ASG_ROW_PRIO
+#define VQGNN_ASG_ROW_PRIO 1
+#endif
+#ifndef VQGNN_ASG_RES_PRIO
+#define VQGNN_ASG_RES_PRIO 0
+#endif
+
 __device__ __forceinline__ int flt_pos(int m) { return m ^ (((m >> 6) & 1) << 4); }
 
 // stage codebook rows [mc0, mc0 + chunk + slack) of E: planes -2 e_hi,
@@ -1523,6 +1541,8 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
                  BnFold fold, unsigned long long* __restrict__ co_state, int co_pass) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int NT = WV * 64;
+  constexpr int kFoldPrio = CO ? 1 : VQGNN_ASG_FOLD_PRIO;   // wave priorities (above)
+  constexpr int kRowPrio = CO ? 0 : VQGNN_ASG_ROW_PRIO;
   const int W = WM == 2 ? 8 : (WM == 1 ? 4 : W_);          // compile-time in the row modes
   const int D = WM != 0 ? 4 : D_;
   const int F = nb * D;
@@ -1713,6 +1733,7 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
     half8 bop[4];
     float xr[8];                                      // the row: scores, resolve, EMA
     const int64_t node = nid;
+    if constexpr (kRowPrio != 0) __builtin_amdgcn_s_setprio(kRowPrio);
     {
       float (&xv)[8] = xr;
       sx = row_vals(raw, xv);
@@ -1755,6 +1776,7 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
       for (int g = 0; g < 4; ++g)
         bop[g] = __builtin_bit_cast(half8, uint4{bw[g][0], bw[g][1], bw[g][2], bw[g][3]});
     }
+    if constexpr (kRowPrio != 0) __builtin_amdgcn_s_setprio(0);
     float best = INFINITY;
     int bidx = 0;
     bool ntie = !(sx < 65536.f);
@@ -1809,7 +1831,7 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
           // against 562-566, arxiv 86-88 against 89.5-90;
           // profiles/r06t_setprio_ab.txt; raised while issuing the MFMAs
           // instead: no gain, r06s_assign_setprio_ab.txt)
-          __builtin_amdgcn_s_setprio(1);
+          __builtin_amdgcn_s_setprio(kFoldPrio);
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
             // by value: clang's __builtin_bit_cast of a vector-element
@@ -1876,6 +1898,7 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
       // ---- hand the owner lane the four quads' statistics of its row: a
       // 4 x 4 transpose over (quad, group); keys carry their quad (index order
       // = pair, then quad)
+      if constexpr (VQGNN_ASG_RES_PRIO != 0) __builtin_amdgcn_s_setprio(VQGNN_ASG_RES_PRIO);
       uint32_t kk[4];
 #pragma unroll
       for (int g = 0; g < 4; ++g) kk[g] = ((cb[g] & pmask) << 2) | (uint32_t)q;
@@ -1976,6 +1999,7 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
         }
       }
       }
+      if constexpr (VQGNN_ASG_RES_PRIO != 0) __builtin_amdgcn_s_setprio(0);
       if (dm < best) {                                // earlier chunk wins ties
         best = dm;
         bidx = mc0 + im;
