@@ -1439,6 +1439,9 @@ __device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
 #ifndef VQGNN_ASG_RES_PRIO
 #define VQGNN_ASG_RES_PRIO 0
 #endif
+#ifndef VQGNN_ASG_OUT_PRIO
+#define VQGNN_ASG_OUT_PRIO 0
+#endif
 
 __device__ __forceinline__ int flt_pos(int m) { return m ^ (((m >> 6) & 1) << 4); }
 
@@ -2017,6 +2020,7 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
     // ---- outputs (owner lane); a near-tie row is appended to the
     // workgroup's list instead (resolved after the row loop)
     const bool near_tie = live && ntie;
+    if constexpr (VQGNN_ASG_OUT_PRIO != 0) __builtin_amdgcn_s_setprio(VQGNN_ASG_OUT_PRIO);
     if (live && !ntie) {
       if (idx_out) idx_out[(int64_t)b * B + row0 + lane] = (int64_t)bidx;
       if (idx32) idx32[(int64_t)b * B + row0 + lane] = bidx;
@@ -2038,6 +2042,7 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
           if (k < W) atomicAdd(a + 1 + k, to_fixed(xr[k], (W != D && k >= D) ? shift_g : shift_f));
       }
     }
+    if constexpr (VQGNN_ASG_OUT_PRIO != 0) __builtin_amdgcn_s_setprio(0);
   }
 
   // ---- near-tie rows of this workgroup: one wave per row sweeps every
