@@ -215,6 +215,11 @@ __global__ void task_jobs_kernel(const int32_t* __restrict__ rowptr, int n_rows,
 #ifndef VQGNN_TASK_PRIO
 #define VQGNN_TASK_PRIO 0
 #endif
+// the codebook walk's consume (fma chain, row stores) at this wave priority
+// (0: not raised; experiments builds)
+#ifndef VQGNN_CB_CONS_PRIO
+#define VQGNN_CB_CONS_PRIO 0
+#endif
 typedef int v4i __attribute__((ext_vector_type(4)));
 
 // Source of record word x (column j = x & kColMask).  Near path: one 24-bit
@@ -456,6 +461,7 @@ __device__ __forceinline__ void task_walk(const TaskArgs& a, int wv, int nwaves,
     if constexpr (VQGNN_TASK_PRIO != 0) __builtin_amdgcn_s_setprio(0);
   };
   auto consume = [&](int e, const Blk& bk, const float4 (&v)[U][NC]) {
+    if constexpr (CB && VQGNN_CB_CONS_PRIO != 0) __builtin_amdgcn_s_setprio(VQGNN_CB_CONS_PRIO);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const float w = __int_as_float(bk.cw[u]);
@@ -518,6 +524,7 @@ __device__ __forceinline__ void task_walk(const TaskArgs& a, int wv, int nwaves,
         head = false;
       }
     }
+    if constexpr (CB && VQGNN_CB_CONS_PRIO != 0) __builtin_amdgcn_s_setprio(0);
   };
 
   // wave-uniform (every lane holds the max): an SGPR loop, not an exec-masked one
