@@ -1442,6 +1442,9 @@ __device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
 #ifndef VQGNN_ASG_OUT_PRIO
 #define VQGNN_ASG_OUT_PRIO 0
 #endif
+#ifndef VQGNN_ASG_DEFER_STORES
+#define VQGNN_ASG_DEFER_STORES 0
+#endif
 
 __device__ __forceinline__ int flt_pos(int m) { return m ^ (((m >> 6) & 1) << 4); }
 
@@ -1729,6 +1732,21 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
     load_raw(r0, raw);
     if (codes) nid = batch_idx[r0];
   }
+  // (VQGNN_ASG_DEFER_STORES) a row's index / code stores are issued in the
+  // next iteration, after its row loads were waited for: gfx950 counts
+  // stores and loads in one in-order counter, so stores issued right before
+  // the loop's back edge made the wait for the prefetched row a wait for
+  // their write acknowledgements as well
+  bool st_do = false;
+  int st_idx = 0, st_row = 0;
+  int64_t st_node = 0;
+  auto flush_stores = [&]() {
+    if (st_do) {
+      if (idx_out) idx_out[(int64_t)b * B + st_row] = (int64_t)st_idx;
+      if (idx32) idx32[(int64_t)b * B + st_row] = st_idx;
+      if (codes) codes[st_node * ldc + b] = (int16_t)st_idx;
+    }
+  };
   for (int it = 0; it < n_iters; ++it) {
     const int row0 = part_begin + it * RPI + wave * 64;
     const bool live = row0 + lane < part_end;
@@ -1780,6 +1798,10 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
         bop[g] = __builtin_bit_cast(half8, uint4{bw[g][0], bw[g][1], bw[g][2], bw[g][3]});
     }
     if constexpr (kRowPrio != 0) __builtin_amdgcn_s_setprio(0);
+    if constexpr (VQGNN_ASG_DEFER_STORES != 0) {    // the previous iteration's outputs
+      flush_stores();
+      st_do = false;
+    }
     float best = INFINITY;
     int bidx = 0;
     bool ntie = !(sx < 65536.f);
@@ -2021,7 +2043,12 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
     // workgroup's list instead (resolved after the row loop)
     const bool near_tie = live && ntie;
     if constexpr (VQGNN_ASG_OUT_PRIO != 0) __builtin_amdgcn_s_setprio(VQGNN_ASG_OUT_PRIO);
-    if (live && !ntie) {
+    if constexpr (VQGNN_ASG_DEFER_STORES != 0) {
+      st_do = live && !ntie;
+      st_idx = bidx;
+      st_row = row0 + lane;
+      st_node = node;
+    } else if (live && !ntie) {
       if (idx_out) idx_out[(int64_t)b * B + row0 + lane] = (int64_t)bidx;
       if (idx32) idx32[(int64_t)b * B + row0 + lane] = bidx;
       if (codes) codes[node * ldc + b] = (int16_t)bidx;
@@ -2044,6 +2071,8 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
     }
     if constexpr (VQGNN_ASG_OUT_PRIO != 0) __builtin_amdgcn_s_setprio(0);
   }
+
+  if constexpr (VQGNN_ASG_DEFER_STORES != 0) flush_stores();   // the last iteration's outputs
 
   // ---- near-tie rows of this workgroup: one wave per row sweeps every
   // codeword in vq.py's arithmetic (BatchNorm apply, |x|^2 and |e|^2 summed
