@@ -1445,6 +1445,12 @@ __device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
 #ifndef VQGNN_ASG_DEFER_STORES
 #define VQGNN_ASG_DEFER_STORES 0
 #endif
+// dead waves leave the filter's row loop: arxiv assign 83.6-85.1 against
+// 85.9-88.0 us, arxiv_gat 205-210 against 214-220, ppi 498-502 against
+// 531-536 (profiles/r06y6_assign_tail_exit_ab.txt)
+#ifndef VQGNN_ASG_TAIL_EXIT
+#define VQGNN_ASG_TAIL_EXIT 1
+#endif
 
 __device__ __forceinline__ int flt_pos(int m) { return m ^ (((m >> 6) & 1) << 4); }
 
@@ -1749,6 +1755,12 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
   };
   for (int it = 0; it < n_iters; ++it) {
     const int row0 = part_begin + it * RPI + wave * 64;
+    // (VQGNN_ASG_TAIL_EXIT) a wave whose rows all lie past its part leaves
+    // the row loop: the part's last iteration is partial (arxiv: 172 of 512
+    // rows), and its dead waves would sweep clamped rows beside the live ones.
+    // Not where the chunk-inner loop restages behind workgroup barriers.
+    if constexpr (VQGNN_ASG_TAIL_EXIT != 0)
+      if ((CO || nchunks == 1) && row0 >= part_end) break;
     const bool live = row0 + lane < part_end;
     float sx;
     half8 bop[4];
