@@ -743,6 +743,12 @@ static size_t cb_lds_bytes(int kc, int chunk) {
 // BatchNorm bound |z| <= sqrt(count - 1) (EMA updates only run in training,
 // vq.py:176/241, with batch statistics): count * 2^shift * bound < 2^62.
 // The count column is in units of 1.
+// (timing probe, experiments builds: the fused assigns without their
+// final slab fold; results invalid)
+#ifndef VQGNN_ASG_NO_FLUSH
+#define VQGNN_ASG_NO_FLUSH 0
+#endif
+
 struct StatShift {
   int f, g;
 };
@@ -1361,8 +1367,10 @@ vq_assign_kernel(const float* __restrict__ X, int64_t ldx,
   if constexpr (FUSED) {   // fold into the single zeroed slab: integer, exact, order-free
     __syncthreads();
     unsigned long long* out = partial + (int64_t)b * M * (W + 1);
-    for (int i = tid; i < M * (W + 1); i += NT)
-      if (acc[i]) atomicAdd(out + i, acc[i]);
+    // (VQGNN_ASG_NO_FLUSH: a timing probe without this fold, results invalid)
+    if constexpr (VQGNN_ASG_NO_FLUSH == 0)
+      for (int i = tid; i < M * (W + 1); i += NT)
+        if (acc[i]) atomicAdd(out + i, acc[i]);
   }
 }
 
@@ -2156,8 +2164,10 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
   if constexpr (FUSED) {   // fold into the single zeroed slab: integer, exact, order-free
     __syncthreads();
     unsigned long long* out = partial + (int64_t)b * M * (W + 1);
-    for (int i = tid; i < M * (W + 1); i += NT)
-      if (acc[i]) atomicAdd(out + i, acc[i]);
+    // (VQGNN_ASG_NO_FLUSH: a timing probe without this fold, results invalid)
+    if constexpr (VQGNN_ASG_NO_FLUSH == 0)
+      for (int i = tid; i < M * (W + 1); i += NT)
+        if (acc[i]) atomicAdd(out + i, acc[i]);
   }
 }
 
