@@ -1444,6 +1444,9 @@ __device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
 #ifndef VQGNN_ASG_ROW_PRIO
 #define VQGNN_ASG_ROW_PRIO 1
 #endif
+#ifndef VQGNN_ASG_CO_PRIO
+#define VQGNN_ASG_CO_PRIO 0
+#endif
 #ifndef VQGNN_ASG_RES_PRIO
 #define VQGNN_ASG_RES_PRIO 0
 #endif
@@ -1561,8 +1564,9 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
                  BnFold fold, unsigned long long* __restrict__ co_state, int co_pass) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int NT = WV * 64;
-  constexpr int kFoldPrio = CO ? 1 : VQGNN_ASG_FOLD_PRIO;   // wave priorities (above)
-  constexpr int kRowPrio = CO ? 0 : VQGNN_ASG_ROW_PRIO;
+  constexpr bool kCoPrio = CO && VQGNN_ASG_CO_PRIO == 0;     // chunk-outer: fold 1, row 0
+  constexpr int kFoldPrio = kCoPrio ? 1 : VQGNN_ASG_FOLD_PRIO;   // wave priorities (above)
+  constexpr int kRowPrio = kCoPrio ? 0 : VQGNN_ASG_ROW_PRIO;
   const int W = WM == 2 ? 8 : (WM == 1 ? 4 : W_);          // compile-time in the row modes
   const int D = WM != 0 ? 4 : D_;
   const int F = nb * D;
