@@ -683,6 +683,14 @@ spmm_task_cb_kernel(TaskArgs a, int nunits) {
   // row M is zeros: the walk reads a code >= M (invalid input) there.
   // (NT < kCbThreads, an experiments-build workgroup shape: several rounds)
   const int npc = (a.cb_M + 1) * G;
+  // the first unit's plan words are requested before the image: their round
+  // trip overlaps the staging loads' instead of following the barrier
+  const int wave = threadIdx.x >> 6;
+  const int g = xcd_remap(blockIdx.x, gridDim.x);
+  const int stride = (int)gridDim.x * (NT / 64);
+  const int nnz = call_nnz(a);
+  int u0 = g * (NT / 64);
+  UnitInfo cur = unit_info<G>(a, __builtin_amdgcn_readfirstlane(u0 + wave), nnz);
 #pragma unroll
   for (int base = 0; base < kCbThreads * kCbStage; base += NT * kCbStage) {
     float4 v[kCbStage];
@@ -705,13 +713,7 @@ spmm_task_cb_kernel(TaskArgs a, int nunits) {
     }
   }
   __syncthreads();
-  const int wave = threadIdx.x >> 6;
-  const int g = xcd_remap(blockIdx.x, gridDim.x);
-  const int stride = (int)gridDim.x * (NT / 64);
-  const int nnz = call_nnz(a);
   // the next unit's plan words are read while this unit is walked
-  int u0 = g * (NT / 64);
-  UnitInfo cur = unit_info<G>(a, __builtin_amdgcn_readfirstlane(u0 + wave), nnz);
   for (; u0 < nunits; u0 += stride) {
     const int wv = __builtin_amdgcn_readfirstlane(u0 + wave);
     const UnitInfo nxt = unit_info<G>(a, wv + stride, nnz);
