@@ -1661,10 +1661,26 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
     s_kt[2][k] = kvv ? coef[(gk ? 5 * F : 4 * F) + c] : 0.f;
     s_kt[3][k] = gk ? grad_scale : 1.f;
   }
+  if constexpr (FUSED) {
+    for (int i = tid; i < M * (W + 1); i += NT) acc[i] = 0ull;
+  }
+  int* const flist = flags + (int64_t)wg * rows_per_part;
+  __syncthreads();
+  if (CO)                     // chunk-outer launch: this pass's chunk, once
+    stage_filter<NT>(E, ldw, W, co_pass * chunk, min(chunk, M - co_pass * chunk), chunk, lds,
+                     tid, &s_bigmin, ef);
+  else if (nchunks == 1)
+    stage_filter<NT>(E, ldw, W, 0, M, chunk, lds, tid, &s_bigmin, ef);
+
   const int part_begin = part * rows_per_part;
   const int part_end = min(B, part_begin + rows_per_part);
   constexpr int RPI = WV * 64;
   const int n_iters = part_end > part_begin ? (part_end - part_begin + RPI - 1) / RPI : 0;
+  // A-fragment byte offset of this lane: plane (q: 0 -> hi, 1 -> lo, 2 -> hi,
+  // 3 -> |e|^2 parts), codeword j of tile 0
+  const uint32_t a_lane = (uint32_t)(((q == 1) ? 1 : (q == 3 ? 2 : 0)) * cs + j) * 16u;
+  if (CO || nchunks == 1) __syncthreads();
+
   // the owner lane's raw row (k-slot order: features, then gradients)
   auto load_raw = [&](int rowi, float (&raw)[8]) {
     if constexpr (WM != 0) {
@@ -1685,33 +1701,6 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
       }
     }
   };
-  float raw[8];                                       // the next row, loaded ahead
-  // its node id for the code scatter too (a dependent load right before the
-  // store would stall the wave on a memory round trip every iteration)
-  int64_t nid = 0;
-  // the first row is requested before the codebook is staged: its round trip
-  // overlaps the staging loads' instead of following the two barriers
-  if (n_iters > 0) {
-    const int r0 = min(part_begin + wave * 64 + lane, part_end - 1);
-    load_raw(r0, raw);
-    if (codes) nid = batch_idx[r0];
-  }
-  if constexpr (FUSED) {
-    for (int i = tid; i < M * (W + 1); i += NT) acc[i] = 0ull;
-  }
-  int* const flist = flags + (int64_t)wg * rows_per_part;
-  __syncthreads();
-  if (CO)                     // chunk-outer launch: this pass's chunk, once
-    stage_filter<NT>(E, ldw, W, co_pass * chunk, min(chunk, M - co_pass * chunk), chunk, lds,
-                     tid, &s_bigmin, ef);
-  else if (nchunks == 1)
-    stage_filter<NT>(E, ldw, W, 0, M, chunk, lds, tid, &s_bigmin, ef);
-
-  // A-fragment byte offset of this lane: plane (q: 0 -> hi, 1 -> lo, 2 -> hi,
-  // 3 -> |e|^2 parts), codeword j of tile 0
-  const uint32_t a_lane = (uint32_t)(((q == 1) ? 1 : (q == 3 ? 2 : 0)) * cs + j) * 16u;
-  if (CO || nchunks == 1) __syncthreads();
-
   // the k-slot coefficients, wave-uniform: read once into scalar registers in
   // the row modes (an LDS table re-read per iteration costs 8 LDS reads)
   float kt[4][8];
@@ -1743,7 +1732,10 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
     return s;
   };
 
-
+  float raw[8];                                       // the next row, loaded ahead
+  // its node id for the code scatter too (a dependent load right before the
+  // store would stall the wave on a memory round trip every iteration)
+  int64_t nid = 0;
   // chunk-outer (CO: one launch per chunk, pass co_pass): the launch stages
   // its chunk once and runs every row against it, carrying each row's best
   // exact distance, index and near-tie flag to the next launch in co_state;
@@ -1753,6 +1745,11 @@ vq_filter_kernel(const float* __restrict__ X, int64_t ldx, const float* __restri
   // pass, not a pass loop: the loop kept 20 more VGPRs live across the row
   // loop -- 139 instead of 119 at 8 waves, spills at 16.)
   const bool co = CO && co_state != nullptr;
+  if (n_iters > 0) {
+    const int r0 = min(part_begin + wave * 64 + lane, part_end - 1);
+    load_raw(r0, raw);
+    if (codes) nid = batch_idx[r0];
+  }
   // (VQGNN_ASG_DEFER_STORES) a row's index / code stores are issued in the
   // next iteration, after its row loads were waited for: gfx950 counts
   // stores and loads in one in-order counter, so stores issued right before
